@@ -1,0 +1,207 @@
+/*
+ * t5gtts.h -- C ABI of the MI355X-native T5Gemma-TTS generate() engine (libt5gtts.so).
+ *
+ * This is the drop-in boundary for the reference's generate() hot path
+ * (tori29umai0123/T5Gemma-TTS @ 2025-12-26). The reference is pure Python, so
+ * there is no native FFI to mirror; each entry point replaces the Python/torch
+ * call sequence named beside it. The Python host mirror
+ * (t5gemma_tts_amd/engine.py: T5GemmaVoiceForConditionalGeneration.inference_tts,
+ * same signature as hf_export/modeling_t5gemma_voice.py:565-580) drives it via
+ * ctypes; INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions: plain pointers and sizes only (no torch types). "dev" pointers are
+ * device (HBM) addresses owned by the caller unless stated; `stream` is a
+ * hipStream_t passed as void*. All calls are stream-ordered and asynchronous
+ * unless documented as synchronous. Return 0 on success, negative T5G_E* on error
+ * (the Python shim maps them to ValueError / RuntimeError, like the reference's
+ * asserts at :581-594). One host thread per engine; no global state.
+ */
+#ifndef T5GTTS_H
+#define T5GTTS_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define T5G_OK 0
+#define T5G_EINVAL (-1)      /* bad shape / argument   -> ValueError  */
+#define T5G_EHIP (-2)        /* HIP runtime failure    -> RuntimeError */
+#define T5G_EUNSUPPORTED (-3)
+#define T5G_ENOMEM (-4)
+#define T5G_ECAPACITY (-5)   /* exceeds engine capacity (max_batch / max_text / max_audio) */
+
+#define T5G_MAX_LAYERS 64
+
+typedef struct t5g_engine t5g_engine;
+
+/* Shapes + sampler constants. Mirrors T5GemmaVoiceConfig
+ * (hf_export/configuration_t5gemma_voice.py:54-144) and the T5Gemma backbone
+ * config ([tf] configuration_t5gemma.py). */
+typedef struct {
+    int32_t hidden, intermediate, n_enc_layers, n_dec_layers;
+    int32_t n_heads, n_kv_heads, head_dim;
+    int32_t text_vocab, n_audio_tokens;
+    float attn_scale;      /* query_pre_attn_scalar ** -0.5 */
+    float softcap;         /* 0: sdpa numerics (no softcap); >0: eager + tanh softcap */
+    float rms_eps;
+    float normalizer;      /* bf16(sqrt(hidden)) */
+    int32_t sliding_window;
+    uint8_t enc_sliding[T5G_MAX_LAYERS]; /* 1 = "sliding_attention" layer */
+    uint8_t dec_sliding[T5G_MAX_LAYERS];
+    int32_t max_batch;     /* utterance rows per call */
+    int32_t max_text;      /* text tokens per row (encoder length capacity) */
+    int32_t max_audio;     /* decoder cache length per row: BOS + prompt + generated */
+    int32_t max_gen;       /* generated-token capacity per row */
+    /* sampler / stop constants (:590-592, :727, :773-777) */
+    int32_t eos;           /* eog_inference */
+    int32_t eos_guard;     /* encodec_sr // 5 */
+    float budget_extra;    /* int(encodec_sr) * extra_cutoff */
+    int32_t text_guard;    /* text_guard_frames_per_token */
+    float progress_scale;
+} t5g_config;
+
+/* Device pointers to bf16 weights. "packed" = P16 layout built by t5g_pack_weight. */
+typedef struct {
+    const void* qkv;       /* packed [q_dim + 2 kv_dim][hidden]: q_proj | k_proj | v_proj rows */
+    const void* o;         /* packed [hidden][q_dim] */
+    const void* gate_up;   /* packed [2 inter][hidden]: 16-row groups gate,up,gate,up,... */
+    const void* down;      /* packed [hidden][inter] */
+    const void* cross_q;   /* decoder only: packed [q_dim][hidden] */
+    const void* cross_kv;  /* decoder only: packed [2 kv_dim][hidden]: k_proj | v_proj */
+    const void* cross_o;   /* decoder only: packed [hidden][q_dim] */
+    const void* norms[6];  /* bf16 [hidden]: pre_self, post_self, pre_cross, post_cross, pre_ff, post_ff */
+} t5g_layer_weights;
+
+typedef struct {
+    const void* enc_embed;       /* bf16 [text_vocab][hidden] row-major */
+    const void* audio_embed;     /* bf16 [n_audio_tokens][hidden] row-major */
+    const void* enc_final_norm;  /* bf16 [hidden] */
+    const void* dec_final_norm;
+    const void* head1;           /* packed [hidden][hidden]     predict_layer.0.0 */
+    const void* head1_bias;      /* bf16 [hidden] */
+    const void* head2;           /* packed [n_audio_tokens][hidden] predict_layer.0.2 */
+    const void* head2_bias;      /* bf16 [n_audio_tokens] */
+    const float* inv_freq;       /* fp32 [head_dim/2] RoPE inverse frequencies */
+    const t5g_layer_weights* enc_layers;  /* host array [n_enc_layers] */
+    const t5g_layer_weights* dec_layers;  /* host array [n_dec_layers] */
+} t5g_weights;
+
+/* Per-utterance sampler parameters (topk_sampling args, :744-750). */
+typedef struct {
+    int32_t top_k;           /* <= 0 disabled */
+    int32_t top_k_list_len;  /* > 0: per-step list (top_k given as a list, :722-723) */
+    int32_t top_k_list_off;
+    float top_p, min_p, temperature;
+    int32_t stop_repetition;
+    int32_t n_silence;
+    int32_t silence_off;
+    int32_t eos_disabled;    /* throughput mode: EOS logit -> -inf (never accepted before the budget) */
+    uint32_t seed_lo, seed_hi;  /* production noise (Philox4x32-10) */
+} t5g_sampler_row;
+
+/* Per-utterance AR state (the locals of inference_tts, :696-700, :717). */
+typedef struct {
+    int32_t cur_num_gen;
+    int32_t current_length;
+    int32_t prompt_offset;
+    int32_t target_total;    /* < 0: none */
+    int32_t est_total;
+    int32_t prev_token;
+    int32_t consec_silence;
+    int32_t first_input_len;
+    int32_t done;
+    int32_t ambiguous_steps;
+    int32_t last_token;
+    float next_pos;
+} t5g_sampler_state;
+
+/* --- weights ------------------------------------------------------------- */
+/* Bytes of the P16-packed image of an [N][K] bf16 matrix (K % 32 == 0). */
+int64_t t5g_packed_bytes(int32_t N, int32_t K);
+/* Pack src_dev [N][K] (row stride ld elements) into dst_dev (t5g_packed_bytes(N,K) bytes). */
+int t5g_pack_weight(const void* src_dev, int32_t N, int32_t K, int64_t ld, void* dst_dev, void* stream);
+
+/* --- engine lifetime --------------------------------------------------------- */
+/* Replaces T5GemmaVoiceForConditionalGeneration.__init__ (:343-479) for the
+ * inference path: binds caller-owned device weights, allocates the KV arena and
+ * scratch in HBM (sized by cfg->max_*). */
+int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5g_engine** out);
+int t5g_engine_destroy(t5g_engine* e);
+int64_t t5g_engine_workspace_bytes(const t5g_engine* e);
+
+/* --- generate() phases --------------------------------------------------------
+ * Token batches are PACKED: ntok tokens of B rows, with per-token row index
+ * tok_row[ntok] and in-row position tok_t[ntok] (device int32). */
+
+/* Encoder (:596-615 -> [tf] T5GemmaEncoder.forward :648-702) over text ids with
+ * float PM positions pos[ntok] (:516-531), then every decoder layer's
+ * PM-RoPE'd cross-attention K/V (:198-230) into the engine's cross cache.
+ * text_len_dev[B] = x_lens. */
+int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t* ids_dev, const int32_t* tok_row_dev,
+               const int32_t* tok_t_dev, const float* pos_dev, const int32_t* text_len_dev, void* stream);
+
+/* Decoder prefill (:630-694): audio ids (BOS + prompt) with float PM positions
+ * (:669-681); fills the self KV cache; writes the logits of each row's last token
+ * (last_index_dev[B] = packed index) into the engine logits buffer.
+ * kv_len_dev[B] = BOS + prompt length per row. */
+int t5g_prefill(t5g_engine* e, int32_t B, int32_t ntok, const int32_t* ids_dev, const int32_t* tok_row_dev,
+                const int32_t* tok_t_dev, const float* pos_dev, const int32_t* kv_len_dev,
+                const int32_t* last_index_dev, void* stream);
+
+/* Sampler setup (host arrays, copied): rows[B], init state[B], shared top-k list
+ * and silence-token buffers. noise_dev: NULL for on-device Philox noise, else
+ * bf16 [B][noise_steps][n_audio_tokens] -- the exact exponential draws of
+ * torch.multinomial (parity mode). */
+int t5g_sampler_setup(t5g_engine* e, int32_t B, const t5g_sampler_row* rows, const t5g_sampler_state* init,
+                      const int32_t* top_k_list, int32_t n_top_k_list, const int32_t* silence, int32_t n_silence,
+                      const void* noise_dev, int32_t noise_steps, void* stream);
+
+/* n_steps iterations of the AR loop (:788-848): sample the current logits
+ * (on-device stop rules), then run the single-token decoder step + predict head
+ * for every row that is not done. use_graph != 0 replays a captured hipGraph of
+ * one iteration. Asynchronous. */
+int t5g_decode(t5g_engine* e, int32_t n_steps, int32_t use_graph, void* stream);
+
+/* Synchronous readback: state[B] and tokens [B][max_gen] (host buffers). */
+int t5g_read_state(t5g_engine* e, t5g_sampler_state* state_out, int32_t B, void* stream);
+int t5g_read_tokens(t5g_engine* e, int32_t* tokens_out, int32_t B, void* stream);
+/* Host write of one row's state (parity-mode correction of an ambiguous step). */
+int t5g_write_state(t5g_engine* e, const t5g_sampler_state* state, int32_t row, int32_t token_slot,
+                    int32_t token, void* stream);
+
+/* Parity-mode pieces of one AR iteration: sample only (flags readable), then
+ * the decoder step + head only. t5g_read_flags: bit0 = ambiguous top-p tie cut,
+ * bit1 = argmax was EOS (synchronous). */
+int t5g_step_only(t5g_engine* e, void* stream);
+int t5g_read_flags(t5g_engine* e, int32_t* flags_out, int32_t B, void* stream);
+/* Host re-run of one sampler step with torch.sort's exact std::sort tie order
+ * (resolves ambiguous steps; see csrc/host_sampler.cpp). Pure host function. */
+int t5g_host_sample(const uint16_t* logits_bf16, int32_t V, const t5g_sampler_row* row,
+                    const int32_t* top_k_list, const int32_t* silence, const t5g_sampler_state* state_in,
+                    const uint16_t* noise_bf16, int32_t eos, int32_t eos_guard, float budget_extra,
+                    int32_t text_guard, float progress_scale, int32_t max_gen,
+                    t5g_sampler_state* state_out, int32_t* token_out);
+
+/* Device pointer of the logits buffer bf16 [max_batch][logits_ld] (debug / parity). */
+void* t5g_logits_ptr(t5g_engine* e, int32_t* logits_ld);
+/* Stream-ordered device copy of the first B logits rows into dst_dev [B][logits_ld]. */
+int t5g_copy_logits(t5g_engine* e, void* dst_dev, int32_t B, void* stream);
+
+/* --- single-op entry points (parity tests, kernel benchmarks) ------------------ */
+/* One sampler step on caller logits (bf16 [B][ld]) using the engine's sampler state. */
+int t5g_sample_only(t5g_engine* e, int32_t B, const void* logits_dev, int32_t ld, void* stream);
+/* Y = X . W^T on a packed W; epi: 0 bf16, 1 +bias bf16, 2 +bias GELU(erf) bf16, 3 GeGLU(tanh), 4 fp32 slabs */
+int t5g_gemm(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K, int32_t splits,
+             const void* bias_dev, void* Y_dev, int32_t ldy, int32_t epi, void* stream);
+/* Time `iters` launches of the decode step's dominant GEMM shape with hipEvents on
+ * `stream`; returns average microseconds per launch in *avg_us. */
+int t5g_time_gemm(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K,
+                  int32_t splits, void* Y_dev, int32_t ldy, int32_t epi, int32_t iters, void* stream,
+                  float* avg_us);
+int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, float* avg_us);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* T5GTTS_H */

@@ -1,0 +1,119 @@
+"""ctypes binding of libt5gtts.so (C ABI declared in include/t5gtts.h).
+
+Fails loudly: there is no fallback path. If the library is missing or cannot be
+loaded, every engine entry point raises ``RuntimeError`` -- the product never
+computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("T5G_LIB", os.path.join(_PKG, "lib", "libt5gtts.so"))
+MAX_LAYERS = 64
+
+T5G_ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "EUNSUPPORTED", -4: "ENOMEM", -5: "ECAPACITY"}
+
+
+class T5GError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc == 0:
+        return
+    name = T5G_ERRORS.get(rc, str(rc))
+    if rc in (-1, -5):
+        raise ValueError(f"{what}: {name}")
+    raise T5GError(f"{what}: {name}")
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("hidden", C.c_int32), ("intermediate", C.c_int32), ("n_enc_layers", C.c_int32),
+        ("n_dec_layers", C.c_int32), ("n_heads", C.c_int32), ("n_kv_heads", C.c_int32),
+        ("head_dim", C.c_int32), ("text_vocab", C.c_int32), ("n_audio_tokens", C.c_int32),
+        ("attn_scale", C.c_float), ("softcap", C.c_float), ("rms_eps", C.c_float),
+        ("normalizer", C.c_float), ("sliding_window", C.c_int32),
+        ("enc_sliding", C.c_uint8 * MAX_LAYERS), ("dec_sliding", C.c_uint8 * MAX_LAYERS),
+        ("max_batch", C.c_int32), ("max_text", C.c_int32), ("max_audio", C.c_int32),
+        ("max_gen", C.c_int32), ("eos", C.c_int32), ("eos_guard", C.c_int32),
+        ("budget_extra", C.c_float), ("text_guard", C.c_int32), ("progress_scale", C.c_float),
+    ]
+
+
+class LayerWeights(C.Structure):
+    _fields_ = [("qkv", C.c_void_p), ("o", C.c_void_p), ("gate_up", C.c_void_p), ("down", C.c_void_p),
+                ("cross_q", C.c_void_p), ("cross_kv", C.c_void_p), ("cross_o", C.c_void_p),
+                ("norms", C.c_void_p * 6)]
+
+
+class Weights(C.Structure):
+    _fields_ = [("enc_embed", C.c_void_p), ("audio_embed", C.c_void_p), ("enc_final_norm", C.c_void_p),
+                ("dec_final_norm", C.c_void_p), ("head1", C.c_void_p), ("head1_bias", C.c_void_p),
+                ("head2", C.c_void_p), ("head2_bias", C.c_void_p), ("inv_freq", C.c_void_p),
+                ("enc_layers", C.POINTER(LayerWeights)), ("dec_layers", C.POINTER(LayerWeights))]
+
+
+class SamplerRow(C.Structure):
+    _fields_ = [("top_k", C.c_int32), ("top_k_list_len", C.c_int32), ("top_k_list_off", C.c_int32),
+                ("top_p", C.c_float), ("min_p", C.c_float), ("temperature", C.c_float),
+                ("stop_repetition", C.c_int32), ("n_silence", C.c_int32), ("silence_off", C.c_int32),
+                ("eos_disabled", C.c_int32), ("seed_lo", C.c_uint32), ("seed_hi", C.c_uint32)]
+
+
+class SamplerState(C.Structure):
+    _fields_ = [("cur_num_gen", C.c_int32), ("current_length", C.c_int32), ("prompt_offset", C.c_int32),
+                ("target_total", C.c_int32), ("est_total", C.c_int32), ("prev_token", C.c_int32),
+                ("consec_silence", C.c_int32), ("first_input_len", C.c_int32), ("done", C.c_int32),
+                ("ambiguous_steps", C.c_int32), ("last_token", C.c_int32), ("next_pos", C.c_float)]
+
+
+# name -> (restype, argtypes); exactly the functions include/t5gtts.h declares
+_P, _I, _L, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
+SIGNATURES = {
+    "t5g_packed_bytes": (_L, [_I, _I]),
+    "t5g_pack_weight": (C.c_int, [_P, _I, _I, _L, _P, _P]),
+    "t5g_engine_create": (C.c_int, [C.POINTER(Config), C.POINTER(Weights), C.POINTER(_P)]),
+    "t5g_engine_destroy": (C.c_int, [_P]),
+    "t5g_engine_workspace_bytes": (_L, [_P]),
+    "t5g_encode": (C.c_int, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "t5g_prefill": (C.c_int, [_P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "t5g_sampler_setup": (C.c_int, [_P, _I, C.POINTER(SamplerRow), C.POINTER(SamplerState), _P, _I, _P, _I,
+                                    _P, _I, _P]),
+    "t5g_decode": (C.c_int, [_P, _I, _I, _P]),
+    "t5g_read_state": (C.c_int, [_P, C.POINTER(SamplerState), _I, _P]),
+    "t5g_read_tokens": (C.c_int, [_P, _P, _I, _P]),
+    "t5g_write_state": (C.c_int, [_P, C.POINTER(SamplerState), _I, _I, _I, _P]),
+    "t5g_step_only": (C.c_int, [_P, _P]),
+    "t5g_read_flags": (C.c_int, [_P, _P, _I, _P]),
+    "t5g_host_sample": (C.c_int, [_P, _I, C.POINTER(SamplerRow), _P, _P, C.POINTER(SamplerState), _P, _I, _I,
+                                  _F, _I, _F, _I, C.POINTER(SamplerState), C.POINTER(_I)]),
+    "t5g_logits_ptr": (_P, [_P, C.POINTER(_I)]),
+    "t5g_copy_logits": (C.c_int, [_P, _P, _I, _P]),
+    "t5g_sample_only": (C.c_int, [_P, _I, _P, _I, _P]),
+    "t5g_gemm": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _I, _I, _P]),
+    "t5g_time_gemm": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _I, _I, _I, _P, C.POINTER(_F)]),
+    "t5g_time_decode_step": (C.c_int, [_P, _I, _P, C.POINTER(_F)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libt5gtts.so once (raises RuntimeError when it is absent)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libt5gtts.so not built ({LIB_PATH}); run __graft_entry__.build() -- "
+                               "there is no CPU fallback")
+        # torch must own the HIP runtime first (same soname libamdhip64.so.7)
+        import torch  # noqa: F401
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib

@@ -1,0 +1,70 @@
+"""Build libt5gtts.so (HIP C++ for gfx950) in-tree with hipcc.
+
+``python t5gemma-tts_amd/build.py`` or ``t5gemma_tts_amd.build.build()``.
+Objects go to ``t5gemma-tts_amd/build/``, the library to ``t5gemma-tts_amd/lib/``
+(git-ignored, shipped to the GPU box by gpurun's snapshot).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OBJ = os.path.join(PKG, "build")
+LIB = os.path.join(PKG, "lib", "libt5gtts.so")
+SOURCES = ["gemm.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "host_sampler.cpp"]
+HEADERS = ["common.h", "t5g_kernels.h"]
+ARCH = os.environ.get("T5G_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+         "-I", os.path.join(REPO, "include")]
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _newest_dep() -> float:
+    deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "t5gtts.h")]
+    return max(os.path.getmtime(p) for p in deps if os.path.exists(p))
+
+
+def _compile(src: str, force: bool) -> str:
+    s = os.path.join(CSRC, src)
+    o = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+    if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), _newest_dep()):
+        return o
+    cmd = [_hipcc()] + FLAGS + ["-c", s, "-o", o]
+    if src.endswith(".cpp"):
+        cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-I",
+               os.path.join(REPO, "include"), "-c", s, "-o", o]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
+    return o
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+        if verbose:
+            print(f"[t5gtts] built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

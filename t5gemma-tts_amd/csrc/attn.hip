@@ -1,0 +1,299 @@
+// PM-RoPE + KV-cache store, and GQA attention (decode / prefill / encoder / cross).
+//
+// RoPE follows [tf] T5GemmaRotaryEmbedding + apply_rotary_pos_emb with FLOAT
+// progress positions (hf_export/modeling_t5gemma_voice.py:516-531, 669-681,
+// 817-832): angle = inv_freq[i] * pos in fp32, cos/sin rounded to bf16, then
+// out = bf16(bf16(x*cos) + bf16(rotate_half(x)*sin)) -- three bf16 tensor ops.
+//
+// Attention: one block per (query, kv head, key split); the G = Hq/Hkv query
+// heads of a GQA group share every K/V row read (GQA reuse). K/V cache rows are
+// read with 16-byte lanes, LPK = D/8 lanes per key (32 at D = 256: two keys per
+// wave instruction, a contiguous 1 KiB). Numerics mirror torch's CPU SDPA flash
+// kernel (fp32 scores, fp32 exp and sum, exp values rounded to bf16 before P.V,
+// O / sum rounded once); ``eager`` mirrors eager_attention_forward (bf16 scores,
+// tanh softcap, bf16-rounded normalised probabilities).
+#include "common.h"
+#include "t5g_kernels.h"
+
+namespace t5g {
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float cs[];  // [D/2] cos, [D/2] sin
+    const int m = blockIdx.x;
+    const int D = a.D, H2 = D / 2;
+    const int row = a.tok_row ? a.tok_row[m] : m;
+    const float pos = a.pos[a.tok_row ? m : row];
+    for (int i = threadIdx.x; i < H2; i += blockDim.x) {
+        float ang = a.inv_freq[i] * pos;
+        cs[i] = rbf(cosf(ang));
+        cs[H2 + i] = rbf(sinf(ang));
+    }
+    __syncthreads();
+    const bf16_t* x = a.X ? a.X + (long)m * a.ldx : nullptr;
+    int slot = 0;
+    if (a.nk + a.nv > 0) slot = a.tok_t ? a.tok_t[m] : a.kv_len[row] - 1;
+    const int nh = a.nq + a.nk + a.nv;
+    for (int idx = threadIdx.x; idx < nh * H2; idx += blockDim.x) {
+        const int h = idx / H2, i = idx % H2;
+        float x1, x2;
+        if (a.Xpart) {
+            x1 = 0.f;
+            x2 = 0.f;
+            for (int s = 0; s < a.nsplit; ++s) {
+                const float* ps = a.Xpart + ((long)s * a.M + m) * a.ldx + h * D;
+                x1 += ps[i];
+                x2 += ps[i + H2];
+            }
+            x1 = rbf(x1);
+            x2 = rbf(x2);
+        } else {
+            const bf16_t* xh = x + h * D;
+            x1 = bf2f(xh[i]);
+            x2 = bf2f(xh[i + H2]);
+        }
+        bool isq = h < a.nq, isk = !isq && h < a.nq + a.nk;
+        bool rope = (isq && a.rope_q) || (isk && a.rope_k);
+        float o1 = x1, o2 = x2;
+        if (rope) {
+            float c = cs[i], s = cs[H2 + i];
+            o1 = rbf(rbf(x1 * c) + rbf(-x2 * s));
+            o2 = rbf(rbf(x2 * c) + rbf(x1 * s));
+        }
+        bf16_t* dst;
+        if (isq) {
+            dst = a.Qout + (long)m * a.ldq + h * D;
+        } else if (isk) {
+            dst = a.Kc + row * a.c_bstride + (h - a.nq) * a.c_hstride + (long)slot * D;
+        } else {
+            dst = a.Vc + row * a.c_bstride + (h - a.nq - a.nk) * a.c_hstride + (long)slot * D;
+        }
+        dst[i] = f2bf(o1);
+        dst[i + H2] = f2bf(o2);
+    }
+}
+
+int rope_store(const RopeArgs& a, hipStream_t st) {
+    if (a.M <= 0) return 0;
+    if (a.nq && a.Qout == a.X && a.ldq != a.ldx) return -1;
+    if (!a.X && !a.Xpart) return -1;
+    // in-place q rope is safe: each (h, i) pair is read and written by one thread
+    hipLaunchKernelGGL(rope_store_kernel, dim3((unsigned)a.M), dim3(256), a.D * sizeof(float), st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------------------
+template <int D, int G, bool EAGER>
+__global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
+    constexpr int LPK = D / 8;        // lanes per key row
+    constexpr int KPW = 64 / LPK;     // keys per wave instruction
+    constexpr int KPB = KPW * 4;      // keys per block iteration
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // [G][chunk] scores, then probs
+    __shared__ float red[32];
+    __shared__ f32x4 ored[4][G][64][2];
+
+    const int qi = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int kg = lane / LPK, dl = lane % LPK;
+    const int row = a.q_row ? a.q_row[qi] : qi;
+    const int len = a.kv_len[row];
+    const int t = a.q_pos ? a.q_pos[qi] : len - 1;
+    int lo = 0, hi = len;
+    if (a.causal) {
+        hi = min(t + 1, len);
+        if (a.window > 0) lo = max(0, t - a.window + 1);
+    } else if (a.window > 0) {
+        lo = max(0, t - a.window);
+        hi = min(len, t + a.window + 1);
+    }
+    const int c0 = lo + sp * a.chunk;
+    const int c1 = min(hi, c0 + a.chunk);
+    const int n = c1 - c0;
+
+    float* part = a.part ? a.part + (((long)qi * a.Hkv + kvh) * a.nsplit + sp) * (G * (D + 2)) : nullptr;
+    if (n <= 0) {
+        if (a.nsplit > 1 && threadIdx.x < G) {
+            part[threadIdx.x * (D + 2)] = -INFINITY;
+            part[threadIdx.x * (D + 2) + 1] = 0.f;
+        }
+        return;
+    }
+    // q fragment: 8 dims per lane per head
+    float q[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        u32x4 w = *(const u32x4*)(a.Q + (long)qi * a.ldq + (kvh * G + g) * D + 8 * dl);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            q[g][2 * j] = bf_lo(w[j]);
+            q[g][2 * j + 1] = bf_hi(w[j]);
+        }
+    }
+    const bf16_t* Kb = a.K + row * a.kv_bstride + kvh * a.kv_hstride;
+    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
+
+    // ---- scores
+    for (int j0 = c0; j0 < c1; j0 += KPB) {
+        const int j = j0 + wave * KPW + kg;
+        float s[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = 0.f;
+        if (j < c1) {
+            u32x4 w = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                float k0 = bf_lo(w[jj]), k1 = bf_hi(w[jj]);
+#pragma unroll
+                for (int g = 0; g < G; ++g) s[g] += q[g][2 * jj] * k0 + q[g][2 * jj + 1] * k1;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+#pragma unroll
+            for (int o = LPK / 2; o > 0; o >>= 1) s[g] += __shfl_xor(s[g], o, 64);
+        }
+        if (dl == 0 && j < c1) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                float v;
+                if constexpr (EAGER) {
+                    v = rbf(rbf(s[g]) * a.scale);
+                    if (a.softcap > 0.f) v = rbf(rbf(tanhf(rbf(v / a.softcap))) * a.softcap);
+                } else {
+                    v = s[g] * a.scale;
+                }
+                sm[g * a.chunk + (j - c0)] = v;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- softmax statistics
+    float mx[G], sum[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        float lm = -INFINITY;
+        for (int i = threadIdx.x; i < n; i += 256) lm = fmaxf(lm, sm[g * a.chunk + i]);
+        mx[g] = block_max(lm, red);
+        float ls = 0.f;
+        for (int i = threadIdx.x; i < n; i += 256) ls += expf(sm[g * a.chunk + i] - mx[g]);
+        sum[g] = block_sum(ls, red);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const float inv = 1.0f / sum[g];
+        for (int i = threadIdx.x; i < n; i += 256) {
+            float e = expf(sm[g * a.chunk + i] - mx[g]);
+            sm[g * a.chunk + i] = EAGER ? rbf(e * inv) : rbf(e);
+        }
+    }
+    __syncthreads();
+    // ---- P.V: lane owns dims [8*dl, 8*dl+8) of key group kg
+    float o[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
+    for (int j0 = c0; j0 < c1; j0 += KPB) {
+        const int j = j0 + wave * KPW + kg;
+        if (j < c1) {
+            u32x4 w = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                float p = sm[g * a.chunk + (j - c0)];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    o[g][2 * jj] += p * bf_lo(w[jj]);
+                    o[g][2 * jj + 1] += p * bf_hi(w[jj]);
+                }
+            }
+        }
+    }
+    // reduce over key groups within the wave (lanes differing in bits >= log2(LPK))
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+#pragma unroll
+            for (int off = LPK; off < 64; off <<= 1) o[g][jj] += __shfl_xor(o[g][jj], off, 64);
+        }
+    if (kg == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            ored[wave][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
+            ored[wave][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
+        }
+    }
+    __syncthreads();
+    // final: thread t handles (g, dl) pairs
+    for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
+        const int g = idx / LPK, d8 = idx % LPK;
+        f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
+        f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
+        float v[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+        if (a.nsplit > 1) {
+            float* pg = part + g * (D + 2);
+            if (d8 == 0) {
+                pg[0] = mx[g];
+                pg[1] = sum[g];
+            }
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) pg[2 + 8 * d8 + jj] = v[jj];
+        } else {
+            const float inv = EAGER ? 1.0f : 1.0f / sum[g];
+            u32x4 w;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) w[jj] = pack2(v[2 * jj] * inv, v[2 * jj + 1] * inv);
+            *(u32x4*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 8 * d8) = w;
+        }
+    }
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a) {
+    const int qi = blockIdx.x, kvh = blockIdx.y;
+    const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2));
+    for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+        const int g = idx / D, d = idx % D;
+        float M = -INFINITY;
+        for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, base[(long)s * G * (D + 2) + g * (D + 2)]);
+        float L = 0.f, O = 0.f;
+        for (int s = 0; s < a.nsplit; ++s) {
+            const float* p = base + (long)s * G * (D + 2) + g * (D + 2);
+            if (p[0] == -INFINITY) continue;
+            float f = expf(p[0] - M);
+            L += f * p[1];
+            O += f * p[2 + d];
+        }
+        a.O[(long)qi * a.ldo + (kvh * G + g) * D + d] = f2bf(O * (1.0f / L));
+    }
+}
+
+template <int D, int G>
+static int launch_attn(const AttnArgs& a, hipStream_t st) {
+    dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
+    size_t shm = (size_t)G * a.chunk * sizeof(float);
+    if (a.eager)
+        hipLaunchKernelGGL((attn_kernel<D, G, true>), grid, dim3(256), shm, st, a);
+    else
+        hipLaunchKernelGGL((attn_kernel<D, G, false>), grid, dim3(256), shm, st, a);
+    if (a.nsplit > 1)
+        hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv), dim3(256), 0,
+                           st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int attention(const AttnArgs& a, hipStream_t st) {
+    if (a.Mq <= 0) return 0;
+    if (a.nsplit < 1 || a.chunk < 1) return -1;
+    if (a.eager && a.nsplit != 1) return -1;       // eager normalises over the full row
+    if (a.nsplit > 1 && !a.part) return -1;
+    if ((size_t)a.G * a.chunk * sizeof(float) > 96 * 1024) return -1;
+    if (a.D == 256 && a.G == 2) return launch_attn<256, 2>(a, st);
+    if (a.D == 64 && a.G == 2) return launch_attn<64, 2>(a, st);
+    if (a.D == 128 && a.G == 2) return launch_attn<128, 2>(a, st);
+    if (a.D == 256 && a.G == 1) return launch_attn<256, 1>(a, st);
+    return -3;
+}
+
+}  // namespace t5g

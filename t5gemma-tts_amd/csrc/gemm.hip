@@ -1,0 +1,229 @@
+// Weight-streaming bf16 GEMM on v_mfma_f32_16x16x32_bf16 for the T5Gemma-TTS engine.
+//
+// Y[M][N] = X[M][K] . W[N][K]^T  (nn.Linear layout), fp32 accumulation, one
+// rounding to bf16 in the epilogue (the reference's CPU bf16 F.linear rounds once).
+//
+// Packed weight layout "P16" (built once at load time by t5g_pack_p16):
+//   fragment (g, kb) = 16 rows x 32 k = 1 KiB, stored in the exact lane order of the
+//   MFMA A operand: lane l holds W[g*16 + (l&15)][kb*32 + 8*(l>>4) + 0..7].
+//   Fragments are g-major, so one row group's K stream is contiguous and a wave
+//   reads each fragment with ONE fully coalesced 1 KiB global_load_dwordx4.
+//   NG (row groups) is padded to a multiple of 4 with zero rows.
+//
+// Activations are the MFMA B operand (lane l: X[m = l&15][k = 8*(l>>4) + 0..7]),
+// so the batch rides in the 16 MFMA columns: at decode (M <= 16) one MFMA per
+// 1 KiB of weights -- VALU stays idle, the kernel is a pure HBM stream.
+//
+// Block = 4 waves. WPG waves share one row group and split its K range
+// (WPG = 4: decode, 1 row group / block; WPG = 1: prefill, 4 row groups / block
+// reading the same X fragments through L1). blockIdx.y splits K across blocks
+// (fp32 partial slabs reduced by the consumer kernel, in fixed order).
+#include "common.h"
+#include "t5g_kernels.h"
+
+namespace t5g {
+
+__global__ void pack_p16_kernel(const bf16_t* __restrict__ src, int N, int K, long ld,
+                                bf16_t* __restrict__ dst, int KB, long nfrag) {
+    long frag = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (frag >= nfrag) return;
+    int lane = threadIdx.x & 63;
+    long g = frag / KB;
+    int kb = (int)(frag % KB);
+    long row = g * 16 + (lane & 15);
+    int k0 = kb * 32 + 8 * (lane >> 4);
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (row < N && k0 < K) v = *(const u32x4*)(src + row * ld + k0);
+    *(u32x4*)(dst + (frag * 64 + lane) * 8) = v;
+}
+
+template <int MT>
+__device__ __forceinline__ void load_x(const bf16_t* __restrict__ X, int ldx, int M, int m0, int kb,
+                                       int lane, bf16x8_s (&xf)[MT]) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        int m = m0 + mt * 16 + (lane & 15);
+        if (m < M) {
+            xf[mt] = *(const bf16x8_s*)(X + (long)m * ldx + kb * 32 + 8 * (lane >> 4));
+        } else {
+            xf[mt] = (bf16x8_s){0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_b, a),
+                                                   __builtin_bit_cast(bf16x8_b, b), c, 0, 0, 0);
+}
+
+template <int MT, int WPG, int EPI>
+__global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
+    constexpr int RG = 4 / WPG;  // row groups per block
+    constexpr int UN = 4;        // k-steps in flight per wave
+    __shared__ f32x4 red[4][MT][64];
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = blockIdx.x * RG + wave / WPG;
+    const int ks = wave % WPG;
+    const int m0 = blockIdx.z * 16 * MT;
+    const int per = (a.KB + a.splits - 1) / a.splits;
+    const int kb_lo = blockIdx.y * per;
+    const int kb_hi = min(a.KB, kb_lo + per);
+
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const bf16x8_s* wp = (const bf16x8_s*)a.W + ((long)g * a.KB) * 64 + lane;
+    int kb = kb_lo + ks;
+    for (; kb + (UN - 1) * WPG < kb_hi; kb += UN * WPG) {
+        bf16x8_s wf[UN];
+        bf16x8_s xf[UN][MT];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) wf[u] = __builtin_nontemporal_load(wp + (long)(kb + u * WPG) * 64);
+#pragma unroll
+        for (int u = 0; u < UN; ++u) load_x<MT>(a.X, a.ldx, a.M, m0, kb + u * WPG, lane, xf[u]);
+#pragma unroll
+        for (int u = 0; u < UN; ++u)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(wf[u], xf[u][mt], acc[mt]);
+    }
+    for (; kb < kb_hi; kb += WPG) {
+        bf16x8_s wf = __builtin_nontemporal_load(wp + (long)kb * 64);
+        bf16x8_s xf[MT];
+        load_x<MT>(a.X, a.ldx, a.M, m0, kb, lane, xf);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(wf, xf[mt], acc[mt]);
+    }
+
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[mt];
+    __syncthreads();
+
+    constexpr int OG = (EPI == EPI_GEGLU) ? RG / 2 : RG;  // output groups per block
+    if (wave >= OG) return;
+    const int og = wave;
+    const int n_out = (EPI == EPI_GEGLU) ? a.N / 2 : a.N;
+    const int gout = blockIdx.x * OG + og;
+    const int n0 = gout * 16 + 4 * (lane >> 4);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int m = m0 + mt * 16 + (lane & 15);
+        if (m >= a.M) continue;
+        float v[4];
+        if constexpr (EPI == EPI_GEGLU) {
+            f32x4 gs = {0.f, 0.f, 0.f, 0.f}, us = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < WPG; ++s) {
+                gs += red[(2 * og) * WPG + s][mt][lane];
+                us += red[(2 * og + 1) * WPG + s][mt][lane];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float gg = rbf(gs[r]);
+                float act = rbf(gelu_tanh(gg));
+                float uu = rbf(us[r]);
+                v[r] = act * uu;
+            }
+        } else {
+            f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < WPG; ++s) s4 += red[og * WPG + s][mt][lane];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = s4[r];
+        }
+        if constexpr (EPI == EPI_F32) {
+            float* y = (float*)a.Y + ((long)blockIdx.y * a.M + m) * a.ldy;
+            if (n0 + 3 < n_out) {
+                *(f32x4*)(y + n0) = (f32x4){v[0], v[1], v[2], v[3]};
+            } else {
+                for (int r = 0; r < 4; ++r)
+                    if (n0 + r < n_out) y[n0 + r] = v[r];
+            }
+        } else {
+            bf16_t o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float x = v[r];
+                const int n = n0 + r;
+                if constexpr (EPI == EPI_BIAS_BF16 || EPI == EPI_BIAS_GELU) {
+                    if (n < n_out) x = x + bf2f(a.bias[n]);
+                }
+                if constexpr (EPI == EPI_BIAS_GELU) x = gelu_erf(rbf(x));
+                o[r] = f2bf(x);
+            }
+            bf16_t* y = (bf16_t*)a.Y + (long)m * a.ldy;
+            if (n0 + 3 < n_out && ((a.ldy & 3) == 0)) {
+                uint2 w;
+                w.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+                w.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+                *(uint2*)(y + n0) = w;
+            } else {
+                for (int r = 0; r < 4; ++r)
+                    if (n0 + r < n_out) y[n0 + r] = o[r];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+int pack_p16(const bf16_t* src, int N, int K, long ld, bf16_t* dst, int NGpad, hipStream_t st) {
+    if (K % 32 != 0 || NGpad * 16 < N || NGpad % 4 != 0) return -1;
+    const int KB = K / 32;
+    long nfrag = (long)NGpad * KB;
+    hipLaunchKernelGGL(pack_p16_kernel, dim3((unsigned)((nfrag + 3) / 4)), dim3(256), 0, st, src, N, K,
+                       ld, dst, KB, nfrag);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <int MT, int WPG, int EPI>
+static void launch_t(const GemmArgs& a, int mblocks, hipStream_t st) {
+    constexpr int RG = 4 / WPG;
+    dim3 grid((unsigned)(a.NG / RG), (unsigned)a.splits, (unsigned)mblocks);
+    hipLaunchKernelGGL((gemm_p16_kernel<MT, WPG, EPI>), grid, dim3(256), 0, st, a);
+}
+
+template <int MT, int WPG>
+static int launch_epi(const GemmArgs& a, int epi, int mblocks, hipStream_t st) {
+    switch (epi) {
+        case EPI_BF16: launch_t<MT, WPG, EPI_BF16>(a, mblocks, st); break;
+        case EPI_BIAS_BF16: launch_t<MT, WPG, EPI_BIAS_BF16>(a, mblocks, st); break;
+        case EPI_BIAS_GELU: launch_t<MT, WPG, EPI_BIAS_GELU>(a, mblocks, st); break;
+        case EPI_GEGLU:
+            if (WPG == 4) return -3;
+            launch_t<MT, WPG == 4 ? 2 : WPG, EPI_GEGLU>(a, mblocks, st);
+            break;
+        case EPI_F32: launch_t<MT, WPG, EPI_F32>(a, mblocks, st); break;
+        default: return -4;
+    }
+    return 0;
+}
+
+// Dispatch: decode-shaped (M <= 64) streams weights with K split over the
+// block's 4 waves (GEGLU: 2 waves per gate/up group); larger M uses 4 row groups
+// per block sharing X fragments.
+int gemm_p16(const GemmArgs& a_in, int epi, hipStream_t st) {
+    GemmArgs a = a_in;
+    if (a.M <= 0) return 0;
+    if (a.NG % 4 != 0 || a.splits < 1) return -1;
+    if (epi == EPI_GEGLU && a.splits != 1) return -1;
+    if (epi != EPI_F32 && a.splits != 1) return -1;
+    int rc;
+    if (a.M <= 64) {
+        const int wpg = (epi == EPI_GEGLU) ? 2 : 4;
+        if (a.M <= 16) {
+            rc = wpg == 2 ? launch_epi<1, 2>(a, epi, 1, st) : launch_epi<1, 4>(a, epi, 1, st);
+        } else if (a.M <= 32) {
+            rc = wpg == 2 ? launch_epi<2, 2>(a, epi, 1, st) : launch_epi<2, 4>(a, epi, 1, st);
+        } else {
+            rc = wpg == 2 ? launch_epi<4, 2>(a, epi, 1, st) : launch_epi<4, 4>(a, epi, 1, st);
+        }
+    } else {
+        const int mblocks = (a.M + 63) / 64;
+        rc = launch_epi<4, 1>(a, epi, mblocks, st);
+    }
+    if (rc) return rc;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace t5g

@@ -1,0 +1,137 @@
+// Internal launcher interface of the gfx950 kernels (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace t5g {
+typedef uint16_t bf16_t;
+
+enum { EPI_BF16 = 0, EPI_BIAS_BF16 = 1, EPI_BIAS_GELU = 2, EPI_GEGLU = 3, EPI_F32 = 4 };
+
+struct GemmArgs {
+    const bf16_t* X;  // [M][ldx] activations
+    int ldx;
+    int M;
+    const bf16_t* W;  // packed P16, NG row groups x KB fragments
+    int N;            // real output rows of W (GEGLU: 2*F interleaved gate/up groups)
+    int NG;           // padded row groups (multiple of 4)
+    int KB;           // K / 32
+    int splits;       // split-K over blockIdx.y (EPI_F32 only)
+    const bf16_t* bias;
+    void* Y;          // bf16 [M][ldy] or f32 [splits][M][ldy]
+    int ldy;
+};
+int pack_p16(const bf16_t* src, int N, int K, long ld, bf16_t* dst, int NGpad, hipStream_t st);
+int gemm_p16(const GemmArgs& a, int epi, hipStream_t st);
+
+// ---- row-wise residual / RMSNorm / embedding -------------------------------
+struct NormArgs {
+    int M, d;
+    const int* ids;          // optional: v = bf16(table[ids[m]] * scale)
+    const bf16_t* table;
+    float scale;
+    const bf16_t* delta;     // [M][d] bf16 (if ids == null and part == null)
+    const float* part;       // fp32 partial slabs [nsplit][M][ldp]
+    int nsplit, ldp;
+    const bf16_t* post_w;    // RMSNorm(1+w) applied to v before the residual add
+    const bf16_t* resid;     // [M][d] or null
+    const bf16_t* pre_w;     // RMSNorm(1+w) producing normed_out
+    float eps;
+    bf16_t* resid_out;       // [M][d] or null
+    bf16_t* normed_out;      // [M][d] or null
+    const int* out_rows;     // optional: process only rows out_rows[i] (i < M), write compact
+};
+int resid_norm(const NormArgs& a, hipStream_t st);
+
+// ---- RoPE + KV-cache store --------------------------------------------------
+struct RopeArgs {
+    const bf16_t* X;         // [M][ldx]: q heads | k heads | v heads
+    const float* Xpart;      // alternatively fp32 split-K slabs [nsplit][M][ldx] (summed, rounded)
+    int nsplit;
+    int ldx, M, D;
+    int nq, nk, nv;          // head counts present in X (column blocks of D)
+    int rope_q, rope_k;
+    const float* pos;        // [M] float PM positions (or pos_dev_row when decode)
+    const float* inv_freq;   // [D/2]
+    const int* tok_row;      // [M] batch row of each token (null: row = m)
+    const int* tok_t;        // [M] cache slot (null: slot = kv_len[row] - 1)
+    const int* kv_len;
+    bf16_t* Qout;            // [M][ldq] (may alias X)
+    int ldq;
+    bf16_t* Kc;              // cache [B][Hkv][Lmax][D]
+    bf16_t* Vc;
+    long c_bstride, c_hstride;
+};
+int rope_store(const RopeArgs& a, hipStream_t st);
+
+// ---- attention ----------------------------------------------------------------
+struct AttnArgs {
+    const bf16_t* Q;         // [Mq][ldq] rope applied
+    int ldq, Mq;
+    const int* q_row;        // [Mq] batch row (null: row = query index)
+    const int* q_pos;        // [Mq] query position t (null: t = kv_len[row] - 1)
+    const bf16_t* K;         // cache [B][Hkv][Lmax][D]
+    const bf16_t* V;
+    long kv_bstride, kv_hstride;
+    const int* kv_len;       // [B] valid keys per row
+    int Hkv, D, G;           // kv heads, head dim, q heads per kv head
+    int causal;              // 1: keys [0, t]; 0: keys [0, len)
+    int window;              // 0 none; causal: k > t-W; bidirectional: |t-k| <= W
+    float scale, softcap;
+    int eager;               // eager numerics (bf16 scores, normalised bf16 probs)
+    int nsplit, chunk;       // split keys over blockIdx.z
+    float* part;             // partial slabs when nsplit > 1
+    bf16_t* O;               // [Mq][ldo]
+    int ldo;
+};
+int attention(const AttnArgs& a, hipStream_t st);
+
+// ---- sampler -------------------------------------------------------------------
+struct SamplerRow {           // per-utterance parameters (device)
+    int top_k;                // <= 0 disabled
+    int top_k_list_len;       // > 0: top_k_list[min(len-1, cur_num_gen)]
+    int top_k_list_off;       // offset into the shared top-k list buffer
+    float top_p, min_p, temperature;
+    int stop_repetition;
+    int n_silence;
+    int silence_off;          // offset into the shared silence-token buffer
+    int eos_disabled;
+    uint32_t seed_lo, seed_hi;
+};
+struct SamplerState {         // per-utterance AR state (device), see inference_tts locals
+    int cur_num_gen;
+    int current_length;       // == self-attention keys in cache after the current input
+    int prompt_offset;
+    int target_total;         // < 0: none
+    int est_total;
+    int prev_token;
+    int consec_silence;
+    int first_input_len;
+    int done;
+    int ambiguous_steps;      // top-p tie groups straddling the cut (parity info)
+    int last_token;
+    float next_pos;           // PM position of the next decoder input
+};
+struct SamplerArgs {
+    const bf16_t* logits;     // [B][ldl]
+    int ldl, V, B;
+    const SamplerRow* rows;
+    SamplerState* state;
+    const int* top_k_list;
+    const int* silence;
+    const bf16_t* noise;      // parity mode: [B][noise_steps][V] bf16 or null (Philox)
+    int noise_steps;
+    int eos, eos_guard;       // eos id, encodec_sr // 5
+    float budget_extra;       // int(encodec_sr) * extra_cutoff
+    int text_guard;           // text_guard_frames_per_token
+    float progress_scale;
+    int* out_tokens;          // [B][max_gen]
+    int max_gen;
+    int* kv_len;              // [B] self-attention keys (advanced with current_length)
+    float* next_pos;          // [B] float PM position for the next step
+    int* next_token;          // [B] token fed to the next decoder step
+    int* flags;               // [B] per-step debug: bit0 ambiguous
+    unsigned* hist;           // scratch [B][65536] (top-p histogram walk)
+};
+int sample(const SamplerArgs& a, hipStream_t st);
+}  // namespace t5g

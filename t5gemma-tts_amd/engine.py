@@ -1,0 +1,444 @@
+"""Python host mirror of the reference's generate() hot path, over libt5gtts.so.
+
+``T5GemmaTTSEngine`` owns device weights (packed once into the P16 MFMA layout)
+and a native engine handle; ``generate`` runs a batch of utterances.
+``T5GemmaVoiceForConditionalGeneration`` keeps the reference's model API
+(hf_export/modeling_t5gemma_voice.py:338-862): ``from_pretrained`` and
+``inference_tts(x, x_lens, y, tgt_y_lens, top_k, top_p, min_p, temperature,
+stop_repetition, silence_tokens, multi_trial, **kwargs) -> (res, gen)`` with the
+same shapes, errors and token semantics -- and batch > 1 accepted (row i is the
+reference run alone on utterance i).
+
+Host-side work is only the reference's index/position plumbing (done with the
+same torch fp32 ops the reference uses, so positions are bit-identical); all
+arithmetic on activations runs in the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Union
+
+import torch
+
+from . import _lib
+from .config import VoiceConfig
+from .weights import check_state_dict
+
+BF16 = torch.bfloat16
+
+
+@dataclass
+class SamplingParams:
+    """``topk_sampling`` / ``sample_helper`` knobs of one utterance (:565-580)."""
+    top_k: Union[int, List[int]] = 30
+    top_p: float = 0.9
+    min_p: float = 0.0
+    temperature: float = 0.8
+    stop_repetition: int = 3
+    silence_tokens: Sequence[int] = ()
+    eos_disabled: bool = False
+
+
+@dataclass
+class Utterance:
+    x: Sequence[int]                 # text token ids (no padding)
+    y: Sequence[int] = ()            # prompt audio codes incl. y_sep (may be empty)
+    tgt_y_len: Optional[int] = None  # tgt_y_lens
+    prompt_frames: Optional[int] = None
+
+
+def reference_noise(seed: int, steps: int, V: int) -> torch.Tensor:
+    """The exponential draws torch.multinomial(p, 1) makes on CPU for ``steps``
+    consecutive calls after ``torch.manual_seed(seed)`` (parity mode, SURVEY a14' 6)."""
+    g = torch.Generator().manual_seed(int(seed))
+    out = torch.empty(steps, V, dtype=BF16)
+    for s in range(steps):
+        out[s] = torch.empty(V, dtype=BF16).exponential_(1, generator=g)
+    return out
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(device) -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class T5GemmaTTSEngine:
+    """One engine per GPU: packed weights + KV arena + sampler state in HBM."""
+
+    def __init__(self, cfg: VoiceConfig, state_dict: Dict[str, torch.Tensor], device="cuda:0",
+                 max_batch: int = 8, max_text: int = 128, max_audio: int = 1024, max_gen: Optional[int] = None,
+                 free_source: bool = False):
+        if not torch.cuda.is_available():
+            raise RuntimeError("T5GemmaTTSEngine needs a ROCm GPU (MI355X); there is no CPU fallback")
+        self.L = _lib.lib()
+        self.cfg = cfg
+        self.bb = bb = cfg.backbone
+        self.device = torch.device(device)
+        self.V = cfg.n_audio_tokens
+        self.max_batch, self.max_text, self.max_audio = max_batch, max_text, max_audio
+        self.max_gen = max_gen or max_audio
+        check_state_dict(cfg, state_dict)
+        self._keep: List[torch.Tensor] = []
+        dev = self.device
+
+        def w(name):
+            t = state_dict[name]
+            if t.device != dev or t.dtype != BF16:
+                t = t.to(device=dev, dtype=BF16)
+            return t.contiguous()
+
+        def keep(t):
+            self._keep.append(t)
+            return t.data_ptr()
+
+        stream = _stream(dev)
+
+        def pack(mat: torch.Tensor) -> int:
+            N, K = mat.shape
+            nbytes = self.L.t5g_packed_bytes(N, K)
+            dst = torch.empty(nbytes // 2, dtype=BF16, device=dev)
+            _lib.check(self.L.t5g_pack_weight(_ptr(mat), N, K, K, _ptr(dst), stream), "pack")
+            return keep(dst)
+
+        d, f = bb.hidden_size, bb.intermediate_size
+
+        def interleave_gate_up(gate, up):
+            return torch.stack([gate.view(f // 16, 16, d), up.view(f // 16, 16, d)], dim=1).reshape(2 * f, d)
+
+        def layer(side: str, i: int) -> _lib.LayerWeights:
+            p = f"backbone.model.{side}.layers.{i}"
+            lw = _lib.LayerWeights()
+            lw.qkv = pack(torch.cat([w(f"{p}.self_attn.q_proj.weight"), w(f"{p}.self_attn.k_proj.weight"),
+                                     w(f"{p}.self_attn.v_proj.weight")], 0))
+            lw.o = pack(w(f"{p}.self_attn.o_proj.weight"))
+            lw.gate_up = pack(interleave_gate_up(w(f"{p}.mlp.gate_proj.weight"), w(f"{p}.mlp.up_proj.weight")))
+            lw.down = pack(w(f"{p}.mlp.down_proj.weight"))
+            names = ["pre_self_attn_layernorm", "post_self_attn_layernorm", "pre_cross_attn_layernorm",
+                     "post_cross_attn_layernorm", "pre_feedforward_layernorm", "post_feedforward_layernorm"]
+            for j, nm in enumerate(names):
+                key = f"{p}.{nm}.weight"
+                lw.norms[j] = keep(w(key)) if key in state_dict else None
+            if side == "decoder":
+                lw.cross_q = pack(w(f"{p}.cross_attn.q_proj.weight"))
+                lw.cross_kv = pack(torch.cat([w(f"{p}.cross_attn.k_proj.weight"),
+                                              w(f"{p}.cross_attn.v_proj.weight")], 0))
+                lw.cross_o = pack(w(f"{p}.cross_attn.o_proj.weight"))
+            return lw
+
+        self._enc = (_lib.LayerWeights * bb.num_encoder_layers)(
+            *[layer("encoder", i) for i in range(bb.num_encoder_layers)])
+        self._dec = (_lib.LayerWeights * bb.num_decoder_layers)(
+            *[layer("decoder", i) for i in range(bb.num_decoder_layers)])
+        W = _lib.Weights()
+        W.enc_embed = keep(w("backbone.model.encoder.embed_tokens.weight"))
+        W.audio_embed = keep(w("audio_embedding.0.weight"))
+        W.enc_final_norm = keep(w("backbone.model.encoder.norm.weight"))
+        W.dec_final_norm = keep(w("backbone.model.decoder.norm.weight"))
+        W.head1 = pack(w("predict_layer.0.0.weight"))
+        W.head1_bias = keep(w("predict_layer.0.0.bias"))
+        W.head2 = pack(w("predict_layer.0.2.weight"))
+        W.head2_bias = keep(w("predict_layer.0.2.bias"))
+        inv = 1.0 / (bb.rope_theta ** (torch.arange(0, bb.head_dim, 2, dtype=torch.float) / bb.head_dim))
+        W.inv_freq = keep(inv.to(dev))
+        W.enc_layers = self._enc
+        W.dec_layers = self._dec
+        self._weights = W
+        if free_source:
+            state_dict.clear()
+
+        c = _lib.Config()
+        c.hidden, c.intermediate = d, f
+        c.n_enc_layers, c.n_dec_layers = bb.num_encoder_layers, bb.num_decoder_layers
+        c.n_heads, c.n_kv_heads, c.head_dim = bb.num_attention_heads, bb.num_key_value_heads, bb.head_dim
+        c.text_vocab, c.n_audio_tokens = bb.text_vocab_size, self.V
+        c.attn_scale = bb.attn_scale
+        c.softcap = bb.softcap
+        c.rms_eps = bb.rms_norm_eps
+        c.normalizer = float(torch.tensor(d ** 0.5, dtype=BF16).item())
+        c.sliding_window = int(bb.sliding_window)
+        for i, lt in enumerate(bb.layer_types("encoder")):
+            c.enc_sliding[i] = 1 if lt == "sliding_attention" else 0
+        for i, lt in enumerate(bb.layer_types("decoder")):
+            c.dec_sliding[i] = 1 if lt == "sliding_attention" else 0
+        c.max_batch, c.max_text, c.max_audio, c.max_gen = max_batch, max_text, max_audio, self.max_gen
+        c.eos = cfg.eog_inference
+        c.eos_guard = cfg.eos_guard_steps
+        c.budget_extra = float(cfg.extra_budget)
+        c.text_guard = int(cfg.text_guard_frames_per_token)
+        c.progress_scale = float(cfg.progress_scale)
+        self._cfg = c
+        torch.cuda.synchronize(dev)
+        h = C.c_void_p()
+        _lib.check(self.L.t5g_engine_create(C.byref(c), C.byref(W), C.byref(h)), "engine_create")
+        self.h = h
+        ld = C.c_int32()
+        self._logits_ptr = self.L.t5g_logits_ptr(h, C.byref(ld))
+        self.logits_ld = ld.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.t5g_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def workspace_bytes(self) -> int:
+        return int(self.L.t5g_engine_workspace_bytes(self.h))
+
+    # ------------------------------------------------------------------
+    def _positions_encoder(self, T: int) -> torch.Tensor:
+        # _build_position_ids (:516-531) for one unpadded row
+        lengths = torch.tensor([T])
+        pos = torch.arange(T, dtype=torch.float32)[None, :]
+        denom = (lengths.clamp(min=2).to(torch.float32) - 1.0)[:, None]
+        p = pos / denom * self.cfg.progress_scale
+        return p.masked_fill(~(pos < lengths[:, None]), 0.0)[0]
+
+    def _positions_prefill(self, cur_len: int, est_total: int) -> torch.Tensor:
+        base = torch.arange(cur_len, dtype=torch.float32).unsqueeze(0)
+        return (base / max(1, est_total - 1) * self.cfg.progress_scale)[0]
+
+    def logits(self, B: int) -> torch.Tensor:
+        """Copy of the current logits [B, V] (bf16, device)."""
+        t = torch.empty(B, self.logits_ld, dtype=BF16, device=self.device)
+        _lib.check(self.L.t5g_copy_logits(self.h, _ptr(t), B, _stream(self.device)), "copy_logits")
+        return t[:, :self.V]
+
+    # ------------------------------------------------------------------
+    def generate(self, utts: Sequence[Utterance], params: Union[SamplingParams, Sequence[SamplingParams]],
+                 seeds: Optional[Sequence[int]] = None, parity: bool = False, use_graph: bool = True,
+                 chunk: int = 32, record_logits: bool = False):
+        """Run inference_tts on a batch. ``parity=True`` uses the reference's CPU RNG
+        stream (seed per row, reseeded before the loop) and resolves tie-ambiguous
+        top-p steps on the host -- token-exact reproduction mode (slow: one host
+        sync per step). Returns dict(res=[...], gen=[...], steps, ambiguous)."""
+        cfg, dev = self.cfg, self.device
+        B = len(utts)
+        if B < 1:
+            raise ValueError("empty batch")
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} > engine max_batch {self.max_batch}")
+        if isinstance(params, SamplingParams):
+            params = [params] * B
+        seeds = list(seeds) if seeds is not None else list(range(1, B + 1))
+        stream = _stream(dev)
+        eos = cfg.eog_inference
+        # ---- host plumbing: packed text / audio tokens and float PM positions
+        ids, trow, tt, tpos, tlen = [], [], [], [], []
+        aid, arow, at, apos, alen, last = [], [], [], [], [], []
+        states = (_lib.SamplerState * B)()
+        rows = (_lib.SamplerRow * B)()
+        topk_list: List[int] = []
+        silence: List[int] = []
+        y_rows = []
+        max_steps = 1
+        for b, u in enumerate(utts):
+            x = [int(v) for v in u.x]
+            if len(x) == 0:
+                raise ValueError("empty text")
+            if len(x) > self.max_text:
+                raise ValueError(f"text length {len(x)} > max_text {self.max_text}")
+            ids += x
+            trow += [b] * len(x)
+            tt += list(range(len(x)))
+            tpos.append(self._positions_encoder(len(x)))
+            tlen.append(len(x))
+            y = [int(v) for v in u.y]
+            if cfg.special_first:
+                y = [v + int(cfg.n_special) for v in y]
+            y_rows.append(y)
+            cated = [cfg.empty_token] + y
+            cur_len = len(cated)
+            pf = len(y) if u.prompt_frames is None else int(u.prompt_frames)
+            tgt = None if u.tgt_y_len is None else int(u.tgt_y_len)
+            if tgt is not None:
+                est = tgt + 1
+            else:
+                est = int(cur_len + int(cfg.encodec_sr) * cfg.progress_lookahead_secs)
+            est = max(est, cur_len)
+            last.append(len(aid) + cur_len - 1)
+            aid += cated
+            arow += [b] * cur_len
+            at += list(range(cur_len))
+            apos.append(self._positions_prefill(cur_len, est))
+            alen.append(cur_len)
+            st = states[b]
+            st.cur_num_gen, st.current_length, st.prompt_offset = 0, cur_len, pf + 1
+            st.target_total = -1 if tgt is None else tgt
+            st.est_total, st.prev_token, st.consec_silence = est, -1, 0
+            st.first_input_len, st.done, st.ambiguous_steps, st.last_token, st.next_pos = len(x), 0, 0, -1, 0.0
+            if tgt is not None:
+                budget = int(math.floor(tgt - (pf + 1) + cfg.extra_budget)) + 2
+            else:
+                budget = self.max_gen
+            budget = min(budget, self.max_gen)
+            if cur_len + budget > self.max_audio:
+                raise ValueError(f"row {b}: prompt {cur_len} + budget {budget} > max_audio {self.max_audio}")
+            max_steps = max(max_steps, budget)
+            p = params[b]
+            r = rows[b]
+            if isinstance(p.top_k, (list, tuple)):
+                r.top_k, r.top_k_list_len, r.top_k_list_off = 0, len(p.top_k), len(topk_list)
+                topk_list += [int(k) for k in p.top_k]
+            else:
+                r.top_k, r.top_k_list_len, r.top_k_list_off = int(p.top_k), 0, 0
+            r.top_p, r.min_p, r.temperature = float(p.top_p), float(p.min_p), float(p.temperature)
+            r.stop_repetition = int(p.stop_repetition)
+            r.n_silence, r.silence_off = len(p.silence_tokens), len(silence)
+            silence += [int(s) for s in p.silence_tokens]
+            r.eos_disabled = int(bool(p.eos_disabled))
+            r.seed_lo, r.seed_hi = int(seeds[b]) & 0xFFFFFFFF, (int(seeds[b]) >> 32) & 0xFFFFFFFF
+        i32 = dict(dtype=torch.int32, device=dev)
+        d_ids, d_trow, d_tt = (torch.tensor(v, **i32) for v in (ids, trow, tt))
+        d_tpos = torch.cat(tpos).to(dev)
+        d_tlen = torch.tensor(tlen, **i32)
+        d_aid, d_arow, d_at = (torch.tensor(v, **i32) for v in (aid, arow, at))
+        d_apos = torch.cat(apos).to(dev)
+        d_alen, d_last = torch.tensor(alen, **i32), torch.tensor(last, **i32)
+        noise = None
+        if parity:
+            noise = torch.stack([reference_noise(s, max_steps, self.V) for s in seeds[:B]]).to(dev)
+        L = self.L
+        _lib.check(L.t5g_encode(self.h, B, len(ids), _ptr(d_ids), _ptr(d_trow), _ptr(d_tt), _ptr(d_tpos),
+                                _ptr(d_tlen), stream), "encode")
+        _lib.check(L.t5g_prefill(self.h, B, len(aid), _ptr(d_aid), _ptr(d_arow), _ptr(d_at), _ptr(d_apos),
+                                 _ptr(d_alen), _ptr(d_last), stream), "prefill")
+        tk = (C.c_int32 * max(1, len(topk_list)))(*topk_list)
+        sl = (C.c_int32 * max(1, len(silence)))(*silence)
+        _lib.check(L.t5g_sampler_setup(self.h, B, rows, states, tk, len(topk_list), sl, len(silence),
+                                       _ptr(noise), max_steps if parity else 0, stream), "sampler_setup")
+        rec = [] if record_logits else None
+        ambiguous_fixed = 0
+        steps = 0
+        if parity:
+            cur = (_lib.SamplerState * B)()
+            _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
+            flags = (C.c_int32 * B)()
+            while not all(cur[b].done for b in range(B)):
+                if rec is not None:
+                    rec.append(self.logits(B).clone())
+                pre = (_lib.SamplerState * B)()
+                C.memmove(pre, cur, C.sizeof(cur))
+                _lib.check(L.t5g_sample_only(self.h, B, C.c_void_p(self._logits_ptr), self.logits_ld, stream),
+                           "sample")
+                _lib.check(L.t5g_read_flags(self.h, flags, B, stream), "read_flags")
+                for b in range(B):
+                    if pre[b].done or not (flags[b] & 1):
+                        continue
+                    lg = self.logits(B)[b].contiguous().cpu()
+                    nz = noise[b, pre[b].cur_num_gen].contiguous().cpu()
+                    out_st = _lib.SamplerState()
+                    tok = C.c_int32()
+                    _lib.check(L.t5g_host_sample(
+                        _ptr(lg), self.V, C.byref(rows[b]), tk, sl, C.byref(pre[b]), _ptr(nz), eos,
+                        self._cfg.eos_guard, self._cfg.budget_extra, self._cfg.text_guard,
+                        self._cfg.progress_scale, self.max_gen, C.byref(out_st), C.byref(tok)), "host_sample")
+                    out_st.ambiguous_steps = pre[b].ambiguous_steps + 1
+                    _lib.check(L.t5g_write_state(self.h, C.byref(out_st), b, pre[b].cur_num_gen, tok.value,
+                                                 stream), "write_state")
+                    ambiguous_fixed += 1
+                _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
+                steps += 1
+                if not all(cur[b].done for b in range(B)):
+                    _lib.check(L.t5g_step_only(self.h, stream), "step")
+        else:
+            cur = (_lib.SamplerState * B)()
+            while True:
+                n = min(chunk, max_steps + 1 - steps)
+                n = max(n, 1)
+                _lib.check(L.t5g_decode(self.h, n, 1 if use_graph else 0, stream), "decode")
+                steps += n
+                _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
+                if all(cur[b].done for b in range(B)):
+                    break
+                if steps > max_steps + 2:
+                    raise RuntimeError("decode did not terminate within the time budget")
+        toks = (C.c_int32 * (B * self.max_gen))()
+        _lib.check(L.t5g_read_tokens(self.h, toks, B, stream), "read_tokens")
+        res, gen = [], []
+        for b in range(B):
+            n = cur[b].cur_num_gen
+            g = [toks[b * self.max_gen + i] for i in range(n)]
+            gt = torch.tensor(g, dtype=torch.long)
+            rt = torch.cat([torch.tensor(y_rows[b], dtype=torch.long), gt])
+            if cfg.special_first:
+                rt = rt - int(cfg.n_special)
+                gt = gt - int(cfg.n_special)
+            res.append(rt)
+            gen.append(gt)
+        out = {"res": res, "gen": gen, "steps": steps,
+               "ambiguous": [cur[b].ambiguous_steps for b in range(B)], "ambiguous_fixed": ambiguous_fixed}
+        if rec is not None:
+            out["logits"] = rec
+        return out
+
+
+# ----------------------------------------------------------------------------
+class T5GemmaVoiceForConditionalGeneration:
+    """Drop-in for the reference's HF model class on the generate() path.
+
+    ``from_pretrained(model_dir)`` reads the HF export (config.json +
+    safetensors, no pickle); ``inference_tts`` keeps the reference signature
+    and return shapes (:565-862)."""
+
+    def __init__(self, cfg: VoiceConfig, state_dict, device="cuda:0", **engine_kw):
+        self.config = cfg
+        self.args = cfg
+        self.engine = T5GemmaTTSEngine(cfg, state_dict, device=device, **engine_kw)
+        self.seed = 1
+
+    @classmethod
+    def from_pretrained(cls, model_dir: str, device="cuda:0", **engine_kw):
+        from .weights import load_hf_checkpoint
+        cfg = VoiceConfig.from_pretrained(model_dir)
+        return cls(cfg, load_hf_checkpoint(model_dir), device=device, **engine_kw)
+
+    def eval(self):
+        return self
+
+    def to(self, *a, **k):
+        return self
+
+    @torch.inference_mode()
+    def inference_tts(self, x, x_lens, y, tgt_y_lens, top_k=-100, top_p=1.0, min_p=0.0, temperature=1.0,
+                      stop_repetition=3, silence_tokens=None, multi_trial=None, parity=False, seeds=None,
+                      **kwargs):
+        cfg = self.config
+        if int(getattr(cfg, "n_codebooks", 1)) != 1:
+            raise ValueError("XCodec2 inference expects n_codebooks=1.")
+        B = x.shape[0]
+        if y.dim() != 3 or y.shape[2] != 1:
+            raise ValueError(f"y must be [B, T, 1], got {tuple(y.shape)}")
+        pf = kwargs.get("prompt_frames", None)
+        utts = []
+        for b in range(B):
+            xl = int(x_lens[b])
+            utts.append(Utterance(x=x[b, :xl].tolist(), y=y[b, :, 0].tolist(),
+                                  tgt_y_len=None if tgt_y_lens is None else int(tgt_y_lens[b]),
+                                  prompt_frames=pf))
+        params = SamplingParams(top_k=top_k, top_p=top_p, min_p=min_p, temperature=temperature,
+                                stop_repetition=stop_repetition, silence_tokens=tuple(silence_tokens or ()))
+        if seeds is None:
+            seeds = [self.seed + b for b in range(B)]
+        out = self.engine.generate(utts, params, seeds=seeds, parity=parity)
+        n = max(len(g) for g in out["gen"])
+        if B == 1:
+            return out["res"][0].view(1, 1, -1), out["gen"][0].view(1, 1, -1)
+        # batched: right-pad with eos so rows stack (per-row lengths in .lengths)
+        eos = cfg.eog_inference
+        gen = torch.full((B, 1, n), eos, dtype=torch.long)
+        res = torch.full((B, 1, max(len(r) for r in out["res"])), eos, dtype=torch.long)
+        for b in range(B):
+            gen[b, 0, :len(out["gen"][b])] = out["gen"][b]
+            res[b, 0, :len(out["res"][b])] = out["res"][b]
+        return res, gen

@@ -1,0 +1,271 @@
+"""Generate golden vectors by running the REFERENCE itself in this container.
+
+Run here only (``python tests/golden/make_golden.py``); never on the GPU box
+(``/root/reference`` does not exist there). Output: small JSON/NPZ fixtures in
+``tests/golden/``. No reference source is copied: we import it read-only.
+
+What is imported: ``/root/reference/models/t5gemma.py`` (``T5GemmaVoiceModel``,
+whose ``inference_tts`` is identical to ``hf_export/modeling_t5gemma_voice.py:565-862``;
+the HF copy raises SyntaxError on import -- ``from __future__`` after the
+auto-added header) and ``models/utils.py`` (``topk_sampling``).
+
+Two mechanical adapters, no arithmetic change:
+1. transformers 5.15 calls decoder layers positionally without ``cache_position``;
+   ``PMDecoderLayer.forward`` expects the 4.57.3 order -> keyword re-routing wrapper.
+2. ``T5GemmaVoiceModel`` loads the backbone with ``from_pretrained(name)``; we point
+   ``name`` at a local directory written by ``T5GemmaForConditionalGeneration(cfg)``.
+Construction runs under default dtype bf16, as inside HF ``from_pretrained(dtype=bf16)``
+(``inference_commandline_hf.py:102-106``): every parameter bf16, RoPE ``inv_freq`` fp32.
+Weights are the repo's seeded generator (``t5gemma_tts_amd.weights.synthetic_weights``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+REF = "/root/reference"
+
+from t5gemma_tts_amd.config import named_config  # noqa: E402
+from t5gemma_tts_amd.weights import state_dict_digest, synthetic_weights  # noqa: E402
+
+
+def _import_reference():
+    sys.path.insert(0, REF)
+    import models.t5gemma as RT  # noqa: E402
+    import models.utils as RU  # noqa: E402
+
+    orig = RT.PMDecoderLayer.forward
+
+    def fwd(self, hidden_states, position_embeddings=None, attention_mask=None, position_ids=None,
+            past_key_values=None, use_cache=False, encoder_hidden_states=None,
+            encoder_attention_mask=None, **kw):
+        return orig(self, hidden_states, position_embeddings=position_embeddings,
+                    attention_mask=attention_mask, position_ids=position_ids,
+                    past_key_values=past_key_values, use_cache=use_cache, cache_position=None,
+                    encoder_hidden_states=encoder_hidden_states,
+                    encoder_attention_mask=encoder_attention_mask, **kw)
+
+    RT.PMDecoderLayer.forward = fwd
+    return RT, RU
+
+
+class _Args:
+    pass
+
+
+def build_reference_model(RT, cfg, seed, workdir):
+    from transformers import T5GemmaConfig, T5GemmaForConditionalGeneration
+
+    bb = cfg.backbone
+    side = dict(hidden_size=bb.hidden_size, intermediate_size=bb.intermediate_size,
+                num_attention_heads=bb.num_attention_heads, num_key_value_heads=bb.num_key_value_heads,
+                head_dim=bb.head_dim, vocab_size=bb.text_vocab_size,
+                query_pre_attn_scalar=int(bb.query_pre_attn_scalar), sliding_window=bb.sliding_window,
+                attn_logit_softcapping=bb.attn_logit_softcapping, rms_norm_eps=bb.rms_norm_eps)
+    tcfg = T5GemmaConfig(encoder=dict(side, num_hidden_layers=bb.num_encoder_layers),
+                         decoder=dict(side, num_hidden_layers=bb.num_decoder_layers),
+                         vocab_size=bb.text_vocab_size)
+    bdir = os.path.join(workdir, "backbone")
+    T5GemmaForConditionalGeneration(tcfg).to(torch.bfloat16).save_pretrained(bdir)
+
+    a = _Args()
+    a.t5gemma_model_name = bdir
+    a.attn_implementation = bb.attn_implementation
+    a.precision = "bfloat16"
+    a.prune_text_modules = 2
+    a.use_pm_rope = 1
+    a.use_lora = 0
+    a.text_input_type = "text"
+    a.n_codebooks = 1
+    for k in ("audio_vocab_size", "n_special", "empty_token", "eog", "audio_pad_token", "eos",
+              "y_sep_token", "x_sep_token", "special_first", "encodec_sr", "progress_scale",
+              "extra_cutoff", "text_guard_frames_per_token", "progress_lookahead_secs"):
+        setattr(a, k, getattr(cfg, k))
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16)
+    try:
+        m = RT.T5GemmaVoiceModel(a)
+    finally:
+        torch.set_default_dtype(prev)
+    m.eval()
+    sd = synthetic_weights(cfg, seed)
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    real_missing = [k for k in missing if not (k.startswith("encoder_module.") or k.startswith("decoder_module.")
+                                               or k.startswith("backbone.lm_head") or k == "class_weight")]
+    assert not real_missing, real_missing[:10]
+    for n, p in m.named_parameters():
+        assert p.dtype == torch.bfloat16, n
+    return m, sd
+
+
+def run_case(RT, m, cfg, case):
+    """One reference inference_tts call, reseeded right before (SURVEY a14' step 8).
+    Records per-step logits by wrapping predict_layer."""
+    x = torch.tensor([case["x"]], dtype=torch.long)
+    y = torch.tensor(case["y"], dtype=torch.long).view(1, -1, 1)
+    tgt = torch.tensor([case["tgt"]], dtype=torch.long)
+    logs = []
+    head = m.predict_layer[0]
+
+    class Rec(torch.nn.Module):
+        def __init__(self, inner):
+            super().__init__()
+            self.inner = inner
+
+        def forward(self, h):
+            o = self.inner(h)
+            logs.append(o.detach().clone().view(-1))
+            return o
+
+    m.predict_layer[0] = Rec(head)
+    try:
+        torch.manual_seed(case["seed"])
+        t0 = time.time()
+        res, gen = m.inference_tts(x, torch.tensor([x.shape[1]]), y, tgt_y_lens=tgt,
+                                   top_k=case["top_k"], top_p=case["top_p"], min_p=case["min_p"],
+                                   temperature=case["temperature"],
+                                   stop_repetition=case["stop_repetition"],
+                                   silence_tokens=case["silence_tokens"],
+                                   prompt_frames=len(case["y"]))
+        dt = time.time() - t0
+    finally:
+        m.predict_layer[0] = head
+    return res.view(-1).tolist(), gen.view(-1).tolist(), torch.stack(logs), dt
+
+
+def bf16_bits(t: torch.Tensor) -> np.ndarray:
+    return t.contiguous().view(torch.int16).numpy().astype(np.int16)
+
+
+def model_cases(cfg, rng, n_cases, vocab_text, with_prompt_frac=0.5, max_tx=20, tgt_frames=(10, 30)):
+    V = cfg.audio_vocab_size
+    cases = []
+    variants = [
+        dict(top_k=30, top_p=0.9, min_p=0.0, temperature=0.8, stop_repetition=3, silence_tokens=[]),
+        dict(top_k=1, top_p=1.0, min_p=0.0, temperature=1.0, stop_repetition=3, silence_tokens=[]),
+        dict(top_k=0, top_p=0.8, min_p=0.0, temperature=1.0, stop_repetition=3, silence_tokens=[]),
+        dict(top_k=30, top_p=1.0, min_p=0.05, temperature=0.9, stop_repetition=3, silence_tokens=[]),
+        dict(top_k=5, top_p=0.95, min_p=0.0, temperature=1.2, stop_repetition=2,
+             silence_tokens=[1, 2, 3]),
+        dict(top_k=[40, 20, 10], top_p=0.9, min_p=0.0, temperature=0.8, stop_repetition=3,
+             silence_tokens=[]),
+    ]
+    for i in range(n_cases):
+        var = variants[i % len(variants)]
+        tx = int(rng.integers(3, max_tx))
+        x = rng.integers(3, vocab_text - 1, size=tx)
+        x[rng.integers(0, tx)] = cfg.x_sep_token
+        tp = int(rng.integers(1, 12)) if (i % 2 == 1) else 0
+        y = rng.integers(0, V, size=tp).tolist()
+        if tp:
+            y.append(cfg.y_sep_token)
+        tgt = len(y) + int(rng.integers(*tgt_frames))
+        if var["silence_tokens"]:
+            y = y[:-1] + [1, 1, 1, 1] + y[-1:] if y else [1, 1, 1, 1, cfg.y_sep_token]
+            tgt = len(y) + int(rng.integers(*tgt_frames))
+        cases.append(dict(x=[int(v) for v in x], y=[int(v) for v in y], tgt=int(tgt),
+                          seed=int(1000 + i), **var))
+    return cases
+
+
+def gen_model_golden(RT, name, cfg_kw, seed, n_cases, out, store_logits="full", max_tx=20,
+                     tgt_frames=(10, 30)):
+    cfg = named_config(name, **cfg_kw)
+    with tempfile.TemporaryDirectory() as td:
+        m, sd = build_reference_model(RT, cfg, seed, td)
+        rng = np.random.default_rng(seed)
+        cases = model_cases(cfg, rng, n_cases, cfg.backbone.text_vocab_size, max_tx=max_tx,
+                            tgt_frames=tgt_frames)
+        arrays = {}
+        for ci, c in enumerate(cases):
+            res, gen, logs, dt = run_case(RT, m, cfg, c)
+            c["res"], c["gen"] = res, gen
+            c["ref_seconds"] = round(dt, 4)
+            c["n_steps"] = int(logs.shape[0])
+            if store_logits == "full":
+                arrays[f"logits_{ci}"] = bf16_bits(logs)
+            else:
+                # sub-sampled: top-64 values/indices per step + full-row sha
+                top = torch.topk(logs.float(), 64, dim=-1)
+                arrays[f"top_vals_{ci}"] = bf16_bits(top.values.to(torch.bfloat16))
+                arrays[f"top_idx_{ci}"] = top.indices.numpy().astype(np.int32)
+                import hashlib
+                c["logit_sha"] = [hashlib.sha256(bf16_bits(r).tobytes()).hexdigest()[:16] for r in logs]
+            print(f"[{name}] case {ci}: T_x={len(c['x'])} T_p={len(c['y'])} gen={len(gen)} "
+                  f"({dt:.2f}s)", flush=True)
+    meta = {"config": name, "config_kw": cfg_kw, "weight_seed": seed,
+            "weight_sha256": state_dict_digest(sd), "torch": torch.__version__,
+            "threads": torch.get_num_threads(), "cases": cases}
+    with open(os.path.join(HERE, f"{out}.json"), "w") as f:
+        json.dump(meta, f)
+    np.savez_compressed(os.path.join(HERE, f"{out}.npz"), **arrays)
+
+
+def gen_sampler_golden(RU, out="golden_sampler", V=65541, n=48):
+    """Per-step sampler cases at the real vocab: reference topk_sampling +
+    torch.multinomial under torch.manual_seed(seed). Logits regenerable from
+    (logit_seed, scale, quant) so no big arrays are stored."""
+    cases = []
+    params = [
+        (30, 0.9, 0.0, 0.8), (30, 0.9, 0.0, 1.0), (1, 1.0, 0.0, 1.0), (0, 0.8, 0.0, 1.0),
+        (30, 1.0, 0.1, 1.0), (50, 0.95, 0.0, 0.7), (10, 0.5, 0.0, 1.3), (0, 0.9, 0.0, 0.8),
+    ]
+    for i in range(n):
+        k, p, mp, t = params[i % len(params)]
+        scale = [0.6, 2.0, 4.0][i % 3]
+        quant = [0.0, 0.25, 0.5][(i // 3) % 3]     # quantised logits -> deliberate ties
+        lseed = 500 + i
+        logits = make_sampler_logits(lseed, V, scale, quant)
+        torch.manual_seed(9000 + i)
+        tok = RU.topk_sampling(logits.clone(), top_k=k, top_p=p, min_p=mp, temperature=t)
+        x = logits.clone()
+        if t != 1.0:
+            x = x / t
+        filt = RU.top_k_top_p_filtering(x, top_k=k, top_p=p, min_p=mp)
+        surv = torch.nonzero(torch.isfinite(filt)).view(-1)
+        cases.append(dict(logit_seed=lseed, V=V, scale=scale, quant=quant, top_k=k, top_p=p,
+                          min_p=mp, temperature=t, noise_seed=9000 + i, token=int(tok.item()),
+                          n_survivors=int(surv.numel()),
+                          survivors_head=[int(v) for v in surv[:64].tolist()]))
+    with open(os.path.join(HERE, f"{out}.json"), "w") as f:
+        json.dump({"torch": torch.__version__, "cases": cases}, f)
+    print(f"[sampler] {n} cases")
+
+
+def make_sampler_logits(seed: int, V: int, scale: float, quant: float) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(V, generator=g) * scale
+    if quant > 0:
+        x = torch.round(x / quant) * quant
+    return x.to(torch.bfloat16)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    RT, RU = _import_reference()
+    todo = args.only.split(",") if args.only else ["sampler", "tiny", "tiny_eager", "tiny_window", "mid"]
+    if "sampler" in todo:
+        gen_sampler_golden(RU)
+    if "tiny" in todo:
+        gen_model_golden(RT, "tiny", {}, seed=7, n_cases=12, out="golden_tiny")
+    if "tiny_eager" in todo:
+        gen_model_golden(RT, "tiny", {"attn_implementation": "eager"}, seed=8, n_cases=4,
+                         out="golden_tiny_eager")
+    if "tiny_window" in todo:
+        gen_model_golden(RT, "tiny", {"sliding_window": 8}, seed=9, n_cases=4, out="golden_tiny_window")
+    if "mid" in todo:
+        gen_model_golden(RT, "mid", {}, seed=11, n_cases=2, out="golden_mid", store_logits="top",
+                         max_tx=40, tgt_frames=(4, 8))
