@@ -56,10 +56,18 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
                                                    __builtin_bit_cast(bf16x8_b, b), c, 0, 0, 0);
 }
 
-template <int MT, int WPG, int EPI>
+// KS = K-interleave factor of the accumulation: k-step kb belongs to slice
+// (kb - kb_lo) % KS, each slice is accumulated in k order, and the slices are
+// summed in slice order at the end. The result is therefore bit-identical
+// whether a slice runs on its own wave (WPG == KS, decode) or all slices of a row
+// group run on one wave (WPG == 1, prefill) -- a row's logits do not depend on
+// which other rows share the batch.
+template <int MT, int WPG, int KS, int EPI>
 __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
+    static_assert(WPG == KS || WPG == 1, "slice mapping");
     constexpr int RG = 4 / WPG;  // row groups per block
-    constexpr int UN = 4;        // k-steps in flight per wave
+    constexpr int SPW = KS / WPG;  // slices per wave
+    constexpr int UN = (WPG == 1) ? KS : 4;  // k-steps in flight per wave per iteration
     __shared__ f32x4 red[4][MT][64];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -70,34 +78,60 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
     const int kb_lo = blockIdx.y * per;
     const int kb_hi = min(a.KB, kb_lo + per);
 
-    f32x4 acc[MT];
+    f32x4 acc[SPW][MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < SPW; ++s)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[s][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     const bf16x8_s* wp = (const bf16x8_s*)a.W + ((long)g * a.KB) * 64 + lane;
-    int kb = kb_lo + ks;
-    for (; kb + (UN - 1) * WPG < kb_hi; kb += UN * WPG) {
-        bf16x8_s wf[UN];
-        bf16x8_s xf[UN][MT];
+    if constexpr (WPG == KS) {
+        // one slice per wave: kb = kb_lo + ks, +KS, ...
+        int kb = kb_lo + ks;
+        for (; kb + (UN - 1) * KS < kb_hi; kb += UN * KS) {
+            bf16x8_s wf[UN];
+            bf16x8_s xf[UN][MT];
 #pragma unroll
-        for (int u = 0; u < UN; ++u) wf[u] = __builtin_nontemporal_load(wp + (long)(kb + u * WPG) * 64);
+            for (int u = 0; u < UN; ++u) wf[u] = __builtin_nontemporal_load(wp + (long)(kb + u * KS) * 64);
 #pragma unroll
-        for (int u = 0; u < UN; ++u) load_x<MT>(a.X, a.ldx, a.M, m0, kb + u * WPG, lane, xf[u]);
+            for (int u = 0; u < UN; ++u) load_x<MT>(a.X, a.ldx, a.M, m0, kb + u * KS, lane, xf[u]);
 #pragma unroll
-        for (int u = 0; u < UN; ++u)
+            for (int u = 0; u < UN; ++u)
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(wf[u], xf[u][mt], acc[mt]);
-    }
-    for (; kb < kb_hi; kb += WPG) {
-        bf16x8_s wf = __builtin_nontemporal_load(wp + (long)kb * 64);
-        bf16x8_s xf[MT];
-        load_x<MT>(a.X, a.ldx, a.M, m0, kb, lane, xf);
+                for (int mt = 0; mt < MT; ++mt) acc[0][mt] = mfma16(wf[u], xf[u][mt], acc[0][mt]);
+        }
+        for (; kb < kb_hi; kb += KS) {
+            bf16x8_s wf = __builtin_nontemporal_load(wp + (long)kb * 64);
+            bf16x8_s xf[MT];
+            load_x<MT>(a.X, a.ldx, a.M, m0, kb, lane, xf);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(wf, xf[mt], acc[mt]);
+            for (int mt = 0; mt < MT; ++mt) acc[0][mt] = mfma16(wf, xf[mt], acc[0][mt]);
+        }
+    } else {
+        // all KS slices on this wave: step u of a group of KS k-steps is slice u
+        for (int kb0 = kb_lo; kb0 < kb_hi; kb0 += KS) {
+            bf16x8_s wf[KS];
+            bf16x8_s xf[KS][MT];
+#pragma unroll
+            for (int u = 0; u < KS; ++u)
+                if (kb0 + u < kb_hi) wf[u] = __builtin_nontemporal_load(wp + (long)(kb0 + u) * 64);
+#pragma unroll
+            for (int u = 0; u < KS; ++u)
+                if (kb0 + u < kb_hi) load_x<MT>(a.X, a.ldx, a.M, m0, kb0 + u, lane, xf[u]);
+#pragma unroll
+            for (int u = 0; u < KS; ++u)
+                if (kb0 + u < kb_hi)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) acc[u][mt] = mfma16(wf[u], xf[u][mt], acc[u][mt]);
+        }
+#pragma unroll
+        for (int s = 1; s < SPW; ++s)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[0][mt] += acc[s][mt];
     }
 
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[mt];
+    for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[0][mt];
     __syncthreads();
 
     constexpr int OG = (EPI == EPI_GEGLU) ? RG / 2 : RG;  // output groups per block
@@ -176,24 +210,24 @@ int pack_p16(const bf16_t* src, int N, int K, long ld, bf16_t* dst, int NGpad, h
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <int MT, int WPG, int EPI>
+template <int MT, int WPG, int KS, int EPI>
 static void launch_t(const GemmArgs& a, int mblocks, hipStream_t st) {
     constexpr int RG = 4 / WPG;
     dim3 grid((unsigned)(a.NG / RG), (unsigned)a.splits, (unsigned)mblocks);
-    hipLaunchKernelGGL((gemm_p16_kernel<MT, WPG, EPI>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm_p16_kernel<MT, WPG, KS, EPI>), grid, dim3(256), 0, st, a);
 }
 
-template <int MT, int WPG>
+// decode (WPG = KS) and prefill (WPG = 1) instantiate the same slice order
+template <int MT, bool PREFILL>
 static int launch_epi(const GemmArgs& a, int epi, int mblocks, hipStream_t st) {
+    constexpr int W4 = PREFILL ? 1 : 4;
+    constexpr int W2 = PREFILL ? 1 : 2;
     switch (epi) {
-        case EPI_BF16: launch_t<MT, WPG, EPI_BF16>(a, mblocks, st); break;
-        case EPI_BIAS_BF16: launch_t<MT, WPG, EPI_BIAS_BF16>(a, mblocks, st); break;
-        case EPI_BIAS_GELU: launch_t<MT, WPG, EPI_BIAS_GELU>(a, mblocks, st); break;
-        case EPI_GEGLU:
-            if (WPG == 4) return -3;
-            launch_t<MT, WPG == 4 ? 2 : WPG, EPI_GEGLU>(a, mblocks, st);
-            break;
-        case EPI_F32: launch_t<MT, WPG, EPI_F32>(a, mblocks, st); break;
+        case EPI_BF16: launch_t<MT, W4, 4, EPI_BF16>(a, mblocks, st); break;
+        case EPI_BIAS_BF16: launch_t<MT, W4, 4, EPI_BIAS_BF16>(a, mblocks, st); break;
+        case EPI_BIAS_GELU: launch_t<MT, W4, 4, EPI_BIAS_GELU>(a, mblocks, st); break;
+        case EPI_GEGLU: launch_t<MT, W2, 2, EPI_GEGLU>(a, mblocks, st); break;
+        case EPI_F32: launch_t<MT, W4, 4, EPI_F32>(a, mblocks, st); break;
         default: return -4;
     }
     return 0;
@@ -209,18 +243,14 @@ int gemm_p16(const GemmArgs& a_in, int epi, hipStream_t st) {
     if (epi == EPI_GEGLU && a.splits != 1) return -1;
     if (epi != EPI_F32 && a.splits != 1) return -1;
     int rc;
-    if (a.M <= 64) {
-        const int wpg = (epi == EPI_GEGLU) ? 2 : 4;
-        if (a.M <= 16) {
-            rc = wpg == 2 ? launch_epi<1, 2>(a, epi, 1, st) : launch_epi<1, 4>(a, epi, 1, st);
-        } else if (a.M <= 32) {
-            rc = wpg == 2 ? launch_epi<2, 2>(a, epi, 1, st) : launch_epi<2, 4>(a, epi, 1, st);
-        } else {
-            rc = wpg == 2 ? launch_epi<4, 2>(a, epi, 1, st) : launch_epi<4, 4>(a, epi, 1, st);
-        }
+    if (a.M <= 16) {
+        rc = launch_epi<1, false>(a, epi, 1, st);
+    } else if (a.M <= 32) {
+        rc = launch_epi<2, false>(a, epi, 1, st);
+    } else if (a.M <= 64) {
+        rc = launch_epi<4, false>(a, epi, 1, st);
     } else {
-        const int mblocks = (a.M + 63) / 64;
-        rc = launch_epi<4, 1>(a, epi, mblocks, st);
+        rc = launch_epi<4, true>(a, epi, (a.M + 63) / 64, st);
     }
     if (rc) return rc;
     return hipGetLastError() == hipSuccess ? 0 : -2;
