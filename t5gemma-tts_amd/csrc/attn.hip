@@ -19,66 +19,67 @@ namespace t5g {
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float cs[];  // [D/2] cos, [D/2] sin
+    // grid: (token, pair-block); thread = one (head, i) rotation pair (i, i + D/2)
     const int m = blockIdx.x;
     const int D = a.D, H2 = D / 2;
-    const int row = a.tok_row ? a.tok_row[m] : m;
-    const float pos = a.pos[a.tok_row ? m : row];
-    for (int i = threadIdx.x; i < H2; i += blockDim.x) {
-        float ang = a.inv_freq[i] * pos;
-        cs[i] = rbf(cosf(ang));
-        cs[H2 + i] = rbf(sinf(ang));
-    }
-    __syncthreads();
-    const bf16_t* x = a.X ? a.X + (long)m * a.ldx : nullptr;
-    int slot = 0;
-    if (a.nk + a.nv > 0) slot = a.tok_t ? a.tok_t[m] : a.kv_len[row] - 1;
     const int nh = a.nq + a.nk + a.nv;
-    for (int idx = threadIdx.x; idx < nh * H2; idx += blockDim.x) {
-        const int h = idx / H2, i = idx % H2;
-        float x1, x2;
-        if (a.Xpart) {
-            x1 = 0.f;
-            x2 = 0.f;
-            for (int s = 0; s < a.nsplit; ++s) {
+    const int idx = blockIdx.y * blockDim.x + threadIdx.x;
+    if (idx >= nh * H2) return;
+    const int h = idx / H2, i = idx % H2;
+    const int row = a.tok_row ? a.tok_row[m] : m;
+    float x1, x2;
+    if (a.Xpart) {
+        float p1[8], p2[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            if (s < a.nsplit) {
                 const float* ps = a.Xpart + ((long)s * a.M + m) * a.ldx + h * D;
-                x1 += ps[i];
-                x2 += ps[i + H2];
+                p1[s] = ps[i];
+                p2[s] = ps[i + H2];
             }
-            x1 = rbf(x1);
-            x2 = rbf(x2);
-        } else {
-            const bf16_t* xh = x + h * D;
-            x1 = bf2f(xh[i]);
-            x2 = bf2f(xh[i + H2]);
-        }
-        bool isq = h < a.nq, isk = !isq && h < a.nq + a.nk;
-        bool rope = (isq && a.rope_q) || (isk && a.rope_k);
-        float o1 = x1, o2 = x2;
-        if (rope) {
-            float c = cs[i], s = cs[H2 + i];
-            o1 = rbf(rbf(x1 * c) + rbf(-x2 * s));
-            o2 = rbf(rbf(x2 * c) + rbf(x1 * s));
-        }
-        bf16_t* dst;
-        if (isq) {
-            dst = a.Qout + (long)m * a.ldq + h * D;
-        } else if (isk) {
-            dst = a.Kc + row * a.c_bstride + (h - a.nq) * a.c_hstride + (long)slot * D;
-        } else {
-            dst = a.Vc + row * a.c_bstride + (h - a.nq - a.nk) * a.c_hstride + (long)slot * D;
-        }
-        dst[i] = f2bf(o1);
-        dst[i + H2] = f2bf(o2);
+        x1 = 0.f;
+        x2 = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            if (s < a.nsplit) {
+                x1 += p1[s];
+                x2 += p2[s];
+            }
+        x1 = rbf(x1);
+        x2 = rbf(x2);
+    } else {
+        const bf16_t* xh = a.X + (long)m * a.ldx + h * D;
+        x1 = bf2f(xh[i]);
+        x2 = bf2f(xh[i + H2]);
     }
+    const bool isq = h < a.nq, isk = !isq && h < a.nq + a.nk;
+    float o1 = x1, o2 = x2;
+    if ((isq && a.rope_q) || (isk && a.rope_k)) {
+        const float ang = a.inv_freq[i] * a.pos[m];
+        const float c = rbf(cosf(ang)), sn = rbf(sinf(ang));
+        o1 = rbf(rbf(x1 * c) + rbf(-x2 * sn));
+        o2 = rbf(rbf(x2 * c) + rbf(x1 * sn));
+    }
+    bf16_t* dst;
+    if (isq) {
+        dst = a.Qout + (long)m * a.ldq + h * D;
+    } else {
+        const int slot = a.tok_t ? a.tok_t[m] : a.kv_len[row] - 1;
+        dst = (isk ? a.Kc + (h - a.nq) * a.c_hstride : a.Vc + (h - a.nq - a.nk) * a.c_hstride) +
+              row * a.c_bstride + (long)slot * D;
+    }
+    dst[i] = f2bf(o1);
+    dst[i + H2] = f2bf(o2);
 }
 
 int rope_store(const RopeArgs& a, hipStream_t st) {
     if (a.M <= 0) return 0;
     if (a.nq && a.Qout == a.X && a.ldq != a.ldx) return -1;
     if (!a.X && !a.Xpart) return -1;
+    if (a.Xpart && a.nsplit > 8) return -1;
+    const int pairs = (a.nq + a.nk + a.nv) * (a.D / 2);
     // in-place q rope is safe: each (h, i) pair is read and written by one thread
-    hipLaunchKernelGGL(rope_store_kernel, dim3((unsigned)a.M), dim3(256), a.D * sizeof(float), st, a);
+    hipLaunchKernelGGL(rope_store_kernel, dim3((unsigned)a.M, (unsigned)((pairs + 255) / 256)), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -249,24 +250,214 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     }
 }
 
+// Decode-shaped attention (one query row per (row, kv head)): 64 keys per block,
+// every K and V row of the block is requested before the first use (16 B per lane,
+// NIT loads of each in flight), softmax statistics by one wave per head.
+template <int D, int G>
+__global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
+    constexpr int CH = 64;
+    constexpr int LPK = D / 8;
+    constexpr int KPW = 64 / LPK;
+    constexpr int KPB = KPW * 4;
+    constexpr int NIT = CH / KPB;
+    __shared__ float sm[G][CH];
+    __shared__ float stat[G][2];
+    __shared__ f32x4 ored[4][G][LPK][2];
+
+    const int qi = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int kg = lane / LPK, dl = lane % LPK;
+    const int row = a.q_row ? a.q_row[qi] : qi;
+    const int len = a.kv_len[row];
+    const int t = a.q_pos ? a.q_pos[qi] : len - 1;
+    int lo = 0, hi = len;
+    if (a.causal) {
+        hi = min(t + 1, len);
+        if (a.window > 0) lo = max(0, t - a.window + 1);
+    } else if (a.window > 0) {
+        lo = max(0, t - a.window);
+        hi = min(len, t + a.window + 1);
+    }
+    const int c0 = lo + sp * CH;
+    const int c1 = min(hi, c0 + CH);
+    const int n = c1 - c0;
+    float* part = a.part + (((long)qi * a.Hkv + kvh) * a.nsplit + sp) * (G * (D + 2));
+    if (n <= 0) {
+        if (threadIdx.x < G) {
+            part[threadIdx.x * (D + 2)] = -INFINITY;
+            part[threadIdx.x * (D + 2) + 1] = 0.f;
+        }
+        return;
+    }
+    const bf16_t* Kb = a.K + row * a.kv_bstride + kvh * a.kv_hstride;
+    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
+    u32x4 kr[NIT], vr[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        const int j = c0 + i * KPB + wave * KPW + kg;
+        if (j < c1) {
+            kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
+            vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
+        } else {
+            kr[i] = (u32x4){0u, 0u, 0u, 0u};
+            vr[i] = (u32x4){0u, 0u, 0u, 0u};
+        }
+    }
+    float q[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        u32x4 w = *(const u32x4*)(a.Q + (long)qi * a.ldq + (kvh * G + g) * D + 8 * dl);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            q[g][2 * j] = bf_lo(w[j]);
+            q[g][2 * j + 1] = bf_hi(w[j]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        float s[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const float k0 = bf_lo(kr[i][jj]), k1 = bf_hi(kr[i][jj]);
+#pragma unroll
+            for (int g = 0; g < G; ++g) s[g] += q[g][2 * jj] * k0 + q[g][2 * jj + 1] * k1;
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int o = LPK / 2; o > 0; o >>= 1) s[g] += __shfl_xor(s[g], o, 64);
+        const int jl = i * KPB + wave * KPW + kg;
+        if (dl == 0) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) sm[g][jl] = s[g] * a.scale;
+        }
+    }
+    __syncthreads();
+    if (wave < G) {
+        const int g = wave;
+        const float s = lane < n ? sm[g][lane] : -INFINITY;
+        const float mx = wave_max(s);
+        const float e = lane < n ? expf(s - mx) : 0.f;
+        const float l = wave_sum(e);
+        sm[g][lane] = rbf(e);
+        if (lane == 0) {
+            stat[g][0] = mx;
+            stat[g][1] = l;
+        }
+    }
+    __syncthreads();
+    float o[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        const int jl = i * KPB + wave * KPW + kg;
+        if (jl < n) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float p = sm[g][jl];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    o[g][2 * jj] += p * bf_lo(vr[i][jj]);
+                    o[g][2 * jj + 1] += p * bf_hi(vr[i][jj]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+            for (int off = LPK; off < 64; off <<= 1) o[g][jj] += __shfl_xor(o[g][jj], off, 64);
+    if (kg == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            ored[wave][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
+            ored[wave][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
+        }
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
+        const int g = idx / LPK, d8 = idx % LPK;
+        const f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
+        const f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
+        if (a.nsplit > 1) {
+            float* pg = part + g * (D + 2);
+            if (d8 == 0) {
+                pg[0] = stat[g][0];
+                pg[1] = stat[g][1];
+            }
+            *(f32x4*)(pg + 2 + 8 * d8) = lo4;
+            *(f32x4*)(pg + 6 + 8 * d8) = hi4;
+        } else {
+            const float inv = 1.0f / stat[g][1];
+            u32x4 w;
+            w[0] = pack2(lo4[0] * inv, lo4[1] * inv);
+            w[1] = pack2(lo4[2] * inv, lo4[3] * inv);
+            w[2] = pack2(hi4[0] * inv, hi4[1] * inv);
+            w[3] = pack2(hi4[2] * inv, hi4[3] * inv);
+            *(u32x4*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 8 * d8) = w;
+        }
+    }
+}
+
+// merge of the key-split partials: O = sum_z e^(m_z - M) o_z / sum_z e^(m_z - M) l_z
 template <int D, int G>
 __global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a) {
+    __shared__ float wz[G][64];
+    __shared__ float Linv[G];
     const int qi = blockIdx.x, kvh = blockIdx.y;
-    const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2));
-    for (int idx = threadIdx.x; idx < G * D; idx += 256) {
-        const int g = idx / D, d = idx % D;
-        float M = -INFINITY;
-        for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, base[(long)s * G * (D + 2) + g * (D + 2)]);
-        float L = 0.f, O = 0.f;
-        for (int s = 0; s < a.nsplit; ++s) {
-            const float* p = base + (long)s * G * (D + 2) + g * (D + 2);
-            if (p[0] == -INFINITY) continue;
-            float f = expf(p[0] - M);
-            L += f * p[1];
-            O += f * p[2 + d];
-        }
-        a.O[(long)qi * a.ldo + (kvh * G + g) * D + d] = f2bf(O * (1.0f / L));
+    const int S = a.nsplit;
+    const float* base = a.part + ((long)qi * a.Hkv + kvh) * S * (G * (D + 2));
+    if (threadIdx.x < 64 * G) {
+        const int g = threadIdx.x / 64, z = threadIdx.x % 64;
+        const float m = z < S ? base[(long)z * G * (D + 2) + g * (D + 2)] : -INFINITY;
+        const float l = z < S ? base[(long)z * G * (D + 2) + g * (D + 2) + 1] : 0.f;
+        const float M = wave_max(m);
+        const float w = (m == -INFINITY) ? 0.f : expf(m - M);
+        const float L = wave_sum(w * l);
+        wz[g][z] = w;
+        if (z == 0) Linv[g] = 1.0f / L;
     }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < G * D / 4; idx += 256) {
+        const int g = idx / (D / 4), d4 = idx % (D / 4);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int z = 0; z < S; ++z) {
+            const float w = wz[g][z];
+            if (w != 0.f) acc += w * *(const f32x4*)(base + (long)z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
+        }
+        const float inv = Linv[g];
+        uint2 o;
+        o.x = pack2(acc[0] * inv, acc[1] * inv);
+        o.y = pack2(acc[2] * inv, acc[3] * inv);
+        *(uint2*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 4 * d4) = o;
+    }
+}
+
+template <int D, int G>
+static int launch_decode(const AttnArgs& a, hipStream_t st) {
+    dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
+    hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, a);
+    if (a.nsplit > 1)
+        hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv), dim3(256), 0,
+                           st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int attention_decode(const AttnArgs& a, hipStream_t st) {
+    if (a.Mq <= 0) return 0;
+    if (a.nsplit < 1 || a.nsplit > 64 || !a.part || a.eager) return -1;
+    if (a.D == 256 && a.G == 2) return launch_decode<256, 2>(a, st);
+    if (a.D == 64 && a.G == 2) return launch_decode<64, 2>(a, st);
+    if (a.D == 128 && a.G == 2) return launch_decode<128, 2>(a, st);
+    if (a.D == 256 && a.G == 1) return launch_decode<256, 1>(a, st);
+    return -3;
 }
 
 template <int D, int G>

@@ -113,7 +113,7 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     const t5g_config& c = *cfg;
     if (c.hidden % 32 || c.intermediate % 32 || c.n_enc_layers > T5G_MAX_LAYERS ||
         c.n_dec_layers > T5G_MAX_LAYERS || c.max_batch <= 0 || c.max_text <= 0 || c.max_audio <= 0 ||
-        c.n_heads % c.n_kv_heads)
+        c.n_heads % c.n_kv_heads || c.max_audio > 4096 || c.max_text > 4096)
         return T5G_EINVAL;
     t5g_engine* e = new t5g_engine();
     e->c = c;
@@ -142,8 +142,9 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     e->part_elems = (int64_t)8 * B * widest(widest(d, e->qkv_dim), 2 * e->kv_dim);
     rc |= alloc(e, &e->part, e->part_elems);
     const int G = c.n_heads / c.n_kv_heads;
-    const int nsplit_dec = (c.max_audio + 127) / 128;
-    e->apart_elems = (int64_t)B * Hkv * nsplit_dec * G * (D + 2);
+    const int nsplit_dec = (c.max_audio + 63) / 64;
+    const int nsplit_x = (c.max_text + 63) / 64;
+    e->apart_elems = (int64_t)B * Hkv * (nsplit_dec > nsplit_x ? nsplit_dec : nsplit_x) * G * (D + 2);
     rc |= alloc(e, &e->apart, e->apart_elems);
     const int64_t enc_cache = (int64_t)B * Hkv * c.max_text * D;
     rc |= alloc(e, &e->enc_k, enc_cache);
@@ -419,17 +420,18 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             a.scale = c.attn_scale;
             a.softcap = c.softcap;
             a.eager = c.softcap > 0.f;
+            a.O = att;
+            a.ldo = e->q_dim;
             if (decode && !a.eager) {
-                a.chunk = 128;
-                a.nsplit = (c.max_audio + 127) / 128;
+                a.chunk = 64;
+                a.nsplit = (c.max_audio + 63) / 64;
                 a.part = e->apart;
+                RC(attention_decode(a, st));
             } else {
                 a.nsplit = 1;
                 a.chunk = c.max_audio;
+                RC(attention(a, st));
             }
-            a.O = att;
-            a.ldo = e->q_dim;
-            RC(attention(a, st));
         }
         RC(gemm(att, e->q_dim, M, L.o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
                 s_o > 1 ? EPI_F32 : EPI_BF16, st));
@@ -491,11 +493,18 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             a.scale = c.attn_scale;
             a.softcap = c.softcap;
             a.eager = c.softcap > 0.f;
-            a.nsplit = 1;
-            a.chunk = c.max_text;
             a.O = att;
             a.ldo = e->q_dim;
-            RC(attention(a, st));
+            if (decode && !a.eager) {
+                a.chunk = 64;
+                a.nsplit = (c.max_text + 63) / 64;
+                a.part = e->apart;
+                RC(attention_decode(a, st));
+            } else {
+                a.nsplit = 1;
+                a.chunk = c.max_text;
+                RC(attention(a, st));
+            }
         }
         RC(gemm(att, e->q_dim, M, L.cross_o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
                 s_o > 1 ? EPI_F32 : EPI_BF16, st));

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
     static_assert(WPG == KS || WPG == 1, "slice mapping");
     constexpr int RG = 4 / WPG;  // row groups per block
     constexpr int SPW = KS / WPG;  // slices per wave
-    constexpr int UN = (WPG == 1) ? KS : 4;  // k-steps in flight per wave per iteration
+    constexpr int UN = (WPG == 1) ? KS : 8;  // k-steps in flight per wave per iteration
     __shared__ f32x4 red[4][MT][64];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;

@@ -16,19 +16,25 @@
 //      bf16-rounded prefix (torch CPU cumsum on bf16) is reproduced exactly
 //      without sorting. Only if the cut falls INSIDE a tie group does the member
 //      order matter (torch.sort's libstdc++ std::sort order); the kernel keeps the
-//      lowest indices and counts the step as ``ambiguous`` (parity mode resolves
-//      such steps on the host).
+//      lowest indices and flags the step ``ambiguous`` (parity mode re-runs such
+//      steps with t5g_host_sample).
 //   7. token = first argmax of bf16(bf16(softmax(x)) / q), q = the exponential
 //      draw torch.multinomial makes (parity: uploaded; production: Philox4x32-10)
 //   8. force-stop / time budget / silence-run state; next PM position computed in
 //      double like the reference's Python float math (:817-823).
+// The row's logits live in LDS as packed bf16 pairs (133 KB of the CU's 160 KB):
+// every transform above rounds to bf16, so nothing is lost; thread t owns pairs
+// t + 1024 * jp, i.e. elements 2 * (t + 1024 * jp) + {0, 1}.
 #include "common.h"
 #include "t5g_kernels.h"
 
 namespace t5g {
 
 constexpr int SN = 1024;
-constexpr int SPER = 65;  // V <= SN * SPER = 66560
+constexpr int NW = SN / 64;
+constexpr int SPER = 66;                // V <= SN * SPER = 67584
+constexpr int SP2 = (SPER + 1) / 2;     // packed pairs
+constexpr int TIE_CAP = 256;
 
 __device__ __forceinline__ uint32_t okey(float v) {
     uint32_t b = (uint32_t)f2bf(v);
@@ -39,7 +45,21 @@ __device__ __forceinline__ float key2f(uint32_t k) {
     return bf2f(b);
 }
 
-// (value, index) arg-max with first-index tie break; red2 holds 2*32 words
+// element j (0..SPER-1) of thread t: pair jp = j >> 1, half j & 1 -> index 2*(t + SN*jp) + (j&1)
+struct Packed {
+    uint32_t* w;  // LDS base of this thread's pairs, stride SN
+    __device__ __forceinline__ float get(int j) const {
+        const uint32_t p = w[(j >> 1) * SN];
+        return (j & 1) ? bf_hi(p) : bf_lo(p);
+    }
+    __device__ __forceinline__ void set(int j, float v) {
+        const uint32_t b = f2bf(v);
+        uint32_t& p = w[(j >> 1) * SN];
+        p = (j & 1) ? ((p & 0xffffu) | (b << 16)) : ((p & 0xffff0000u) | b);
+    }
+};
+__device__ __forceinline__ int eidx(int tid, int j) { return 2 * (tid + SN * (j >> 1)) + (j & 1); }
+
 __device__ __forceinline__ int block_argmax(float v, int idx, float* redv, int* redi) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -53,25 +73,70 @@ __device__ __forceinline__ int block_argmax(float v, int idx, float* redv, int* 
     __syncthreads();
     float bv = redv[0];
     int bi = redi[0];
-    for (int i = 1; i < SN / 64; ++i) {
+    for (int i = 1; i < NW; ++i)
         if (redv[i] > bv || (redv[i] == bv && redi[i] < bi)) { bv = redv[i]; bi = redi[i]; }
-    }
     return bi;
 }
 
 __device__ __forceinline__ int block_count(int c, int* redi) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    c = wave_sum(c);
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     __syncthreads();
     if (l == 0) redi[w] = c;
     __syncthreads();
     int s = 0;
-    for (int i = 0; i < SN / 64; ++i) s += redi[i];
+    for (int i = 0; i < NW; ++i) s += redi[i];
     return s;
 }
 
-// Philox4x32-10 -> one uint32 per (seed, row, step, index)
+// Sum the per-wave histograms into hsum (all threads call).
+__device__ __forceinline__ void hist_reduce(unsigned (*wh)[256], unsigned* hsum) {
+    __syncthreads();
+    if (threadIdx.x < 256) {
+        unsigned s = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s += wh[w][threadIdx.x];
+        hsum[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ void hist_clear(unsigned (*wh)[256]) {
+    for (int i = threadIdx.x; i < NW * 256; i += SN) (&wh[0][0])[i] = 0;
+    __syncthreads();
+}
+
+// Wave 0: bin b (descending from 255) where the running count from the top first
+// reaches k; writes sel = b and above = count strictly above b.
+__device__ __forceinline__ void find_bin_wave0(const unsigned* h, int k, int* sel, int* above) {
+    const int l = threadIdx.x;  // lane of wave 0; covers bins 255-4l .. 252-4l
+    int c[4];
+    int loc = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        c[r] = (int)h[255 - 4 * l - r];
+        loc += c[r];
+    }
+    int inc = loc;  // inclusive scan over lanes (lane 0 = top bins)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(inc, o, 64);
+        if (l >= o) inc += t;
+    }
+    const int exc = inc - loc;
+    const unsigned long long hit = __ballot(inc >= k);
+    const int first = hit ? __ffsll((long long)hit) - 1 : 63;
+    if (l == first) {
+        int run = exc, b = 255 - 4 * l - 3;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (run + c[r] >= k) { b = 255 - 4 * l - r; break; }
+            run += c[r];
+        }
+        *sel = b;
+        *above = run;
+    }
+}
+
 __device__ __forceinline__ uint32_t philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0, uint32_t k1) {
     uint32_t c3 = 0x9E3779B9u;
 #pragma unroll
@@ -89,28 +154,40 @@ __device__ __forceinline__ uint32_t philox(uint32_t c0, uint32_t c1, uint32_t c2
 }
 
 __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
-    __shared__ float redv[32];
-    __shared__ int redi[32];
-    __shared__ unsigned hist[256];
-    __shared__ unsigned hist2[256];
-    __shared__ unsigned eqmask[(SN * SPER + 31) / 32];
+    __shared__ float redv[NW];
+    __shared__ int redi[NW];
+    __shared__ unsigned wh[NW][256];
+    __shared__ unsigned hsum[256];
+    __shared__ float gval[256];     // compact list of distinct values of one coarse bin
+    __shared__ int gcnt[256];
+    __shared__ int tie_idx[TIE_CAP];
+    __shared__ uint32_t xs[SN * SP2];
     __shared__ int sh_int[8];
     __shared__ float sh_f[4];
 
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
     SamplerState st = a.state[b];
     if (st.done) return;
     const SamplerRow pr = a.rows[b];
     const int V = a.V;
     const bf16_t* lg = a.logits + (long)b * a.ldl;
 
-    float x[SPER];
+    Packed x{xs + tid};
 #pragma unroll
-    for (int j = 0; j < SPER; ++j) {
-        int i = tid + SN * j;
-        x[j] = i < V ? bf2f(lg[i]) : -INFINITY;
+    for (int jp = 0; jp < SP2; ++jp) {
+        const int i = 2 * (tid + SN * jp);
+        uint32_t w;
+        if (i + 1 < V && ((a.ldl & 1) == 0)) {
+            w = *(const uint32_t*)(lg + i);
+        } else {
+            const uint32_t lo = i < V ? lg[i] : 0xff80u, hi = i + 1 < V ? lg[i + 1] : 0xff80u;
+            w = lo | (hi << 16);
+        }
+        xs[tid + SN * jp] = w;
     }
+    __syncthreads();
     // ---- 1. edits (:717-742)
     const int eff_len = max(0, st.current_length - st.prompt_offset);
     int kk = pr.top_k;
@@ -119,16 +196,19 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
     for (int s = 0; s < pr.n_silence; ++s) in_sil_prev |= (a.silence[pr.silence_off + s] == st.prev_token);
     const bool sil_rule = pr.stop_repetition > 0 && in_sil_prev && st.consec_silence > pr.stop_repetition;
     const float sil_f = (float)(st.consec_silence - (pr.stop_repetition - 1));
-#pragma unroll
-    for (int j = 0; j < SPER; ++j) {
-        const int i = tid + SN * j;
-        if (i == a.eos) {
-            if (eff_len == 0) x[j] = rbf(-1e9f);
-            if (st.cur_num_gen <= a.eos_guard) x[j] = rbf(-10000.0f);
-            if (pr.eos_disabled) x[j] = -INFINITY;
+    if (tid == 0) {
+        bf16_t* xh = (bf16_t*)xs;  // element index i lives at half-word i of the pair array
+        float v = bf2f(xh[a.eos]);
+        if (eff_len == 0) v = rbf(-1e9f);
+        if (st.cur_num_gen <= a.eos_guard) v = rbf(-10000.0f);
+        if (pr.eos_disabled) v = -INFINITY;
+        xh[a.eos] = f2bf(v);
+        if (sil_rule && st.prev_token >= 0 && st.prev_token < V) {
+            const float u = bf2f(xh[st.prev_token]);
+            xh[st.prev_token] = f2bf(u < 0.f ? u * sil_f : u / sil_f);
         }
-        if (sil_rule && i == st.prev_token) x[j] = x[j] < 0.f ? rbf(x[j] * sil_f) : rbf(x[j] / sil_f);
     }
+    __syncthreads();
     // ---- 2. argmax of the edited logits (:753-755)
     int amax;
     {
@@ -136,37 +216,38 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
         int bi = 0x7fffffff;
 #pragma unroll
         for (int j = 0; j < SPER; ++j) {
-            const int i = tid + SN * j;
-            if (i < V && (x[j] > bv || bi == 0x7fffffff)) { bv = x[j]; bi = i; }
+            const int i = eidx(tid, j);
+            const float v = x.get(j);
+            if (i < V && (v > bv || bi == 0x7fffffff)) { bv = v; bi = i; }
         }
         amax = block_argmax(bv, bi, redv, redi);
     }
     // ---- 3. temperature
     if (pr.temperature != 1.0f) {
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) x[j] = rbf(x[j] / pr.temperature);
+        for (int j = 0; j < SPER; ++j) x.set(j, x.get(j) / pr.temperature);
     }
     float top_p = pr.top_p;
     // ---- 4. min_p (:92-99)
     if (pr.min_p > 0.f && pr.min_p < 1.f) {
         float lm = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) lm = fmaxf(lm, x[j]);
+        for (int j = 0; j < SPER; ++j) lm = fmaxf(lm, x.get(j));
         const float m = block_max(lm, redv);
         float ls = 0.f;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) ls += expf(x[j] - m);
+        for (int j = 0; j < SPER; ++j) ls += expf(x.get(j) - m);
         const float inv = 1.0f / block_sum(ls, redv);
         const float thr = rbf(pr.min_p);
         int rm = 0;
 #pragma unroll
         for (int j = 0; j < SPER; ++j)
-            if (tid + SN * j < V) rm += (rbf(expf(x[j] - m) * inv) < thr) ? 1 : 0;
+            if (eidx(tid, j) < V) rm += (rbf(expf(x.get(j) - m) * inv) < thr) ? 1 : 0;
         const int removed = block_count(rm, redi);
         if (removed < V) {
 #pragma unroll
             for (int j = 0; j < SPER; ++j)
-                if (rbf(expf(x[j] - m) * inv) < thr) x[j] = -INFINITY;
+                if (rbf(expf(x.get(j) - m) * inv) < thr) x.set(j, -INFINITY);
             kk = 0;
             top_p = 1.0f;
         }
@@ -174,140 +255,156 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
     // ---- 5. top-k threshold (k-th largest, ties kept) (:101-105)
     if (kk > 0) {
         const int k = min(kk, V);
-        for (int i = tid; i < 256; i += SN) hist[i] = 0;
-        __syncthreads();
+        hist_clear(wh);
 #pragma unroll
         for (int j = 0; j < SPER; ++j)
-            if (tid + SN * j < V) atomicAdd(&hist[okey(x[j]) >> 8], 1u);
-        __syncthreads();
-        if (tid == 0) {
-            int above = 0, bsel = 0;
-            for (int bb = 255; bb >= 0; --bb) {
-                if (above + (int)hist[bb] >= k) { bsel = bb; break; }
-                above += hist[bb];
-            }
-            sh_int[0] = bsel;
-            sh_int[1] = k - above;
-        }
-        for (int i = tid; i < 256; i += SN) hist2[i] = 0;
+            if (eidx(tid, j) < V) atomicAdd(&wh[wid][okey(x.get(j)) >> 8], 1u);
+        hist_reduce(wh, hsum);
+        if (wid == 0) find_bin_wave0(hsum, k, &sh_int[0], &sh_int[1]);
         __syncthreads();
         const uint32_t hb = (uint32_t)sh_int[0];
+        const int need = k - sh_int[1];
+        hist_clear(wh);
 #pragma unroll
         for (int j = 0; j < SPER; ++j)
-            if (tid + SN * j < V) {
-                uint32_t kq = okey(x[j]);
-                if ((kq >> 8) == hb) atomicAdd(&hist2[kq & 255u], 1u);
+            if (eidx(tid, j) < V) {
+                const uint32_t kq = okey(x.get(j));
+                if ((kq >> 8) == hb) atomicAdd(&wh[wid][kq & 255u], 1u);
             }
+        hist_reduce(wh, hsum);
+        if (wid == 0) find_bin_wave0(hsum, need, &sh_int[2], &sh_int[3]);
         __syncthreads();
-        if (tid == 0) {
-            int need = sh_int[1], above = 0, lsel = 0;
-            for (int bb = 255; bb >= 0; --bb) {
-                if (above + (int)hist2[bb] >= need) { lsel = bb; break; }
-                above += hist2[bb];
-            }
-            sh_f[0] = key2f((hb << 8) | (uint32_t)lsel);
-        }
-        __syncthreads();
-        const float thr = sh_f[0];
+        const float thr = key2f((hb << 8) | (uint32_t)sh_int[2]);
 #pragma unroll
         for (int j = 0; j < SPER; ++j)
-            if (x[j] < thr) x[j] = -INFINITY;
+            if (x.get(j) < thr) x.set(j, -INFINITY);
     }
     // ---- 6. top-p (:118-129)
     int ambiguous = 0;
     if (top_p < 1.0f) {
         float lm = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) lm = fmaxf(lm, x[j]);
+        for (int j = 0; j < SPER; ++j) lm = fmaxf(lm, x.get(j));
         const float m = block_max(lm, redv);
         float ls = 0.f;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) ls += expf(x[j] - m);
+        for (int j = 0; j < SPER; ++j) ls += expf(x.get(j) - m);
         const float inv = 1.0f / block_sum(ls, redv);
         const float thr = rbf(top_p);
-        for (int i = tid; i < 256; i += SN) hist[i] = 0;
-        __syncthreads();
+        hist_clear(wh);
 #pragma unroll
-        for (int j = 0; j < SPER; ++j)
-            if (x[j] > -INFINITY) atomicAdd(&hist[okey(x[j]) >> 8], 1u);
-        __syncthreads();
-        // walk high bins from the top; sh_int[2] = state (0 walking, 1 cut found, 2 exhausted)
-        float acc = 0.f;  // meaningful in thread 0 only
-        if (tid == 0) { sh_int[2] = 0; sh_int[3] = 255; }
+        for (int j = 0; j < SPER; ++j) {
+            const float v = x.get(j);
+            if (v > -INFINITY) atomicAdd(&wh[wid][okey(v) >> 8], 1u);
+        }
+        hist_reduce(wh, hsum);
+        __shared__ unsigned coarse[256];
+        if (tid < 256) coarse[tid] = hsum[tid];
+        if (tid == 0) {
+            sh_int[4] = 0;      // state: 0 walking, 1 cut found, 2 exhausted
+            sh_int[5] = 255;    // next coarse bin to visit
+            sh_f[0] = 0.f;      // running fp32 cumsum
+        }
         __syncthreads();
         while (true) {
-            if (tid == 0 && sh_int[2] == 0) {
-                int bb = sh_int[3];
-                while (bb >= 0 && hist[bb] == 0) --bb;
-                if (bb < 0) sh_int[2] = 2;
-                sh_int[3] = bb;
+            if (tid == 0 && sh_int[4] == 0) {
+                int bb = sh_int[5];
+                while (bb >= 0 && coarse[bb] == 0) --bb;
+                if (bb < 0) sh_int[4] = 2;
+                sh_int[5] = bb;
             }
-            for (int i = tid; i < 256; i += SN) hist2[i] = 0;
-            __syncthreads();
-            if (sh_int[2] != 0) break;
-            const uint32_t hb = (uint32_t)sh_int[3];
+            hist_clear(wh);  // (has a barrier)
+            if (sh_int[4] != 0) break;
+            const uint32_t hb = (uint32_t)sh_int[5];
 #pragma unroll
-            for (int j = 0; j < SPER; ++j)
-                if (x[j] > -INFINITY) {
-                    uint32_t kq = okey(x[j]);
-                    if ((kq >> 8) == hb) atomicAdd(&hist2[kq & 255u], 1u);
+            for (int j = 0; j < SPER; ++j) {
+                const float v = x.get(j);
+                if (v > -INFINITY) {
+                    const uint32_t kq = okey(v);
+                    if ((kq >> 8) == hb) atomicAdd(&wh[wid][kq & 255u], 1u);
                 }
+            }
+            hist_reduce(wh, hsum);
+            if (wid == 0) {  // compact the non-empty fine bins, descending
+                int c[4];
+                int loc = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    c[r] = hsum[255 - 4 * lane - r] ? 1 : 0;
+                    loc += c[r];
+                }
+                int inc = loc;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    int t = __shfl_up(inc, o, 64);
+                    if (lane >= o) inc += t;
+                }
+                int pos = inc - loc;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int lb = 255 - 4 * lane - r;
+                    if (c[r]) {
+                        gval[pos] = key2f((hb << 8) | (uint32_t)lb);
+                        gcnt[pos] = (int)hsum[lb];
+                        ++pos;
+                    }
+                }
+                if (lane == 63) sh_int[6] = inc;
+            }
             __syncthreads();
             if (tid == 0) {
-                for (int lb = 255; lb >= 0 && sh_int[2] == 0; --lb) {
-                    const int c = (int)hist2[lb];
-                    if (c == 0) continue;
-                    const float v = key2f((hb << 8) | (uint32_t)lb);
+                float acc = sh_f[0];
+                const int ng = sh_int[6];
+                for (int q = 0; q < ng && sh_int[4] == 0; ++q) {
+                    const float v = gval[q];
+                    const int c = gcnt[q];
                     const float pv = rbf(expf(v - m) * inv);
                     for (int r = 0; r < c; ++r) {
                         acc += pv;
                         if (rbf(acc) > thr) {
-                            sh_int[2] = 1;
-                            sh_f[1] = v;           // cut value
-                            sh_int[4] = r + 1;     // members of the cut group kept
-                            sh_int[5] = c;         // group size
+                            sh_int[4] = 1;
+                            sh_f[1] = v;      // cut value
+                            sh_int[1] = r + 1;  // members of the cut group kept
+                            sh_int[2] = c;      // group size
                             break;
                         }
                     }
                 }
-                sh_int[3] = sh_int[3] - 1;
+                sh_f[0] = acc;
+                sh_int[5] = sh_int[5] - 1;
             }
             __syncthreads();
         }
-        if (sh_int[2] == 1) {
+        if (sh_int[4] == 1) {
             const float vc = sh_f[1];
-            const int keep = sh_int[4], gsz = sh_int[5];
+            const int keep = sh_int[1], gsz = sh_int[2];
 #pragma unroll
             for (int j = 0; j < SPER; ++j)
-                if (x[j] < vc) x[j] = -INFINITY;
+                if (x.get(j) < vc) x.set(j, -INFINITY);
             if (keep < gsz) {
+                // production tie-break: keep the `keep` lowest indices of the tie group
                 ambiguous = 1;
-                for (int i = tid; i < (SN * SPER + 31) / 32; i += SN) eqmask[i] = 0;
+                if (tid == 0) sh_int[7] = 0;
                 __syncthreads();
 #pragma unroll
                 for (int j = 0; j < SPER; ++j) {
-                    const int i = tid + SN * j;
-                    if (x[j] == vc) atomicOr(&eqmask[i >> 5], 1u << (i & 31));
-                }
-                __syncthreads();
-                if (tid == 0) {  // keep the lowest `keep` indices of the tie group
-                    int left = keep;
-                    for (int w = 0; w < (V + 31) / 32; ++w) {
-                        unsigned bits = eqmask[w];
-                        unsigned out = 0;
-                        while (bits) {
-                            unsigned lowb = bits & (~bits + 1u);
-                            if (left > 0) { out |= lowb; --left; }
-                            bits &= bits - 1u;
-                        }
-                        eqmask[w] = out;
+                    const int i = eidx(tid, j);
+                    if (x.get(j) == vc) {
+                        const int p = atomicAdd(&sh_int[7], 1);
+                        if (p < TIE_CAP) tie_idx[p] = i;
                     }
                 }
                 __syncthreads();
+                const int cnt = min(sh_int[7], TIE_CAP);
+                // rank of each collected member = #members with a smaller index
 #pragma unroll
                 for (int j = 0; j < SPER; ++j) {
-                    const int i = tid + SN * j;
-                    if (x[j] == vc && !((eqmask[i >> 5] >> (i & 31)) & 1u)) x[j] = -INFINITY;
+                    const int i = eidx(tid, j);
+                    if (x.get(j) == vc) {
+                        int rank = 0;
+                        for (int q = 0; q < cnt; ++q) rank += tie_idx[q] < i;
+                        if (rank >= keep) x.set(j, -INFINITY);
+                    }
                 }
             }
         }
@@ -317,20 +414,20 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
     {
         float lm = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) lm = fmaxf(lm, x[j]);
+        for (int j = 0; j < SPER; ++j) lm = fmaxf(lm, x.get(j));
         const float m = block_max(lm, redv);
         float ls = 0.f;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) ls += expf(x[j] - m);
+        for (int j = 0; j < SPER; ++j) ls += expf(x.get(j) - m);
         const float inv = 1.0f / block_sum(ls, redv);
         const bf16_t* nz = a.noise ? a.noise + ((long)b * a.noise_steps + st.cur_num_gen) * V : nullptr;
         float bv = -1.f;
         int bi = 0x7fffffff;
 #pragma unroll
         for (int j = 0; j < SPER; ++j) {
-            const int i = tid + SN * j;
+            const int i = eidx(tid, j);
             if (i >= V) continue;
-            const float p = rbf(expf(x[j] - m) * inv);
+            const float p = rbf(expf(x.get(j) - m) * inv);
             float r = 0.f;
             if (p > 0.f) {
                 float q;

@@ -85,6 +85,8 @@ struct AttnArgs {
     int ldo;
 };
 int attention(const AttnArgs& a, hipStream_t st);
+// decode-shaped (64-key blocks, split over blockIdx.z, sdpa numerics); nsplit = ceil(keys/64)
+int attention_decode(const AttnArgs& a, hipStream_t st);
 
 // ---- sampler -------------------------------------------------------------------
 struct SamplerRow {           // per-utterance parameters (device)

@@ -1,0 +1,4 @@
+source tools/gpu_run.sh
+rm -f gpurun_out/summary.txt
+export TMPDIR=/tmp
+run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
