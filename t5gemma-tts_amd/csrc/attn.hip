@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
 #pragma unroll
         for (int s = 0; s < 8; ++s)
             if (s < a.nsplit) {
-                const float* ps = a.Xpart + ((long)s * a.M + m) * a.ldx + h * D;
+                const float* ps = a.Xpart + ((long)s * a.M + m) * a.ldx + a.col0 + h * D;
                 p1[s] = ps[i];
                 p2[s] = ps[i + H2];
             }
@@ -48,15 +48,22 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
         x1 = rbf(x1);
         x2 = rbf(x2);
     } else {
-        const bf16_t* xh = a.X + (long)m * a.ldx + h * D;
+        const bf16_t* xh = a.X + (long)m * a.ldx + a.col0 + h * D;
         x1 = bf2f(xh[i]);
         x2 = bf2f(xh[i + H2]);
     }
     const bool isq = h < a.nq, isk = !isq && h < a.nq + a.nk;
     float o1 = x1, o2 = x2;
     if ((isq && a.rope_q) || (isk && a.rope_k)) {
-        const float ang = a.inv_freq[i] * a.pos[m];
-        const float c = rbf(cosf(ang)), sn = rbf(sinf(ang));
+        float c, sn;
+        if (a.rope_tab) {
+            c = a.rope_tab[(long)row * D + i];
+            sn = a.rope_tab[(long)row * D + H2 + i];
+        } else {
+            const float ang = a.inv_freq[i] * a.pos[m];
+            c = rbf(cosf(ang));
+            sn = rbf(sinf(ang));
+        }
         o1 = rbf(rbf(x1 * c) + rbf(-x2 * sn));
         o2 = rbf(rbf(x2 * c) + rbf(x1 * sn));
     }
@@ -70,6 +77,21 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
     }
     dst[i] = f2bf(o1);
     dst[i + H2] = f2bf(o2);
+}
+
+__global__ void rope_table_kernel(const float* pos, const float* inv_freq, int D, float* tab) {
+    const int r = blockIdx.x, H2 = D / 2;
+    for (int i = threadIdx.x; i < H2; i += blockDim.x) {
+        const float ang = inv_freq[i] * pos[r];
+        tab[(long)r * D + i] = rbf(cosf(ang));
+        tab[(long)r * D + H2 + i] = rbf(sinf(ang));
+    }
+}
+
+int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st) {
+    if (rows <= 0) return 0;
+    hipLaunchKernelGGL(rope_table_kernel, dim3((unsigned)rows), dim3(128), 0, st, pos, inv_freq, D, tab);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int rope_store(const RopeArgs& a, hipStream_t st) {
@@ -253,8 +275,57 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 // Decode-shaped attention (one query row per (row, kv head)): 64 keys per block,
 // every K and V row of the block is requested before the first use (16 B per lane,
 // NIT loads of each in flight), softmax statistics by one wave per head.
+// Fusions: (1) q may come straight from the q-projection's fp32 split-K slabs; the
+// block sums them, rounds to bf16 and applies the float-position PM-RoPE with a
+// lane shuffle (rotate_half partner = lane ^ LPK/2), bit-identical to
+// rope_store_kernel; (2) the key-split partials are merged in the same launch by
+// the last-arriving block of each (row, kv head) (agent-scope release/acquire
+// ticket, CDNA guide G16), so no combine launch.
 template <int D, int G>
-__global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
+__device__ __forceinline__ void merge_splits(const AttnArgs& a, const float* base, int qi, int kvh, float* wz,
+                                             float* Linv) {
+    constexpr int ZMAX = 16;  // splits held in registers; more are streamed
+    const int S = a.nsplit;
+    // every thread owns <= 1 (g, d4) quad when G*D/4 <= blockDim (D = 256, G = 2: 128 quads)
+    const int idx = threadIdx.x;
+    const bool own = idx < G * D / 4;
+    const int g = own ? idx / (D / 4) : 0, d4 = own ? idx % (D / 4) : 0;
+    f32x4 pv[ZMAX];
+#pragma unroll
+    for (int z = 0; z < ZMAX; ++z)
+        if (own && z < S) pv[z] = *(const f32x4*)(base + (long)z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
+    if (threadIdx.x < 64 * G) {
+        const int gg = threadIdx.x / 64, z = threadIdx.x % 64;
+        const float m = z < S ? base[(long)z * G * (D + 2) + gg * (D + 2)] : -INFINITY;
+        const float l = z < S ? base[(long)z * G * (D + 2) + gg * (D + 2) + 1] : 0.f;
+        const float M = wave_max(m);
+        const float w = (m == -INFINITY) ? 0.f : expf(m - M);
+        const float L = wave_sum(w * l);
+        wz[gg * 64 + z] = w;
+        if (z == 0) Linv[gg] = 1.0f / L;
+    }
+    __syncthreads();
+    if (!own) return;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int z = 0; z < ZMAX; ++z)
+        if (z < S) {
+            const float w = wz[g * 64 + z];
+            if (w != 0.f) acc += w * pv[z];
+        }
+    for (int z = ZMAX; z < S; ++z) {
+        const float w = wz[g * 64 + z];
+        if (w != 0.f) acc += w * *(const f32x4*)(base + (long)z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
+    }
+    const float inv = Linv[g];
+    uint2 o;
+    o.x = pack2(acc[0] * inv, acc[1] * inv);
+    o.y = pack2(acc[2] * inv, acc[3] * inv);
+    *(uint2*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 4 * d4) = o;
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     constexpr int CH = 64;
     constexpr int LPK = D / 8;
     constexpr int KPW = 64 / LPK;
@@ -263,11 +334,94 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
     __shared__ float sm[G][CH];
     __shared__ float stat[G][2];
     __shared__ f32x4 ored[4][G][LPK][2];
+    __shared__ float wz[G * 64];
+    __shared__ float Linv[G];
+    __shared__ int last_flag;
 
     const int qi = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int kg = lane / LPK, dl = lane % LPK;
     const int row = a.q_row ? a.q_row[qi] : qi;
+    const bf16_t* Kb = a.K + row * a.kv_bstride + kvh * a.kv_hstride;
+    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
+    // Without a sliding window the block's keys start at sp*CH whatever the row
+    // length: request K/V before kv_len arrives (one memory round trip per block).
+    const bool spec = a.window == 0;
+    u32x4 kr[NIT], vr[NIT];
+    if (spec) {
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int j = sp * CH + i * KPB + wave * KPW + kg;
+            if (j < a.kv_cap) {
+                kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
+                vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
+            }
+        }
+    }
+    // q (+ PM-RoPE) does not depend on the row length either: load it now too
+    float q[G][8];
+    if (a.Qpart) {
+        float c8[8], s8[8];
+        if (a.rope_tab) {
+            const float* tr = a.rope_tab + (long)row * D;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const int fi = (8 * dl + jj) % (D / 2);
+                c8[jj] = tr[fi];
+                s8[jj] = tr[D / 2 + fi];
+            }
+        } else {
+            const float ps = a.pos[row];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const float ang = a.inv_freq[(8 * dl + jj) % (D / 2)] * ps;
+                c8[jj] = rbf(cosf(ang));
+                s8[jj] = rbf(sinf(ang));
+            }
+        }
+        const bool lower = dl < LPK / 2;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            f32x4 u[8][2];
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s < a.q_nsplit) {
+                    const f32x4* pp =
+                        (const f32x4*)(a.Qpart + ((long)s * a.Mq + qi) * a.ldqp + (kvh * G + g) * D + 8 * dl);
+                    u[s][0] = pp[0];
+                    u[s][1] = pp[1];
+                }
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s < a.q_nsplit) {
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        x[jj] += u[s][0][jj];
+                        x[4 + jj] += u[s][1][jj];
+                    }
+                }
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) x[jj] = rbf(x[jj]);
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const float pr = __shfl_xor(x[jj], LPK / 2, 64);
+                // lower half: x*c + (-x2)*s ; upper half: x*c + x1*s
+                q[g][jj] = lower ? rbf(rbf(x[jj] * c8[jj]) + rbf(-pr * s8[jj]))
+                                 : rbf(rbf(x[jj] * c8[jj]) + rbf(pr * s8[jj]));
+            }
+        }
+    } else {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            u32x4 w = *(const u32x4*)(a.Q + (long)qi * a.ldq + (kvh * G + g) * D + 8 * dl);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                q[g][2 * j] = bf_lo(w[j]);
+                q[g][2 * j + 1] = bf_hi(w[j]);
+            }
+        }
+    }
     const int len = a.kv_len[row];
     const int t = a.q_pos ? a.q_pos[qi] : len - 1;
     int lo = 0, hi = len;
@@ -281,82 +435,65 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
     const int c0 = lo + sp * CH;
     const int c1 = min(hi, c0 + CH);
     const int n = c1 - c0;
-    float* part = a.part + (((long)qi * a.Hkv + kvh) * a.nsplit + sp) * (G * (D + 2));
-    if (n <= 0) {
-        if (threadIdx.x < G) {
-            part[threadIdx.x * (D + 2)] = -INFINITY;
-            part[threadIdx.x * (D + 2) + 1] = 0.f;
+    const long pstride = (long)G * (D + 2);
+    float* pbase = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * pstride;
+    float* part = pbase + sp * pstride;
+    if (n > 0) {
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int j = c0 + i * KPB + wave * KPW + kg;
+            if (!spec && j < c1) {
+                kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
+                vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
+            }
+            if (j >= c1) {
+                kr[i] = (u32x4){0u, 0u, 0u, 0u};
+                vr[i] = (u32x4){0u, 0u, 0u, 0u};
+            }
         }
-        return;
-    }
-    const bf16_t* Kb = a.K + row * a.kv_bstride + kvh * a.kv_hstride;
-    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
-    u32x4 kr[NIT], vr[NIT];
 #pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-        const int j = c0 + i * KPB + wave * KPW + kg;
-        if (j < c1) {
-            kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
-            vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
-        } else {
-            kr[i] = (u32x4){0u, 0u, 0u, 0u};
-            vr[i] = (u32x4){0u, 0u, 0u, 0u};
+        for (int i = 0; i < NIT; ++i) {
+            float s[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) s[g] = 0.f;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const float k0 = bf_lo(kr[i][jj]), k1 = bf_hi(kr[i][jj]);
+#pragma unroll
+                for (int g = 0; g < G; ++g) s[g] += q[g][2 * jj] * k0 + q[g][2 * jj + 1] * k1;
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int o = LPK / 2; o > 0; o >>= 1) s[g] += __shfl_xor(s[g], o, 64);
+            const int jl = i * KPB + wave * KPW + kg;
+            if (dl == 0) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) sm[g][jl] = s[g] * a.scale;
+            }
         }
-    }
-    float q[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        u32x4 w = *(const u32x4*)(a.Q + (long)qi * a.ldq + (kvh * G + g) * D + 8 * dl);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            q[g][2 * j] = bf_lo(w[j]);
-            q[g][2 * j + 1] = bf_hi(w[j]);
+        __syncthreads();
+        if (wave < G) {
+            const int g = wave;
+            const float s = lane < n ? sm[g][lane] : -INFINITY;
+            const float mx = wave_max(s);
+            const float e = lane < n ? expf(s - mx) : 0.f;
+            const float l = wave_sum(e);
+            sm[g][lane] = rbf(e);
+            if (lane == 0) {
+                stat[g][0] = mx;
+                stat[g][1] = l;
+            }
         }
-    }
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-        float s[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) s[g] = 0.f;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const float k0 = bf_lo(kr[i][jj]), k1 = bf_hi(kr[i][jj]);
-#pragma unroll
-            for (int g = 0; g < G; ++g) s[g] += q[g][2 * jj] * k0 + q[g][2 * jj + 1] * k1;
-        }
+        __syncthreads();
+        float o[G][8];
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int o = LPK / 2; o > 0; o >>= 1) s[g] += __shfl_xor(s[g], o, 64);
-        const int jl = i * KPB + wave * KPW + kg;
-        if (dl == 0) {
+            for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
 #pragma unroll
-            for (int g = 0; g < G; ++g) sm[g][jl] = s[g] * a.scale;
-        }
-    }
-    __syncthreads();
-    if (wave < G) {
-        const int g = wave;
-        const float s = lane < n ? sm[g][lane] : -INFINITY;
-        const float mx = wave_max(s);
-        const float e = lane < n ? expf(s - mx) : 0.f;
-        const float l = wave_sum(e);
-        sm[g][lane] = rbf(e);
-        if (lane == 0) {
-            stat[g][0] = mx;
-            stat[g][1] = l;
-        }
-    }
-    __syncthreads();
-    float o[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-        const int jl = i * KPB + wave * KPW + kg;
-        if (jl < n) {
+        for (int i = 0; i < NIT; ++i) {
+            const int jl = i * KPB + wave * KPW + kg;
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const float p = sm[g][jl];
@@ -367,84 +504,84 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
                 }
             }
         }
-    }
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj)
+            for (int jj = 0; jj < 8; ++jj)
 #pragma unroll
-            for (int off = LPK; off < 64; off <<= 1) o[g][jj] += __shfl_xor(o[g][jj], off, 64);
-    if (kg == 0) {
+                for (int off = LPK; off < 64; off <<= 1) o[g][jj] += __shfl_xor(o[g][jj], off, 64);
+        if (kg == 0) {
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            ored[wave][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
-            ored[wave][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
+            for (int g = 0; g < G; ++g) {
+                ored[wave][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
+                ored[wave][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
+            }
         }
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
+            const int g = idx / LPK, d8 = idx % LPK;
+            const f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
+            const f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
+            if (a.nsplit > 1) {
+                float* pg = part + g * (D + 2);
+                if (d8 == 0) {
+                    pg[0] = stat[g][0];
+                    pg[1] = stat[g][1];
+                }
+                *(f32x4*)(pg + 2 + 8 * d8) = lo4;
+                *(f32x4*)(pg + 6 + 8 * d8) = hi4;
+            } else {
+                const float inv = 1.0f / stat[g][1];
+                u32x4 w;
+                w[0] = pack2(lo4[0] * inv, lo4[1] * inv);
+                w[1] = pack2(lo4[2] * inv, lo4[3] * inv);
+                w[2] = pack2(hi4[0] * inv, hi4[1] * inv);
+                w[3] = pack2(hi4[2] * inv, hi4[3] * inv);
+                *(u32x4*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 8 * d8) = w;
+            }
+        }
+    } else if (a.nsplit > 1 && threadIdx.x < G) {
+        part[threadIdx.x * (D + 2)] = -INFINITY;
+        part[threadIdx.x * (D + 2) + 1] = 0.f;
+    }
+    if (a.nsplit == 1 || !a.counters) return;
+    // ---- in-launch merge: release this block's slab, take a ticket; the last merges
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int* ctr = a.counters + qi * a.Hkv + kvh;
+        const int ticket = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = ticket == a.nsplit - 1;
+        if (last) {
+            __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next launch
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        last_flag = last;
     }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
-        const int g = idx / LPK, d8 = idx % LPK;
-        const f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
-        const f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
-        if (a.nsplit > 1) {
-            float* pg = part + g * (D + 2);
-            if (d8 == 0) {
-                pg[0] = stat[g][0];
-                pg[1] = stat[g][1];
-            }
-            *(f32x4*)(pg + 2 + 8 * d8) = lo4;
-            *(f32x4*)(pg + 6 + 8 * d8) = hi4;
-        } else {
-            const float inv = 1.0f / stat[g][1];
-            u32x4 w;
-            w[0] = pack2(lo4[0] * inv, lo4[1] * inv);
-            w[1] = pack2(lo4[2] * inv, lo4[3] * inv);
-            w[2] = pack2(hi4[0] * inv, hi4[1] * inv);
-            w[3] = pack2(hi4[2] * inv, hi4[3] * inv);
-            *(u32x4*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 8 * d8) = w;
-        }
-    }
+    if (!last_flag) return;
+    merge_splits<D, G>(a, pbase, qi, kvh, wz, Linv);
 }
 
-// merge of the key-split partials: O = sum_z e^(m_z - M) o_z / sum_z e^(m_z - M) l_z
+// merge of the key-split partials (used when no ticket counters are supplied):
+// O = sum_z e^(m_z - M) o_z / sum_z e^(m_z - M) l_z
 template <int D, int G>
 __global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a) {
-    __shared__ float wz[G][64];
+    __shared__ float wz[G * 64];
     __shared__ float Linv[G];
     const int qi = blockIdx.x, kvh = blockIdx.y;
-    const int S = a.nsplit;
-    const float* base = a.part + ((long)qi * a.Hkv + kvh) * S * (G * (D + 2));
-    if (threadIdx.x < 64 * G) {
-        const int g = threadIdx.x / 64, z = threadIdx.x % 64;
-        const float m = z < S ? base[(long)z * G * (D + 2) + g * (D + 2)] : -INFINITY;
-        const float l = z < S ? base[(long)z * G * (D + 2) + g * (D + 2) + 1] : 0.f;
-        const float M = wave_max(m);
-        const float w = (m == -INFINITY) ? 0.f : expf(m - M);
-        const float L = wave_sum(w * l);
-        wz[g][z] = w;
-        if (z == 0) Linv[g] = 1.0f / L;
-    }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < G * D / 4; idx += 256) {
-        const int g = idx / (D / 4), d4 = idx % (D / 4);
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        for (int z = 0; z < S; ++z) {
-            const float w = wz[g][z];
-            if (w != 0.f) acc += w * *(const f32x4*)(base + (long)z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
-        }
-        const float inv = Linv[g];
-        uint2 o;
-        o.x = pack2(acc[0] * inv, acc[1] * inv);
-        o.y = pack2(acc[2] * inv, acc[3] * inv);
-        *(uint2*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 4 * d4) = o;
-    }
+    const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2));
+    merge_splits<D, G>(a, base, qi, kvh, wz, Linv);
 }
 
 template <int D, int G>
 static int launch_decode(const AttnArgs& a, hipStream_t st) {
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
     hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, a);
-    if (a.nsplit > 1)
+    if (a.nsplit > 1 && !a.counters)
         hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv), dim3(256), 0,
                            st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -62,6 +62,8 @@ struct t5g_engine {
     int* next_token;
     int* flags;
     int* last_rows;
+    int* attn_tickets;  // [max_batch][Hkv] in-launch split-merge counters (self-re-arming)
+    float* rope_tab;    // [max_batch][D] per-row cos|sin of the decode step's PM position
     int B = 0;            // rows of the current call
     const bf16_t* noise = nullptr;
     int noise_steps = 0;
@@ -179,6 +181,8 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->next_token, B);
     rc |= alloc(e, &e->flags, B);
     rc |= alloc(e, &e->last_rows, B);
+    rc |= alloc(e, &e->attn_tickets, (int64_t)B * Hkv);
+    rc |= alloc(e, &e->rope_tab, (int64_t)B * D);
     if (rc) {
         t5g_engine_destroy(e);
         return T5G_ENOMEM;
@@ -357,6 +361,12 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
     const int G = c.n_heads / c.n_kv_heads;
     // split-K factors (decode: spread weight streams over >= 512 blocks)
     const int s_qkv = decode ? 2 : 1, s_o = decode ? 4 : 1, s_cq = decode ? 4 : 1, s_down = decode ? 8 : 1;
+    // one cos/sin table per step: every layer's q/k rotation uses the same positions
+    const float* tab = nullptr;
+    if (decode) {
+        RC(rope_table(pos, e->w.inv_freq, M, D, e->rope_tab, st));
+        tab = e->rope_tab;
+    }
     for (int l = 0; l < c.n_dec_layers; ++l) {
         const t5g_layer_weights& L = e->dec[l];
         if (l == 0) {
@@ -383,7 +393,9 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         r.ldx = e->qkv_dim;
         r.M = M;
         r.D = D;
-        r.nq = c.n_heads;
+        // decode: q is rotated inside the attention kernel; only k/v go to the cache here
+        r.nq = decode ? 0 : c.n_heads;
+        r.col0 = decode ? e->q_dim : 0;
         r.nk = c.n_kv_heads;
         r.nv = c.n_kv_heads;
         r.rope_q = r.rope_k = 1;
@@ -392,6 +404,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         r.tok_row = tok_row;
         r.tok_t = tok_t;
         r.kv_len = e->kv_len;
+        r.rope_tab = tab;
         r.Qout = q;
         r.ldq = e->q_dim;
         r.Kc = e->sk[l];
@@ -425,9 +438,28 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             if (decode && !a.eager) {
                 a.chunk = 64;
                 a.nsplit = (c.max_audio + 63) / 64;
+                a.kv_cap = c.max_audio;
                 a.part = e->apart;
+                a.counters = nullptr;  // separate combine launch (cheaper than in-launch tickets)
+                if (s_qkv > 1) {
+                    a.Qpart = e->part;
+                    a.q_nsplit = s_qkv;
+                    a.ldqp = e->qkv_dim;
+                    a.pos = pos;
+                    a.inv_freq = e->w.inv_freq;
+                    a.rope_tab = tab;
+                } else {
+                    return T5G_EINVAL;
+                }
                 RC(attention_decode(a, st));
             } else {
+                if (decode) {  // eager decode: q rope via rope_store (q only)
+                    RopeArgs rq = r;
+                    rq.nq = c.n_heads;
+                    rq.nk = rq.nv = 0;
+                    rq.col0 = 0;
+                    RC(rope_store(rq, st));
+                }
                 a.nsplit = 1;
                 a.chunk = c.max_audio;
                 RC(attention(a, st));
@@ -469,9 +501,11 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         r.pos = pos;
         r.inv_freq = e->w.inv_freq;
         r.tok_row = tok_row;
+        r.rope_tab = tab;
         r.Qout = q;
         r.ldq = e->q_dim;
-        RC(rope_store(r, st));
+        const bool fuse_q = decode && c.softcap <= 0.f && s_cq > 1;
+        if (!fuse_q) RC(rope_store(r, st));
         {
             AttnArgs a;
             memset(&a, 0, sizeof(a));
@@ -495,10 +529,18 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             a.eager = c.softcap > 0.f;
             a.O = att;
             a.ldo = e->q_dim;
-            if (decode && !a.eager) {
+            if (fuse_q) {
                 a.chunk = 64;
                 a.nsplit = (c.max_text + 63) / 64;
+                a.kv_cap = c.max_text;
                 a.part = e->apart;
+                a.counters = nullptr;  // separate combine launch (cheaper than in-launch tickets)
+                a.Qpart = e->part;
+                a.q_nsplit = s_cq;
+                a.ldqp = e->q_dim;
+                a.pos = pos;
+                a.inv_freq = e->w.inv_freq;
+                a.rope_tab = tab;
                 RC(attention_decode(a, st));
             } else {
                 a.nsplit = 1;

@@ -33,8 +33,7 @@ __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
     return w;
 }
 
-__device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, const bf16_t* __restrict__ w, int c,
-                                     float eps, float* red) {
+__device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, u32x4 w8, float eps, float* red) {
     float ss = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
@@ -42,7 +41,7 @@ __device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, const bf
     float r = 1.0f / sqrtf(tot / (float)d + eps);
     if (!active) return;
     float wf[8];
-    unpack8(*(const u32x4*)(w + 8 * c), wf);
+    unpack8(w8, wf);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = rbf((v[j] * r) * (1.0f + wf[j]));
 }
@@ -56,8 +55,11 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a) {
     const bool active = 8 * c < d;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float r8[8];
-    u32x4 rw = {0u, 0u, 0u, 0u};
+    u32x4 rw = {0u, 0u, 0u, 0u}, w_post = {0u, 0u, 0u, 0u}, w_pre = {0u, 0u, 0u, 0u};
     if (active) {
+        // every load of the row is issued up front (one memory round trip)
+        if (a.post_w) w_post = *(const u32x4*)(a.post_w + 8 * c);
+        if (a.pre_w) w_pre = *(const u32x4*)(a.pre_w + 8 * c);
         if (a.resid) rw = *(const u32x4*)(a.resid + (long)m * d + 8 * c);
         if (a.ids) {
             unpack8(*(const u32x4*)(a.table + (long)a.ids[m] * d + 8 * c), v);
@@ -87,7 +89,7 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a) {
             unpack8(*(const u32x4*)(a.delta + (long)m * d + 8 * c), v);
         }
     }
-    if (a.post_w) rms8(v, active, d, a.post_w, c, a.eps, red);
+    if (a.post_w) rms8(v, active, d, w_post, a.eps, red);
     if (a.resid && active) {
         unpack8(rw, r8);
 #pragma unroll
@@ -96,7 +98,7 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a) {
     const long orow = a.out_rows ? (long)mi : (long)m;
     if (a.resid_out && active) *(u32x4*)(a.resid_out + orow * d + 8 * c) = pack8(v);
     if (a.pre_w) {
-        rms8(v, active, d, a.pre_w, c, a.eps, red);
+        rms8(v, active, d, w_pre, a.eps, red);
         if (active) *(u32x4*)(a.normed_out + orow * d + 8 * c) = pack8(v);
     }
 }

@@ -255,10 +255,31 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
     // ---- 5. top-k threshold (k-th largest, ties kept) (:101-105)
     if (kk > 0) {
         const int k = min(kk, V);
+        // candidate prefilter: only values >= M - delta (delta grown until >= k of them)
+        // enter the histograms, which keeps LDS-atomic contention off the bulk
+        float thr0 = -INFINITY;
+        if (k < V) {
+            float lm = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < SPER; ++j) lm = fmaxf(lm, x.get(j));
+            const float M = block_max(lm, redv);
+            float delta = 2.0f;
+            for (int it = 0; it < 6; ++it) {
+                const float t0 = M - delta;
+                int c = 0;
+#pragma unroll
+                for (int j = 0; j < SPER; ++j) c += (eidx(tid, j) < V && x.get(j) >= t0) ? 1 : 0;
+                if (block_count(c, redi) >= k) {
+                    thr0 = t0;
+                    break;
+                }
+                delta *= 4.0f;
+            }
+        }
         hist_clear(wh);
 #pragma unroll
         for (int j = 0; j < SPER; ++j)
-            if (eidx(tid, j) < V) atomicAdd(&wh[wid][okey(x.get(j)) >> 8], 1u);
+            if (eidx(tid, j) < V && x.get(j) >= thr0) atomicAdd(&wh[wid][okey(x.get(j)) >> 8], 1u);
         hist_reduce(wh, hsum);
         if (wid == 0) find_bin_wave0(hsum, k, &sh_int[0], &sh_int[1]);
         __syncthreads();
@@ -267,7 +288,7 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
         hist_clear(wh);
 #pragma unroll
         for (int j = 0; j < SPER; ++j)
-            if (eidx(tid, j) < V) {
+            if (eidx(tid, j) < V && x.get(j) >= thr0) {
                 const uint32_t kq = okey(x.get(j));
                 if ((kq >> 8) == hb) atomicAdd(&wh[wid][kq & 255u], 1u);
             }
@@ -288,17 +309,41 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
         const float m = block_max(lm, redv);
         float ls = 0.f;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) ls += expf(x.get(j) - m);
+        for (int j = 0; j < SPER; ++j) {
+            const float v = x.get(j);
+            if (v > -INFINITY) ls += expf(v - m);
+        }
         const float inv = 1.0f / block_sum(ls, redv);
         const float thr = rbf(top_p);
+        // candidate prefilter: the top values whose probability mass already exceeds
+        // top_p (the cut lies inside them); falls back to every value otherwise
+        float thr0 = -INFINITY;
+        {
+            float delta = 4.0f;
+            for (int it = 0; it < 4; ++it) {
+                const float t0 = m - delta;
+                float ms = 0.f;
+#pragma unroll
+                for (int j = 0; j < SPER; ++j) {
+                    const float v = x.get(j);
+                    if (v >= t0) ms += rbf(expf(v - m) * inv);
+                }
+                if (block_sum(ms, redv) > thr + 0.02f) {
+                    thr0 = t0;
+                    break;
+                }
+                delta *= 2.0f;
+            }
+        }
+        __shared__ unsigned coarse[256];
+    restart_walk:
         hist_clear(wh);
 #pragma unroll
         for (int j = 0; j < SPER; ++j) {
             const float v = x.get(j);
-            if (v > -INFINITY) atomicAdd(&wh[wid][okey(v) >> 8], 1u);
+            if (v > -INFINITY && v >= thr0) atomicAdd(&wh[wid][okey(v) >> 8], 1u);
         }
         hist_reduce(wh, hsum);
-        __shared__ unsigned coarse[256];
         if (tid < 256) coarse[tid] = hsum[tid];
         if (tid == 0) {
             sh_int[4] = 0;      // state: 0 walking, 1 cut found, 2 exhausted
@@ -319,7 +364,7 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
 #pragma unroll
             for (int j = 0; j < SPER; ++j) {
                 const float v = x.get(j);
-                if (v > -INFINITY) {
+                if (v > -INFINITY && v >= thr0) {
                     const uint32_t kq = okey(v);
                     if ((kq >> 8) == hb) atomicAdd(&wh[wid][kq & 255u], 1u);
                 }
@@ -375,6 +420,11 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
             }
             __syncthreads();
         }
+        if (sh_int[4] == 2 && thr0 > -INFINITY) {  // cut not inside the candidates: use all
+            thr0 = -INFINITY;
+            __syncthreads();
+            goto restart_walk;
+        }
         if (sh_int[4] == 1) {
             const float vc = sh_f[1];
             const int keep = sh_int[1], gsz = sh_int[2];
@@ -418,7 +468,10 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
         const float m = block_max(lm, redv);
         float ls = 0.f;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) ls += expf(x.get(j) - m);
+        for (int j = 0; j < SPER; ++j) {
+            const float v = x.get(j);
+            if (v > -INFINITY) ls += expf(v - m);
+        }
         const float inv = 1.0f / block_sum(ls, redv);
         const bf16_t* nz = a.noise ? a.noise + ((long)b * a.noise_steps + st.cur_num_gen) * V : nullptr;
         float bv = -1.f;
@@ -427,7 +480,9 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
         for (int j = 0; j < SPER; ++j) {
             const int i = eidx(tid, j);
             if (i >= V) continue;
-            const float p = rbf(expf(x.get(j) - m) * inv);
+            const float xv = x.get(j);
+            if (xv == -INFINITY) continue;  // p = 0 -> r = 0 can never beat a survivor
+            const float p = rbf(expf(xv - m) * inv);
             float r = 0.f;
             if (p > 0.f) {
                 float q;

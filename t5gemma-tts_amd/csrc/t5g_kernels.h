@@ -49,7 +49,8 @@ struct RopeArgs {
     const float* Xpart;      // alternatively fp32 split-K slabs [nsplit][M][ldx] (summed, rounded)
     int nsplit;
     int ldx, M, D;
-    int nq, nk, nv;          // head counts present in X (column blocks of D)
+    int nq, nk, nv;          // head counts present in X (column blocks of D, from column col0)
+    int col0;
     int rope_q, rope_k;
     const float* pos;        // [M] float PM positions (or pos_dev_row when decode)
     const float* inv_freq;   // [D/2]
@@ -61,8 +62,11 @@ struct RopeArgs {
     bf16_t* Kc;              // cache [B][Hkv][Lmax][D]
     bf16_t* Vc;
     long c_bstride, c_hstride;
+    const float* rope_tab;   // optional [rows][D]: bf16-rounded cos (D/2) | sin (D/2) per row
 };
 int rope_store(const RopeArgs& a, hipStream_t st);
+// tab[r][i] = bf16(cos(inv_freq[i] * pos[r])), tab[r][D/2 + i] = bf16(sin(...)), r < rows
+int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st);
 
 // ---- attention ----------------------------------------------------------------
 struct AttnArgs {
@@ -83,6 +87,14 @@ struct AttnArgs {
     float* part;             // partial slabs when nsplit > 1
     bf16_t* O;               // [Mq][ldo]
     int ldo;
+    // decode extras: q straight from the projection's fp32 split-K slabs, PM-RoPE'd in-kernel
+    const float* Qpart;      // [q_nsplit][Mq][ldqp] or null (then Q is used)
+    int q_nsplit, ldqp;
+    const float* pos;        // [rows] float PM positions for the q rotation
+    const float* inv_freq;   // [D/2]
+    int* counters;           // [Mq][Hkv] arrival tickets: the last split block merges (zeroed)
+    const float* rope_tab;   // optional per-row cos/sin table (see rope_table)
+    int kv_cap;              // allocated keys per (row, head): speculative loads stay below it
 };
 int attention(const AttnArgs& a, hipStream_t st);
 // decode-shaped (64-key blocks, split over blockIdx.z, sdpa numerics); nsplit = ceil(keys/64)
