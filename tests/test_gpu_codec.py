@@ -1,0 +1,152 @@
+"""GPU parity of the XCodec2 decoder through the xc2_* C ABI.
+
+Bar (BASELINE north star): waveform RMS error within 1e-4 of the reference's fp32 CPU
+decode. The references are the committed transformers-Xcodec2Model goldens and the
+CPU oracle (oracle/xc2_oracle.py) on the same seeded weights and codes.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-4          # north-star waveform bound
+MAX_TOL = 1e-4
+
+
+def _case(name):
+    from t5gemma_tts_amd.codec import CodecConfig
+    m = json.load(open(os.path.join(GOLDEN, f"golden_codec_{name}.json")))
+    wav = np.load(os.path.join(GOLDEN, f"golden_codec_{name}.npz"))["wav"]
+    cfg = CodecConfig(**{k: (tuple(v) if isinstance(v, list) else v) for k, v in m["config"].items()})
+    return m, cfg, wav
+
+
+def _errs(a, b):
+    d = np.asarray(a, dtype=np.float64) - np.asarray(b, dtype=np.float64)
+    return math.sqrt((d ** 2).mean()), float(np.abs(d).max())
+
+
+_codecs = {}
+
+
+def _codec(name, max_batch=4, max_frames=64):
+    from t5gemma_tts_amd.codec import XCodec2Decoder, synthetic_codec_weights
+    key = (name, max_batch, max_frames)
+    if key not in _codecs:
+        m, cfg, _ = _case(name)
+        _codecs[key] = XCodec2Decoder(cfg, synthetic_codec_weights(cfg, m["weight_seed"]), device="cuda:0",
+                                      max_batch=max_batch, max_frames=max_frames)
+    return _codecs[key]
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(128, 128, 32, 0), (100, 200, 64, 0), (37, 1282, 256, 0),
+                                       (513, 1024, 1024, 1), (1, 96, 2048, 0), (300, 4096, 1024, 1)])
+def test_f32_gemm_matches_fp64(M, N, K, epi):
+    import ctypes as C
+    from t5gemma_tts_amd import _lib
+    from t5gemma_tts_amd.codec import XC2_SIGNATURES
+    L = _lib.lib()
+    fn = L.xc2_gemm
+    fn.restype, fn.argtypes = XC2_SIGNATURES["xc2_gemm"]
+    g = torch.Generator().manual_seed(M * 7 + N)
+    X = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g)
+    ref = X.double() @ W.double().T + b.double()
+    if epi == 1:
+        ref = ref * torch.sigmoid(ref)
+    Xd, Wd, bd = X.cuda(), W.cuda(), b.cuda()
+    Y = torch.full((M, N), float("nan"), device="cuda")
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert fn(C.c_void_p(Xd.data_ptr()), K, M, C.c_void_p(Wd.data_ptr()), N, K, C.c_void_p(bd.data_ptr()),
+              C.c_void_p(Y.data_ptr()), N, epi, st) == 0
+    torch.cuda.synchronize()
+    err = (Y.cpu().double() - ref).abs().max().item()
+    bound = 2e-6 * math.sqrt(K) * (X.abs().max().item() + 1)
+    assert err <= bound, (err, bound)
+
+
+@pytest.mark.parametrize("name", ["tiny", "full16k", "hop882"])
+def test_decode_matches_transformers_golden(name):
+    m, cfg, wav = _case(name)
+    codec = _codec(name)
+    out = codec.decode(torch.tensor(m["codes"], dtype=torch.int64)).cpu().numpy()
+    assert out.shape == wav.shape
+    rms, mx = _errs(out, wav)
+    print(f"{name}: waveform RMS err {rms:.3e}, max {mx:.3e} (signal RMS {m['wav_rms']:.3e})")
+    assert rms <= RMS_TOL and mx <= MAX_TOL, (rms, mx)
+    assert rms <= 1e-5        # fp32 MFMA path: expected ~1e-7
+
+
+def test_batched_rows_equal_single_rows_bitwise():
+    m, cfg, _ = _case("tiny")
+    codec = _codec("tiny")
+    codes = torch.tensor(m["codes"], dtype=torch.int64)
+    both = codec.decode(codes)
+    for b in range(codes.shape[0]):
+        one = codec.decode(codes[b:b + 1])
+        assert torch.equal(both[b], one[0])
+
+
+def test_ragged_lens_match_oracle():
+    from oracle import xc2_oracle as xo
+    from t5gemma_tts_amd.codec import synthetic_codec_weights
+    m, cfg, _ = _case("tiny")
+    codec = _codec("tiny")
+    codes = torch.tensor(m["codes"], dtype=torch.int64)
+    lens = [codes.shape[1], 20]
+    out = codec.decode(codes, lens=lens).cpu()
+    ref = xo.decode(synthetic_codec_weights(cfg, m["weight_seed"]), codes, cfg, lens=lens)
+    rms, mx = _errs(out.numpy(), ref.numpy())
+    assert rms <= 1e-5 and mx <= MAX_TOL, (rms, mx)
+    assert torch.all(out[1, :, 20 * cfg.hop_length:] == 0)
+    # a short row inside a batch equals that row decoded alone, bitwise
+    alone = codec.decode(codes[1:, :20])
+    assert torch.equal(out[1, :, :20 * cfg.hop_length], alone[0].cpu())
+
+
+def test_special_ids_wrap_mod_codebook():
+    m, cfg, _ = _case("tiny")
+    codec = _codec("tiny")
+    codes = torch.tensor(m["codes"], dtype=torch.int64)[:1].clone()
+    codes[0, 3], codes[0, 9], codes[0, 17] = 65536, 65537, 65538
+    a = codec.decode(codes)
+    b = codec.decode(codes % 65536)
+    assert torch.equal(a, b)
+
+
+def test_capacity_errors():
+    codec = _codec("tiny", max_batch=4, max_frames=64)
+    with pytest.raises(ValueError):
+        codec.decode(torch.zeros(1, 65, dtype=torch.int64))
+    with pytest.raises(ValueError):
+        codec.decode(torch.zeros(5, 10, dtype=torch.int64))
+    with pytest.raises(ValueError):
+        codec.decode(torch.zeros(2, 3, 10, dtype=torch.int64))
+
+
+def test_full_size_batch_row_matches_oracle():
+    """Real 16 kHz dims, B = 4 x 250 frames (5 s): one row against the CPU oracle, every
+    row against its own single-row decode (batch invariance)."""
+    from oracle import xc2_oracle as xo
+    from t5gemma_tts_amd.codec import XCodec2Decoder, codec_16k, synthetic_codec_weights
+    cfg = codec_16k()
+    sd = synthetic_codec_weights(cfg, 12)
+    codec = XCodec2Decoder(cfg, sd, device="cuda:0", max_batch=4, max_frames=256)
+    g = torch.Generator().manual_seed(5)
+    codes = torch.randint(0, 65536, (4, 250), generator=g)
+    out = codec.decode(codes)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ref = xo.decode(sd, codes[2:3], cfg)
+    rms, mx = _errs(out[2].cpu().numpy(), ref[0].numpy())
+    print(f"full16k B4x250 row2: RMS err {rms:.3e}, max {mx:.3e}")
+    assert rms <= RMS_TOL and mx <= MAX_TOL
+    assert torch.equal(out[3], codec.decode(codes[3:4])[0])
+    codec.close()
