@@ -83,7 +83,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--batch", type=int, default=B_PER_GPU)
-    ap.add_argument("--profile-kernels", action="store_true", default=True)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, default) or gloo (CPU collectives; lets N ranks share one GPU "
+                         "to rehearse the sharded path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -93,9 +95,13 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(args.dist_backend)
+    dev = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}")
+    comm_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     torch.cuda.set_device(dev)
 
     import t5gemma_tts_amd  # noqa: F401
@@ -111,21 +117,29 @@ def main():
     eng = T5GemmaTTSEngine(cfg, sd, device=str(dev), max_batch=B, max_text=64,
                            max_audio=T_P + 1 + n_tok_row + 8, max_gen=n_tok_row + 4)
 
-    # global batch drawn on rank 0, broadcast over RCCL (8(e))
+    # global batch drawn on rank 0; each step broadcasts it over RCCL, shards it (LPT over
+    # the token budget, B per rank), generates, and all-gathers the ids (8(e))
+    from t5gemma_tts_amd.distributed import run_sharded
     G = B * world
-    flat = torch.empty(G, T_X + T_P, dtype=torch.int32, device=dev)
+    rows = costs = None
     if rank == 0:
-        rows = make_batch(cfg, G, seed=20251226)
-        flat.copy_(torch.tensor([r[0] + r[1] for r in rows], dtype=torch.int32))
-    if dist is not None:
-        dist.broadcast(flat, src=0)
-    mine = flat[rank * B:(rank + 1) * B].cpu().tolist()
-    utts = [Utterance(x=r[:T_X], y=r[T_X:], tgt_y_len=T_P + DUR_FRAMES) for r in mine]
+        rows = [[len(x), tgt] + x + y for x, y, tgt in make_batch(cfg, G, seed=20251226)]
+        costs = [r[1] for r in rows]
     params = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3, eos_disabled=True)
+    gen_tokens = [0]
+
+    def generate(shard, i):
+        utts = [Utterance(x=r[2:2 + r[0]], y=r[2 + r[0]:], tgt_y_len=r[1]) for r in shard]
+        out = eng.generate(utts, params, seeds=[1000 * i + rank * B + b for b in range(len(utts))], chunk=64)
+        gen_tokens[0] += sum(len(g) for g in out["gen"])
+        return [g.tolist() for g in out["gen"]]
 
     def step(i):
-        out = eng.generate(utts, params, seeds=[1000 * i + rank * B + b for b in range(B)], chunk=64)
-        return sum(len(g) for g in out["gen"])
+        if dist is None:
+            return sum(len(g) for g in generate(rows, i))
+        before = gen_tokens[0]
+        run_sharded(rows, costs, lambda sh: generate(sh, i), comm_dev, max_per_rank=B, max_len=n_tok_row + 8)
+        return gen_tokens[0] - before
 
     for i in range(args.warmup):
         step(i)
@@ -140,7 +154,7 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    tot = torch.tensor([float(tokens), dt], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(tokens), dt], dtype=torch.float64, device=comm_dev)
     if dist is not None:
         t_tok = tot[:1].clone()
         dist.all_reduce(t_tok, op=dist.ReduceOp.SUM)
@@ -182,7 +196,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, sd, ([int(v) for v in utts[0].x], list(utts[0].y), utts[0].tgt_y_len))
+        r0 = rows[0]
+        cpu = cpu_baseline(cfg, sd, (r0[2:2 + r0[0]], r0[2 + r0[0]:], r0[1]))
 
     if rank == 0:
         ms = dt_max / args.steps * 1e3

@@ -1,0 +1,230 @@
+"""Host plumbing around generate(): the reference's ``inference_one_sample``
+(inference_tts_utils.py:140-378) restated over this build's engine and codec.
+
+SURVEY 8(a) rows covered here:
+  a17  token plumbing: text ids = [bos] + prefix + [x_sep] + target + [eos]
+       (:253-273), prompt codes + repeat_prompt + [y_sep] (:179-243), tgt_y_lens
+       (:279-285);
+  a15  output assembly ``_strip_sep_and_eos`` (:323-357);
+  and the codec call on the concatenated / generated frames (:359-366).
+
+Out of scope: text normalisation + SentencePiece (callers pass token ids
+or any tokenizer object with ``encode(text, add_special_tokens=False)``), the XCodec2
+*encoder* (callers pass prompt codes instead of an audio path), Whisper.
+
+``inference_batch`` is the batched form the reference lacks (its batch is asserted to
+1, :288): many utterances through one engine call and one batched codec decode.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Union
+
+import torch
+
+IntList = Union[Sequence[int], torch.Tensor]
+
+
+def build_text_tokens(target: Union[str, IntList], prefix: Optional[Union[str, IntList]] = None,
+                      text_tokenizer=None, x_sep_token: Optional[int] = None, add_eos_token: int = 0,
+                      add_bos_token: int = 0) -> List[int]:
+    """inference_tts_utils.py:253-273."""
+    def enc(t):
+        if isinstance(t, str):
+            if text_tokenizer is None:
+                raise ValueError("text given as a string but no text_tokenizer")
+            return list(text_tokenizer.encode(t.strip(), add_special_tokens=False))
+        if isinstance(t, list) and t and isinstance(t[0], str):
+            return enc(" ".join(t))
+        return [int(v) for v in (t.tolist() if isinstance(t, torch.Tensor) else t)]
+
+    ids = enc(target)
+    if prefix:
+        p = enc(prefix)
+        ids = p + [int(x_sep_token)] + ids if x_sep_token is not None else p + ids
+    if add_eos_token:
+        ids.append(int(add_eos_token))
+    if add_bos_token:
+        ids = [int(add_bos_token)] + ids
+    return ids
+
+
+def build_prompt(prompt_codes: Optional[IntList], y_sep_token: Optional[int], codec_sr: float,
+                 target_generation_length: float, repeat_prompt: Union[int, str] = 0,
+                 audio_max_length: float = 40.0) -> torch.Tensor:
+    """Prompt frames -> original_audio [1, T_p, 1] (inference_tts_utils.py:179-243).
+    ``prompt_codes`` None / empty = no reference audio (no y_sep is inserted)."""
+    if prompt_codes is None:
+        frames = torch.empty(1, 1, 0, dtype=torch.long)
+    else:
+        frames = torch.as_tensor(prompt_codes, dtype=torch.long)
+        if frames.ndim == 1:
+            frames = frames.view(1, 1, -1)
+        elif frames.ndim == 2:
+            frames = frames.unsqueeze(0)
+        if frames.ndim != 3 or frames.shape[0] != 1:
+            raise ValueError(f"Unexpected prompt shape {tuple(frames.shape)}")
+        if frames.shape[2] == 1:
+            frames = frames.transpose(1, 2).contiguous()
+        if frames.shape[1] != 1:
+            raise ValueError(f"Expected a single codebook axis, got shape {tuple(frames.shape)}")
+    has_ref = frames.shape[2] > 0
+    single = frames.clone()
+    if isinstance(repeat_prompt, int) and repeat_prompt > 0:
+        for _ in range(repeat_prompt):
+            frames = torch.cat([frames, single], dim=2)
+    elif isinstance(repeat_prompt, str) and repeat_prompt.lower() == "max":
+        while frames.shape[2] + codec_sr * target_generation_length + single.shape[2] < audio_max_length * codec_sr:
+            frames = torch.cat([frames, single], dim=2)
+            if single.shape[2] == 0:
+                break
+    if y_sep_token is not None and has_ref and frames.shape[2] > 0:
+        frames = torch.cat([frames, torch.full((1, 1, 1), int(y_sep_token), dtype=torch.long)], dim=2)
+    return frames.transpose(2, 1).contiguous()
+
+
+def target_length(prompt_frames: int, codec_sr: float, target_generation_length: float,
+                  parallel_pattern: int = 0) -> int:
+    """inference_tts_utils.py:279-285 (effective_delay_inc = 0)."""
+    extra = 2 if parallel_pattern else 0
+    return int(prompt_frames + codec_sr * target_generation_length + extra)
+
+
+def strip_sep_and_eos(frames: torch.Tensor, sep_token: Optional[int], eos_token: Optional[int]) -> torch.Tensor:
+    """Drop y_sep / EOS ids from [B, K, T] frames (inference_tts_utils.py:323-354). When
+    rows keep different counts, every row is cut (or padded with sep) to the minimum."""
+    mask = torch.ones_like(frames, dtype=torch.bool)
+    if sep_token is not None:
+        mask &= frames.ne(sep_token)
+    if eos_token is not None:
+        mask &= frames.ne(eos_token)
+    if bool(mask.all()):
+        return frames
+    keep = mask.sum(dim=2)
+    if not bool(torch.all(keep.eq(keep[..., :1]))):
+        n = int(keep.min())
+        rows = []
+        for b in range(frames.shape[0]):
+            per = []
+            for k in range(frames.shape[1]):
+                v = frames[b, k][mask[b, k]]
+                if v.numel() < n:
+                    v = torch.nn.functional.pad(v, (0, n - v.numel()), value=sep_token if sep_token is not None else 0)
+                per.append(v[:n].unsqueeze(0))
+            rows.append(torch.cat(per, 0).unsqueeze(0))
+        return torch.cat(rows, 0).to(frames.device)
+    n = int(keep[0, 0])
+    return frames[mask].view(frames.size(0), frames.size(1), n)
+
+
+def _eos_token(model_args):
+    return getattr(model_args, "eos", getattr(model_args, "eog", None))
+
+
+@torch.no_grad()
+def inference_one_sample(model, model_args, text_tokenizer, audio_tokenizer, prompt_codes, target_text, lang,
+                         device, decode_config, prompt_end_frame, target_generation_length, prefix_transcript=None,
+                         quiet=False, repeat_prompt=0, multi_trial=None, return_frames=False, seed=None,
+                         parity=False):
+    """Same arguments and returns as the reference (inference_tts_utils.py:140-378),
+    except that ``prompt_codes`` (codec ids of the reference audio, or None) replaces
+    ``audio_fn`` because the codec encoder is out of scope; ``prompt_end_frame`` > 0
+    truncates them like the reference's ``num_frames``. ``lang``/``device`` are accepted
+    for signature compatibility (normalisation is out of scope; the engine's device wins)."""
+    multi_trial = multi_trial or []
+    if int(getattr(model_args, "n_codebooks", 1)) != 1:
+        raise ValueError("XCodec2 backend supports only n_codebooks=1.")
+    if multi_trial:
+        raise AssertionError("multi_trial is not supported (reference asserts multi_trial == [])")
+    if int(decode_config.get("sample_batch_size", 1) or 1) > 1:
+        raise AssertionError("sample_batch_size must be <= 1 (inference_tts_utils.py:288)")
+    codec_sr = float(decode_config["codec_sr"])
+    silence = decode_config.get("silence_tokens", []) or []
+    if isinstance(silence, str):
+        silence = [int(v) for v in silence.strip("[]() ").split(",") if v.strip()]
+    if prompt_codes is not None and prompt_end_frame and prompt_end_frame > 0:
+        pc = torch.as_tensor(prompt_codes).reshape(-1)
+        prompt_codes = pc[:int(prompt_end_frame)]
+    original_audio = build_prompt(prompt_codes, getattr(model_args, "y_sep_token", None), codec_sr,
+                                  target_generation_length, repeat_prompt,
+                                  float(getattr(model_args, "audio_max_length", 40.0)))
+    has_ref = prompt_codes is not None and original_audio.shape[1] > 0
+    prompt_frames = original_audio.shape[1]
+    ids = build_text_tokens(target_text, prefix_transcript, text_tokenizer, getattr(model_args, "x_sep_token", None),
+                            getattr(model_args, "add_eos_to_text", 0), getattr(model_args, "add_bos_to_text", 0))
+    x = torch.LongTensor(ids).unsqueeze(0)
+    x_lens = torch.LongTensor([x.shape[-1]])
+    tgt = torch.LongTensor([target_length(prompt_frames, codec_sr, target_generation_length,
+                                          getattr(model_args, "parallel_pattern", 0))])
+    t0 = time.time()
+    concat_frames, gen_frames = model.inference_tts(
+        x, x_lens, original_audio, tgt_y_lens=tgt, top_k=decode_config["top_k"], top_p=decode_config["top_p"],
+        min_p=decode_config.get("min_p", 0.0), temperature=decode_config["temperature"],
+        stop_repetition=decode_config.get("stop_repetition", 3), silence_tokens=silence,
+        prompt_frames=prompt_frames, seeds=None if seed is None else [int(seed)], parity=parity)
+    dt = time.time() - t0
+    n = gen_frames.shape[-1]
+    if not quiet:
+        print(f"[Speed] {n / dt if dt > 0 else 0.0:.2f} tokens/s | RTF: {n / codec_sr / dt if dt > 0 else 0.0:.2f}x | "
+              f"Generated {n} tokens in {dt:.2f}s")
+    y_sep, eos = getattr(model_args, "y_sep_token", None), _eos_token(model_args)
+    concat_frames = strip_sep_and_eos(concat_frames, y_sep, eos)
+    gen_frames = strip_sep_and_eos(gen_frames, y_sep, eos)
+    concat_sample = audio_tokenizer.decode(concat_frames) if has_ref and concat_frames.shape[-1] > 0 else None
+    gen_sample = audio_tokenizer.decode(gen_frames)
+    if concat_sample is None:
+        concat_sample = gen_sample
+    if return_frames:
+        return concat_sample, gen_sample, concat_frames.detach().cpu(), gen_frames.detach().cpu()
+    return concat_sample, gen_sample
+
+
+@dataclass
+class TTSRequest:
+    target: Union[str, IntList]
+    duration_s: float
+    prefix: Optional[Union[str, IntList]] = None
+    prompt_codes: Optional[IntList] = None
+    seed: int = 1
+
+
+@torch.no_grad()
+def inference_batch(engine, model_args, audio_tokenizer, requests: Sequence[TTSRequest], decode_config,
+                    text_tokenizer=None, parity=False):
+    """Batched text -> waveform: one generate() over all requests, then one batched codec
+    decode of the stripped generated frames (ragged lengths via the codec's lens).
+    Returns (list of wav [1, n * hop] tensors, list of generated frame tensors, stats)."""
+    from .engine import SamplingParams, Utterance
+    codec_sr = float(decode_config["codec_sr"])
+    utts = []
+    for r in requests:
+        oa = build_prompt(r.prompt_codes, getattr(model_args, "y_sep_token", None), codec_sr, r.duration_s)
+        ids = build_text_tokens(r.target, r.prefix, text_tokenizer, getattr(model_args, "x_sep_token", None),
+                                getattr(model_args, "add_eos_to_text", 0), getattr(model_args, "add_bos_to_text", 0))
+        utts.append(Utterance(x=ids, y=oa[0, :, 0].tolist(), tgt_y_len=target_length(oa.shape[1], codec_sr,
+                                                                                     r.duration_s)))
+    params = SamplingParams(top_k=decode_config["top_k"], top_p=decode_config["top_p"],
+                            min_p=decode_config.get("min_p", 0.0), temperature=decode_config["temperature"],
+                            stop_repetition=decode_config.get("stop_repetition", 3),
+                            silence_tokens=tuple(decode_config.get("silence_tokens", []) or ()))
+    t0 = time.time()
+    out = engine.generate(utts, params, seeds=[r.seed for r in requests], parity=parity)
+    t_gen = time.time() - t0
+    y_sep, eos = getattr(model_args, "y_sep_token", None), _eos_token(model_args)
+    frames = [strip_sep_and_eos(g.view(1, 1, -1), y_sep, eos)[0, 0] for g in out["gen"]]
+    lens = [max(1, int(f.numel())) for f in frames]
+    T = max(lens)
+    codes = torch.zeros(len(frames), T, dtype=torch.long)
+    for b, f in enumerate(frames):
+        codes[b, :f.numel()] = f
+    t1 = time.time()
+    wav = audio_tokenizer.codec.decode(codes, lens=lens)
+    torch.cuda.synchronize(wav.device)
+    t_codec = time.time() - t1
+    hop = audio_tokenizer.codec.cfg.hop_length
+    wavs = [wav[b, :, :lens[b] * hop] for b in range(len(frames))]
+    n_tok = sum(len(g) for g in out["gen"])
+    stats = {"tokens": n_tok, "t_generate": t_gen, "t_codec": t_codec,
+             "audio_s": sum(lens) / codec_sr, "rtf": sum(lens) / codec_sr / (t_gen + t_codec)}
+    return wavs, frames, stats

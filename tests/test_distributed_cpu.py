@@ -1,0 +1,77 @@
+"""N>1 path on CPU: world_size-2 gloo runs of the utterance sharding --
+broadcast of the request batch from rank 0, LPT shard assignment, per-rank generate,
+all-gather back into request order. Same code as the RCCL path on GPUs."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import t5gemma_tts_amd  # noqa: F401
+from t5gemma_tts_amd.distributed import assign_shards, pack_requests, run_sharded, unpack_requests
+
+
+def test_assign_shards_balanced_and_deterministic():
+    costs = [751, 300, 751, 120, 500, 500, 60, 900]
+    s = assign_shards(costs, 2)
+    assert sorted(i for sh in s for i in sh) == list(range(len(costs)))
+    loads = [sum(costs[i] for i in sh) for sh in s]
+    assert abs(loads[0] - loads[1]) <= max(costs)
+    assert s == assign_shards(costs, 2)
+    assert assign_shards(costs, 1) == [list(range(8))]
+    capped = assign_shards([1] * 8, 4, max_per_rank=2)
+    assert all(len(x) == 2 for x in capped)
+    with pytest.raises(ValueError):
+        assign_shards([1] * 9, 4, max_per_rank=2)
+    # more ranks than utterances: empty shards allowed
+    assert sum(len(x) for x in assign_shards([5, 4], 8)) == 2
+
+
+def test_pack_roundtrip():
+    rows = [[1, 2, 3], [], [7], list(range(100))]
+    assert unpack_requests(pack_requests(rows)) == rows
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rows = [[i] * (3 + i) for i in range(7)] if rank == 0 else None
+        costs = [10 + (i * 37) % 11 for i in range(7)] if rank == 0 else None
+
+        def generate(shard):   # stand-in for engine.generate: deterministic per utterance
+            return [[v * 2 + rank * 0 for v in r] + [len(r)] for r in shard]
+
+        out, mine = run_sharded(rows, costs, generate, torch.device("cpu"), max_per_rank=4, max_len=16)
+        q.put((rank, out, mine))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_run_sharded_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = [[i * 2] * (3 + i) + [3 + i] for i in range(7)]
+    mines = []
+    for rank, out, mine in res:
+        assert out == expect
+        mines += mine
+    assert sorted(mines) == list(range(7))
