@@ -194,10 +194,11 @@ int t5g_sample_only(t5g_engine* e, int32_t B, const void* logits_dev, int32_t ld
 /* Y = X . W^T on a packed W; epi: 0 bf16, 1 +bias bf16, 2 +bias GELU(erf) bf16, 3 GeGLU(tanh), 4 fp32 slabs */
 int t5g_gemm(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K, int32_t splits,
              const void* bias_dev, void* Y_dev, int32_t ldy, int32_t epi, void* stream);
-/* Time `iters` launches of the decode step's dominant GEMM shape with hipEvents on
- * `stream`; returns average microseconds per launch in *avg_us. */
-int t5g_time_gemm(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K,
-                  int32_t splits, void* Y_dev, int32_t ldy, int32_t epi, int32_t iters, void* stream,
+/* Time `iters` launches of one GEMM shape with hipEvents on `stream`; launch i uses packed
+ * weights Wp_list[i % n_w] (rotate over more bytes than the 256 MiB Infinity Cache to time
+ * HBM-cold streaming as in a real decode step); average microseconds per launch in *avg_us. */
+int t5g_time_gemm(const void* X_dev, int32_t ldx, int32_t M, const void* const* Wp_list, int32_t n_w, int32_t N,
+                  int32_t K, int32_t splits, void* Y_dev, int32_t ldy, int32_t epi, int32_t iters, void* stream,
                   float* avg_us);
 int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, float* avg_us);
 

@@ -802,17 +802,20 @@ extern "C" int t5g_gemm(const void* X, int32_t ldx, int32_t M, const void* Wp, i
     return T5G_OK;
 }
 
-extern "C" int t5g_time_gemm(const void* X, int32_t ldx, int32_t M, const void* Wp, int32_t N, int32_t K,
-                             int32_t splits, void* Y, int32_t ldy, int32_t epi, int32_t iters, void* stream,
-                             float* avg_us) {
-    if (iters <= 0 || !avg_us) return T5G_EINVAL;
+extern "C" int t5g_time_gemm(const void* X, int32_t ldx, int32_t M, const void* const* Wp_list, int32_t n_w,
+                             int32_t N, int32_t K, int32_t splits, void* Y, int32_t ldy, int32_t epi, int32_t iters,
+                             void* stream, float* avg_us) {
+    if (iters <= 0 || !avg_us || !Wp_list || n_w <= 0) return T5G_EINVAL;
+    for (int i = 0; i < n_w; ++i)
+        if (!Wp_list[i]) return T5G_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    RC(gemm((const bf16_t*)X, ldx, M, Wp, N, K, splits, nullptr, Y, ldy, epi, st));  // warm
+    RC(gemm((const bf16_t*)X, ldx, M, Wp_list[0], N, K, splits, nullptr, Y, ldy, epi, st));  // warm
     HIPCHK(hipEventRecord(e0, st));
-    for (int i = 0; i < iters; ++i) RC(gemm((const bf16_t*)X, ldx, M, Wp, N, K, splits, nullptr, Y, ldy, epi, st));
+    for (int i = 0; i < iters; ++i)
+        RC(gemm((const bf16_t*)X, ldx, M, Wp_list[i % n_w], N, K, splits, nullptr, Y, ldy, epi, st));
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;
