@@ -337,6 +337,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     __shared__ float wz[G * 64];
     __shared__ float Linv[G];
     __shared__ int last_flag;
+    __shared__ float qs[G][D];
 
     const int qi = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -358,9 +359,26 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             }
         }
     }
-    // q (+ PM-RoPE) does not depend on the row length either: load it now too
+    // q (+ PM-RoPE) does not depend on the row length either: load it now too.
+    // Split-K slabs are summed once per block into LDS (one f32x4 per slab per thread,
+    // issued alongside the K/V loads), then every lane rotates its 8 q values reading the
+    // rotate_half partner from LDS -- no shuffles, no slab fan-out per lane.
     float q[G][8];
     if (a.Qpart) {
+        for (int idx = threadIdx.x; idx < G * D / 4; idx += 256) {
+            const int g = idx / (D / 4), c4 = idx % (D / 4);
+            f32x4 u[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s < a.q_nsplit)
+                    u[s] = *(const f32x4*)(a.Qpart + ((long)s * a.Mq + qi) * a.ldqp + (kvh * G + g) * D + 4 * c4);
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s < a.q_nsplit) acc += u[s];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) qs[g][4 * c4 + jj] = rbf(acc[jj]);
+        }
         float c8[8], s8[8];
         if (a.rope_tab) {
             const float* tr = a.rope_tab + (long)row * D;
@@ -379,38 +397,18 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
                 s8[jj] = rbf(sinf(ang));
             }
         }
+        __syncthreads();
         const bool lower = dl < LPK / 2;
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            f32x4 u[8][2];
-#pragma unroll
-            for (int s = 0; s < 8; ++s)
-                if (s < a.q_nsplit) {
-                    const f32x4* pp =
-                        (const f32x4*)(a.Qpart + ((long)s * a.Mq + qi) * a.ldqp + (kvh * G + g) * D + 8 * dl);
-                    u[s][0] = pp[0];
-                    u[s][1] = pp[1];
-                }
-#pragma unroll
-            for (int s = 0; s < 8; ++s)
-                if (s < a.q_nsplit) {
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        x[jj] += u[s][0][jj];
-                        x[4 + jj] += u[s][1][jj];
-                    }
-                }
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) x[jj] = rbf(x[jj]);
+        for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
-                const float pr = __shfl_xor(x[jj], LPK / 2, 64);
+                const int dd = 8 * dl + jj;
+                const float x = qs[g][dd];
+                const float pr = qs[g][(dd + D / 2) % D];
                 // lower half: x*c + (-x2)*s ; upper half: x*c + x1*s
-                q[g][jj] = lower ? rbf(rbf(x[jj] * c8[jj]) + rbf(-pr * s8[jj]))
-                                 : rbf(rbf(x[jj] * c8[jj]) + rbf(pr * s8[jj]));
+                q[g][jj] = lower ? rbf(rbf(x * c8[jj]) + rbf(-pr * s8[jj])) : rbf(rbf(x * c8[jj]) + rbf(pr * s8[jj]));
             }
-        }
     } else {
 #pragma unroll
         for (int g = 0; g < G; ++g) {

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <stdlib.h>
 
 #include <vector>
 
@@ -64,6 +65,15 @@ struct t5g_engine {
     int* last_rows;
     int* attn_tickets;  // [max_batch][Hkv] in-launch split-merge counters (self-re-arming)
     float* rope_tab;    // [max_batch][D] per-row cos|sin of the decode step's PM position
+    // multi-block sampler scratch (sampler.hip fast path)
+    float* fs_val;
+    int* fs_idx;
+    int* fs_cnt;
+    float* fs_amv;
+    int* fs_ami;
+    unsigned* fs_ticket;
+    int* fs_slow;
+    bool fast_sampler = true;   // T5G_SAMPLER_FAST=0 at creation: single-block sampler only
     int B = 0;            // rows of the current call
     const bf16_t* noise = nullptr;
     int noise_steps = 0;
@@ -183,6 +193,17 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->last_rows, B);
     rc |= alloc(e, &e->attn_tickets, (int64_t)B * Hkv);
     rc |= alloc(e, &e->rope_tab, (int64_t)B * D);
+    rc |= alloc(e, &e->fs_val, (int64_t)B * FS_NB * FS_CAP);
+    rc |= alloc(e, &e->fs_idx, (int64_t)B * FS_NB * FS_CAP);
+    rc |= alloc(e, &e->fs_cnt, (int64_t)B * FS_NB);
+    rc |= alloc(e, &e->fs_amv, (int64_t)B * FS_NB);
+    rc |= alloc(e, &e->fs_ami, (int64_t)B * FS_NB);
+    rc |= alloc(e, &e->fs_ticket, B);
+    rc |= alloc(e, &e->fs_slow, B);
+    {
+        const char* fsv = getenv("T5G_SAMPLER_FAST");
+        e->fast_sampler = !(fsv && fsv[0] == '0');
+    }
     if (rc) {
         t5g_engine_destroy(e);
         return T5G_ENOMEM;
@@ -678,6 +699,13 @@ static SamplerArgs sampler_args(t5g_engine* e, const bf16_t* logits, int ld, int
     s.next_pos = e->next_pos;
     s.next_token = e->next_token;
     s.flags = e->flags;
+    s.fs_val = e->fs_val;
+    s.fs_idx = e->fs_idx;
+    s.fs_cnt = e->fs_cnt;
+    s.fs_amv = e->fs_amv;
+    s.fs_ami = e->fs_ami;
+    s.fs_ticket = e->fs_ticket;
+    s.fs_slow = e->fast_sampler ? e->fs_slow : nullptr;
     return s;
 }
 

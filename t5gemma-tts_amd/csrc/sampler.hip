@@ -73,7 +73,8 @@ __device__ __forceinline__ int block_argmax(float v, int idx, float* redv, int* 
     __syncthreads();
     float bv = redv[0];
     int bi = redi[0];
-    for (int i = 1; i < NW; ++i)
+    const int nw = (int)(blockDim.x >> 6);
+    for (int i = 1; i < nw; ++i)
         if (redv[i] > bv || (redv[i] == bv && redi[i] < bi)) { bv = redv[i]; bi = redi[i]; }
     return bi;
 }
@@ -85,7 +86,8 @@ __device__ __forceinline__ int block_count(int c, int* redi) {
     if (l == 0) redi[w] = c;
     __syncthreads();
     int s = 0;
-    for (int i = 0; i < NW; ++i) s += redi[i];
+    const int nw = (int)(blockDim.x >> 6);
+    for (int i = 0; i < nw; ++i) s += redi[i];
     return s;
 }
 
@@ -94,14 +96,14 @@ __device__ __forceinline__ void hist_reduce(unsigned (*wh)[256], unsigned* hsum)
     __syncthreads();
     if (threadIdx.x < 256) {
         unsigned s = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) s += wh[w][threadIdx.x];
+        const int nw = (int)(blockDim.x >> 6);
+        for (int w = 0; w < nw; ++w) s += wh[w][threadIdx.x];
         hsum[threadIdx.x] = s;
     }
     __syncthreads();
 }
 __device__ __forceinline__ void hist_clear(unsigned (*wh)[256]) {
-    for (int i = threadIdx.x; i < NW * 256; i += SN) (&wh[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < (int)(blockDim.x >> 6) * 256; i += blockDim.x) (&wh[0][0])[i] = 0;
     __syncthreads();
 }
 
@@ -153,6 +155,52 @@ __device__ __forceinline__ uint32_t philox(uint32_t c0, uint32_t c1, uint32_t c2
     return c0;
 }
 
+// The exponential draw q of torch.multinomial for element i: parity mode reads the
+// uploaded reference stream, production draws Philox4x32-10(i, step, row; seed).
+__device__ __forceinline__ float draw_q(const SamplerArgs& a, const SamplerRow& pr, const SamplerState& st, int b,
+                                        int i) {
+    if (a.noise) return bf2f(a.noise[((long)b * a.noise_steps + st.cur_num_gen) * a.V + i]);
+    const uint32_t u = philox((uint32_t)i, (uint32_t)st.cur_num_gen, (uint32_t)b, pr.seed_lo, pr.seed_hi);
+    const float uf = ((float)(u >> 8) + 1.0f) * (1.0f / 16777216.0f);
+    float q = rbf(-logf(uf));
+    if (q <= 0.f) q = 5.9604645e-08f;
+    return q;
+}
+
+// Stop rules + per-row state update (:753-786, :806-832); one thread.
+__device__ void finish_row(const SamplerArgs& a, const SamplerRow& pr, SamplerState st, int b, int token, int amax,
+                           int ambiguous, int eff_len) {
+    bool force = (token == a.eos) || (amax == a.eos);
+    if (a.text_guard > 0) force = force || (eff_len > max(1, st.first_input_len) * a.text_guard);
+    bool budget = st.target_total >= 0 &&
+                  (double)st.cur_num_gen > (double)(st.target_total - st.prompt_offset) + (double)a.budget_extra;
+    if (force || budget) token = a.eos;
+    bool in_sil = false;
+    for (int s = 0; s < pr.n_silence; ++s) in_sil |= (a.silence[pr.silence_off + s] == token);
+    if (in_sil && token == st.prev_token)
+        st.consec_silence += 1;
+    else
+        st.consec_silence = 0;
+    st.prev_token = token;
+    a.out_tokens[(long)b * a.max_gen + st.cur_num_gen] = token;
+    st.cur_num_gen += 1;
+    st.current_length += 1;
+    st.last_token = token;
+    st.ambiguous_steps += ambiguous;
+    if (token == a.eos || st.cur_num_gen >= a.max_gen) {
+        st.done = 1;
+    } else {
+        double v = (double)(st.current_length - 1) / (double)max(1, st.est_total - 1) * (double)a.progress_scale;
+        v = v < (double)a.progress_scale ? v : (double)a.progress_scale;
+        st.next_pos = (float)v;
+        a.kv_len[b] = st.current_length;
+        a.next_pos[b] = st.next_pos;
+        a.next_token[b] = token;
+    }
+    if (a.flags) a.flags[b] = ambiguous | (amax == a.eos ? 2 : 0);
+    a.state[b] = st;
+}
+
 __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
     __shared__ float redv[NW];
     __shared__ int redi[NW];
@@ -170,6 +218,7 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
     const int lane = tid & 63, wid = tid >> 6;
     SamplerState st = a.state[b];
     if (st.done) return;
+    if (a.fs_slow && !a.fs_slow[b]) return;   // finished by sampler_fast_kernel this step
     const SamplerRow pr = a.rows[b];
     const int V = a.V;
     const bf16_t* lg = a.logits + (long)b * a.ldl;
@@ -484,59 +533,325 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
             if (xv == -INFINITY) continue;  // p = 0 -> r = 0 can never beat a survivor
             const float p = rbf(expf(xv - m) * inv);
             float r = 0.f;
-            if (p > 0.f) {
-                float q;
-                if (nz) {
-                    q = bf2f(nz[i]);
-                } else {
-                    uint32_t u = philox((uint32_t)i, (uint32_t)st.cur_num_gen, (uint32_t)b, pr.seed_lo, pr.seed_hi);
-                    float uf = ((float)(u >> 8) + 1.0f) * (1.0f / 16777216.0f);
-                    q = rbf(-logf(uf));
-                    if (q <= 0.f) q = 5.9604645e-08f;
-                }
-                r = rbf(p / q);
-            }
+            if (p > 0.f) r = rbf(p / (nz ? bf2f(nz[i]) : draw_q(a, pr, st, b, i)));
             if (r > bv || (r == bv && i < bi)) { bv = r; bi = i; }
         }
         token = block_argmax(bv, bi, redv, redi);
     }
     // ---- 8. stop rules + state (:753-786, :806-832)
-    if (tid == 0) {
-        bool force = (token == a.eos) || (amax == a.eos);
-        if (a.text_guard > 0) force = force || (eff_len > max(1, st.first_input_len) * a.text_guard);
-        bool budget = st.target_total >= 0 &&
-                      (double)st.cur_num_gen > (double)(st.target_total - st.prompt_offset) + (double)a.budget_extra;
-        if (force || budget) token = a.eos;
-        bool in_sil = false;
-        for (int s = 0; s < pr.n_silence; ++s) in_sil |= (a.silence[pr.silence_off + s] == token);
-        if (in_sil && token == st.prev_token)
-            st.consec_silence += 1;
-        else
-            st.consec_silence = 0;
-        st.prev_token = token;
-        a.out_tokens[(long)b * a.max_gen + st.cur_num_gen] = token;
-        st.cur_num_gen += 1;
-        st.current_length += 1;
-        st.last_token = token;
-        st.ambiguous_steps += ambiguous;
-        if (token == a.eos || st.cur_num_gen >= a.max_gen) {
-            st.done = 1;
-        } else {
-            double v = (double)(st.current_length - 1) / (double)max(1, st.est_total - 1) * (double)a.progress_scale;
-            v = v < (double)a.progress_scale ? v : (double)a.progress_scale;
-            st.next_pos = (float)v;
-            a.kv_len[b] = st.current_length;
-            a.next_pos[b] = st.next_pos;
-            a.next_token[b] = token;
-        }
-        if (a.flags) a.flags[b] = ambiguous | (amax == a.eos ? 2 : 0);
-        a.state[b] = st;
+    if (tid == 0) finish_row(a, pr, st, b, token, amax, ambiguous, eff_len);
+}
+
+
+// ============================================================================
+// Multi-block fast path. The single-block kernel above keeps a whole 65 541-entry
+// row in one CU; with top-k active (the reference's defaults: k = 30, p = 0.9,
+// inference_commandline_hf.py:80-83) everything after the top-k filter involves only
+// the survivors, so the row is split over FS_NB blocks:
+//   every block: edits + argmax + temperature over its slice, then its LOCAL top-k
+//     candidates (all values >= the slice's k-th largest, ties included);
+//   the last block to arrive (atomic ticket): merges the candidates (the global top-k
+//     is a subset of them), takes the k-th largest as the threshold, sorts the
+//     survivors (value desc, index asc), runs the top-p walk over distinct values,
+//     softmaxes the final survivors and samples argmax(bf16(p / q)) -- the same
+//     arithmetic as the single-block kernel -- then applies the stop rules.
+// Rows the fast path cannot take (min_p, top-k off or > FS_KMAX, a slice with more
+// than FS_CAP candidates, more than FS_SMAX survivors) are flagged in fs_slow and
+// finished by the single-block kernel launched right after.
+constexpr int FT = 256;
+__device__ __forceinline__ bool lane_ok(int t) { return t < FS_NB; }
+constexpr int FEPT = 24;   // V <= FS_NB * FT * FEPT = 98304
+
+__device__ __forceinline__ float block_argmax_v(float v, int& idx, float* redv, int* redi) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float ov = __shfl_xor(v, o, 64);
+        int oi = __shfl_xor(idx, o, 64);
+        if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
     }
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) { redv[w] = v; redi[w] = idx; }
+    __syncthreads();
+    float bv = redv[0];
+    int bi = redi[0];
+    const int nw = (int)(blockDim.x >> 6);
+    for (int i = 1; i < nw; ++i)
+        if (redv[i] > bv || (redv[i] == bv && redi[i] < bi)) { bv = redv[i]; bi = redi[i]; }
+    idx = bi;
+    return bv;
+}
+
+__global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
+    __shared__ float redv[FT / 64];
+    __shared__ int redi[FT / 64];
+    __shared__ unsigned wh[FT / 64][256];
+    __shared__ unsigned hsum[256];
+    __shared__ int sh_int[8];
+    __shared__ float cv[FS_NB * FS_CAP];
+    __shared__ int ci[FS_NB * FS_CAP];
+    __shared__ float sv[FS_SMAX];
+    __shared__ int si[FS_SMAX];
+    __shared__ int soff[FS_NB + 1];
+    __shared__ int is_last;
+
+    const int sl = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, wid = tid >> 6;
+    SamplerState st = a.state[b];
+    if (st.done) return;
+    const SamplerRow pr = a.rows[b];
+    int kk = pr.top_k;
+    if (pr.top_k_list_len > 0) kk = a.top_k_list[pr.top_k_list_off + min(pr.top_k_list_len - 1, st.cur_num_gen)];
+    const bool fast = kk > 0 && kk <= FS_KMAX && !(pr.min_p > 0.f && pr.min_p < 1.f);
+    if (!fast) {
+        if (sl == 0 && tid == 0) a.fs_slow[b] = 1;
+        return;
+    }
+    const int V = a.V;
+    const int k = min(kk, V);
+    const int SL = (V + FS_NB - 1) / FS_NB;
+    const int i0 = sl * SL, i1 = min(V, i0 + SL);
+    const bf16_t* lg = a.logits + (long)b * a.ldl;
+    // ---- 1-3. edits, argmax of the edited logits, temperature (as sampler_kernel)
+    const int eff_len = max(0, st.current_length - st.prompt_offset);
+    bool in_sil_prev = false;
+    for (int q = 0; q < pr.n_silence; ++q) in_sil_prev |= (a.silence[pr.silence_off + q] == st.prev_token);
+    const bool sil_rule = pr.stop_repetition > 0 && in_sil_prev && st.consec_silence > pr.stop_repetition;
+    const float sil_f = (float)(st.consec_silence - (pr.stop_repetition - 1));
+    float x[FEPT];
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < FEPT; ++j) {
+        const int i = i0 + tid + FT * j;
+        x[j] = -INFINITY;
+        if (i < i1) {
+            float v = bf2f(lg[i]);
+            if (i == a.eos) {
+                if (eff_len == 0) v = rbf(-1e9f);
+                if (st.cur_num_gen <= a.eos_guard) v = rbf(-10000.0f);
+                if (pr.eos_disabled) v = -INFINITY;
+                v = rbf(v);
+            }
+            if (sil_rule && i == st.prev_token) v = rbf(v < 0.f ? v * sil_f : v / sil_f);
+            if (v > bv || bi == 0x7fffffff) { bv = v; bi = i; }
+            x[j] = pr.temperature != 1.0f ? rbf(v / pr.temperature) : v;
+        }
+    }
+    const float amv = block_argmax_v(bv, bi, redv, redi);
+    // ---- 5a. local top-k candidates (k-th largest of the slice, ties kept)
+    float thr = -INFINITY;
+    if (i1 - i0 > k) {
+        hist_clear(wh);
+#pragma unroll
+        for (int j = 0; j < FEPT; ++j)
+            if (i0 + tid + FT * j < i1) atomicAdd(&wh[wid][okey(x[j]) >> 8], 1u);
+        hist_reduce(wh, hsum);
+        if (wid == 0) find_bin_wave0(hsum, k, &sh_int[0], &sh_int[1]);
+        __syncthreads();
+        const uint32_t hb = (uint32_t)sh_int[0];
+        const int need = k - sh_int[1];
+        hist_clear(wh);
+#pragma unroll
+        for (int j = 0; j < FEPT; ++j)
+            if (i0 + tid + FT * j < i1) {
+                const uint32_t kq = okey(x[j]);
+                if ((kq >> 8) == hb) atomicAdd(&wh[wid][kq & 255u], 1u);
+            }
+        hist_reduce(wh, hsum);
+        if (wid == 0) find_bin_wave0(hsum, need, &sh_int[2], &sh_int[3]);
+        __syncthreads();
+        thr = key2f((hb << 8) | (uint32_t)sh_int[2]);
+    }
+    if (tid == 0) sh_int[4] = 0;
+    __syncthreads();
+    float* gv = a.fs_val + ((long)b * FS_NB + sl) * FS_CAP;
+    int* gi = a.fs_idx + ((long)b * FS_NB + sl) * FS_CAP;
+#pragma unroll
+    for (int j = 0; j < FEPT; ++j) {
+        const int i = i0 + tid + FT * j;
+        if (i < i1 && x[j] >= thr) {
+            const int p = atomicAdd(&sh_int[4], 1);
+            if (p < FS_CAP) {
+                gv[p] = x[j];
+                gi[p] = i;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.fs_cnt[b * FS_NB + sl] = sh_int[4] > FS_CAP ? -1 : sh_int[4];
+        a.fs_amv[b * FS_NB + sl] = amv;
+        a.fs_ami[b * FS_NB + sl] = bi;
+    }
+    // ---- arrival ticket: the last slice block of the row finishes it
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) is_last = atomicAdd(&a.fs_ticket[b], 1u) == (unsigned)(FS_NB - 1);
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    // slice counts / argmaxes: one load per lane of wave 0, scan + argmax in registers
+    if (wid == 0) {
+        int c = 0, mi = 0x7fffffff;
+        float mv = -INFINITY;
+        if (lane_ok(tid)) {
+            c = a.fs_cnt[b * FS_NB + tid];
+            mv = a.fs_amv[b * FS_NB + tid];
+            mi = a.fs_ami[b * FS_NB + tid];
+        }
+        const unsigned long long badm = __ballot(c < 0);
+        int inc = max(c, 0);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(inc, o, 64);
+            if (tid >= o) inc += t;
+        }
+        if (tid < FS_NB) soff[tid + 1] = inc;
+        if (tid == 0) {
+            soff[0] = 0;
+            sh_int[5] = badm != 0ull;
+            a.fs_ticket[b] = 0;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(mv, o, 64);
+            const int oi = __shfl_xor(mi, o, 64);
+            if (ov > mv || (ov == mv && oi < mi)) { mv = ov; mi = oi; }
+        }
+        if (tid == 0) sh_int[6] = mi;
+    }
+    __syncthreads();
+    if (sh_int[5]) {
+        if (tid == 0) a.fs_slow[b] = 1;
+        return;
+    }
+    const int amax = sh_int[6];
+    const int n = soff[FS_NB];
+    for (int q = tid; q < n; q += FT) {
+        int sidx = 0;
+#pragma unroll
+        for (int t = 1; t < FS_NB; ++t) sidx += (q >= soff[t]);
+        const long src = ((long)b * FS_NB + sidx) * FS_CAP + (q - soff[sidx]);
+        cv[q] = a.fs_val[src];
+        ci[q] = a.fs_idx[src];
+    }
+    __syncthreads();
+    // ---- 5b. global k-th largest over the merged candidates
+    float gthr = -INFINITY;
+    if (n > k) {
+        hist_clear(wh);
+        for (int q = tid; q < n; q += FT) atomicAdd(&wh[wid][okey(cv[q]) >> 8], 1u);
+        hist_reduce(wh, hsum);
+        if (wid == 0) find_bin_wave0(hsum, k, &sh_int[0], &sh_int[1]);
+        __syncthreads();
+        const uint32_t hb = (uint32_t)sh_int[0];
+        const int need = k - sh_int[1];
+        hist_clear(wh);
+        for (int q = tid; q < n; q += FT) {
+            const uint32_t kq = okey(cv[q]);
+            if ((kq >> 8) == hb) atomicAdd(&wh[wid][kq & 255u], 1u);
+        }
+        hist_reduce(wh, hsum);
+        if (wid == 0) find_bin_wave0(hsum, need, &sh_int[2], &sh_int[3]);
+        __syncthreads();
+        gthr = key2f((hb << 8) | (uint32_t)sh_int[2]);
+    }
+    if (tid == 0) sh_int[4] = 0;
+    __syncthreads();
+    for (int q = tid; q < n; q += FT)
+        if (cv[q] >= gthr) {
+            const int p = atomicAdd(&sh_int[4], 1);
+            if (p < FS_SMAX) {
+                sv[p] = cv[q];
+                si[p] = ci[q];
+            }
+        }
+    __syncthreads();
+    const int ns = sh_int[4];
+    if (ns > FS_SMAX) {
+        if (tid == 0) a.fs_slow[b] = 1;
+        return;
+    }
+    // survivors sorted by (value desc, index asc) into cv / ci
+    if (tid < ns) {
+        const float v = sv[tid];
+        const int i = si[tid];
+        int rank = 0;
+        for (int r = 0; r < ns; ++r) rank += (sv[r] > v) || (sv[r] == v && si[r] < i);
+        cv[rank] = v;
+        ci[rank] = i;
+    }
+    __syncthreads();
+    const float m = cv[0];
+    // ---- 6. top-p walk over distinct values (:118-129)
+    int nkeep = ns, ambiguous = 0;
+    if (pr.top_p < 1.0f) {
+        float ls = 0.f;
+        if (tid < ns && cv[tid] > -INFINITY) ls = expf(cv[tid] - m);
+        const float inv = 1.0f / block_sum(ls, redv);
+        if (tid == 0) {
+            const float pthr = rbf(pr.top_p);
+            float acc = 0.f;
+            int keep_n = ns, amb = 0;
+            for (int q = 0; q < ns;) {
+                const float v = cv[q];
+                int c = 1;
+                while (q + c < ns && cv[q + c] == v) ++c;
+                if (v == -INFINITY) break;
+                const float pv = rbf(expf(v - m) * inv);
+                bool cut = false;
+                for (int r = 0; r < c; ++r) {
+                    acc += pv;
+                    if (rbf(acc) > pthr) {
+                        keep_n = q + r + 1;
+                        amb = (r + 1 < c);
+                        cut = true;
+                        break;
+                    }
+                }
+                if (cut) break;
+                q += c;
+            }
+            sh_int[0] = keep_n;
+            sh_int[1] = amb;
+        }
+        __syncthreads();
+        nkeep = sh_int[0];
+        ambiguous = sh_int[1];
+    }
+    // ---- 7. softmax over the kept survivors + multinomial-as-argmax(p / q)
+    float ls = 0.f;
+    if (tid < nkeep && cv[tid] > -INFINITY) ls = expf(cv[tid] - m);
+    const float inv = 1.0f / block_sum(ls, redv);
+    float rbv = -1.f;
+    int rbi = 0x7fffffff;
+    if (tid < nkeep && cv[tid] > -INFINITY) {
+        const int i = ci[tid];
+        const float p = rbf(expf(cv[tid] - m) * inv);
+        float r = 0.f;
+        if (p > 0.f) r = rbf(p / draw_q(a, pr, st, b, i));
+        rbv = r;
+        rbi = i;
+    }
+    int token = rbi;
+    block_argmax_v(rbv, token, redv, redi);
+    if (tid == 0) {
+        a.fs_slow[b] = 0;
+        finish_row(a, pr, st, b, token, amax, ambiguous, eff_len);
+    }
+}
+
+size_t sampler_fast_ws_bytes(int B) {
+    return (size_t)B * ((size_t)FS_NB * FS_CAP * 8 + (size_t)FS_NB * 12 + 8);
 }
 
 int sample(const SamplerArgs& a, hipStream_t st) {
     if (a.B <= 0) return 0;
     if (a.V > SN * SPER) return -1;
+    if (a.fs_slow) {
+        if (a.V > FS_NB * FT * FEPT || !a.fs_val || !a.fs_ticket) return -1;
+        hipLaunchKernelGGL(sampler_fast_kernel, dim3(FS_NB, (unsigned)a.B), dim3(FT), 0, st, a);
+    }
     hipLaunchKernelGGL(sampler_kernel, dim3((unsigned)a.B), dim3(SN), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -146,6 +146,19 @@ struct SamplerArgs {
     int* next_token;          // [B] token fed to the next decoder step
     int* flags;               // [B] per-step debug: bit0 ambiguous
     unsigned* hist;           // scratch [B][65536] (top-p histogram walk)
+    // multi-block fast path (top-k <= FS_KMAX, no min_p): per-slice candidates
+    float* fs_val;            // [B][FS_NB][FS_CAP] temperature-scaled candidate values
+    int* fs_idx;              // [B][FS_NB][FS_CAP]
+    int* fs_cnt;              // [B][FS_NB] candidates written (-1: overflow)
+    float* fs_amv;            // [B][FS_NB] slice argmax value (edited logits)
+    int* fs_ami;              // [B][FS_NB] slice argmax index
+    unsigned* fs_ticket;      // [B] arrival counters (reset by the last block)
+    int* fs_slow;             // [B] 1: row left to the single-block kernel this step
 };
+constexpr int FS_NB = 16;     // slices (blocks) per row
+constexpr int FS_CAP = 128;   // candidates per slice
+constexpr int FS_KMAX = 64;   // largest top-k the fast path takes
+constexpr int FS_SMAX = 256;  // largest top-k survivor set (ties) the fast path takes
+size_t sampler_fast_ws_bytes(int B);
 int sample(const SamplerArgs& a, hipStream_t st);
 }  // namespace t5g

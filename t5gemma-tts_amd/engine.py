@@ -72,7 +72,9 @@ class T5GemmaTTSEngine:
 
     def __init__(self, cfg: VoiceConfig, state_dict: Dict[str, torch.Tensor], device="cuda:0",
                  max_batch: int = 8, max_text: int = 128, max_audio: int = 1024, max_gen: Optional[int] = None,
-                 free_source: bool = False):
+                 free_source: bool = False, shared_from: Optional["T5GemmaTTSEngine"] = None):
+        """``shared_from``: reuse another engine's packed weights on the same device (e.g. a
+        second KV arena / batch slot set without a second 10.6 GB weight copy)."""
         if not torch.cuda.is_available():
             raise RuntimeError("T5GemmaTTSEngine needs a ROCm GPU (MI355X); there is no CPU fallback")
         self.L = _lib.lib()
@@ -82,9 +84,16 @@ class T5GemmaTTSEngine:
         self.V = cfg.n_audio_tokens
         self.max_batch, self.max_text, self.max_audio = max_batch, max_text, max_audio
         self.max_gen = max_gen or max_audio
+        dev = self.device
+        if shared_from is not None:
+            if shared_from.device != dev or shared_from.cfg != cfg:
+                raise ValueError("shared_from must be an engine of the same config on the same device")
+            self._keep = shared_from._keep
+            self._enc, self._dec, self._weights = shared_from._enc, shared_from._dec, shared_from._weights
+            self._create(cfg, shared_from._weights)
+            return
         check_state_dict(cfg, state_dict)
         self._keep: List[torch.Tensor] = []
-        dev = self.device
 
         def w(name):
             t = state_dict[name]
@@ -150,7 +159,12 @@ class T5GemmaTTSEngine:
         self._weights = W
         if free_source:
             state_dict.clear()
+        self._create(cfg, W)
 
+    def _create(self, cfg: VoiceConfig, W) -> None:
+        bb, dev = cfg.backbone, self.device
+        d, f = bb.hidden_size, bb.intermediate_size
+        max_batch, max_text, max_audio = self.max_batch, self.max_text, self.max_audio
         c = _lib.Config()
         c.hidden, c.intermediate = d, f
         c.n_enc_layers, c.n_dec_layers = bb.num_encoder_layers, bb.num_decoder_layers
@@ -222,6 +236,17 @@ class T5GemmaTTSEngine:
         stream (seed per row, reseeded before the loop) and resolves tie-ambiguous
         top-p steps on the host -- token-exact reproduction mode (slow: one host
         sync per step). Returns dict(res=[...], gen=[...], steps, ambiguous)."""
+        stream = _stream(self.device)
+        ctx = self._prepare(utts, params, seeds, parity, stream)
+        if parity:
+            self._run_parity(ctx, stream, record_logits)
+        else:
+            while not self._decode_chunk(ctx, chunk, use_graph, stream):
+                pass
+        return self._collect(ctx, stream)
+
+    # -- phases ------------------------------------------------------------------
+    def _prepare(self, utts, params, seeds, parity, stream):
         cfg, dev = self.cfg, self.device
         B = len(utts)
         if B < 1:
@@ -231,8 +256,6 @@ class T5GemmaTTSEngine:
         if isinstance(params, SamplingParams):
             params = [params] * B
         seeds = list(seeds) if seeds is not None else list(range(1, B + 1))
-        stream = _stream(dev)
-        eos = cfg.eog_inference
         # ---- host plumbing: packed text / audio tokens and float PM positions
         ids, trow, tt, tpos, tlen = [], [], [], [], []
         aid, arow, at, apos, alen, last = [], [], [], [], [], []
@@ -309,6 +332,8 @@ class T5GemmaTTSEngine:
         if parity:
             noise = torch.stack([reference_noise(s, max_steps, self.V) for s in seeds[:B]]).to(dev)
         L = self.L
+        # the host tensors above were filled on torch's current stream: order them first
+        torch.cuda.current_stream(dev).synchronize()
         _lib.check(L.t5g_encode(self.h, B, len(ids), _ptr(d_ids), _ptr(d_trow), _ptr(d_tt), _ptr(d_tpos),
                                 _ptr(d_tlen), stream), "encode")
         _lib.check(L.t5g_prefill(self.h, B, len(aid), _ptr(d_aid), _ptr(d_arow), _ptr(d_at), _ptr(d_apos),
@@ -317,69 +342,83 @@ class T5GemmaTTSEngine:
         sl = (C.c_int32 * max(1, len(silence)))(*silence)
         _lib.check(L.t5g_sampler_setup(self.h, B, rows, states, tk, len(topk_list), sl, len(silence),
                                        _ptr(noise), max_steps if parity else 0, stream), "sampler_setup")
+        return {"B": B, "rows": rows, "tk": tk, "sl": sl, "noise": noise, "y_rows": y_rows,
+                "max_steps": max_steps, "steps": 0, "ambiguous_fixed": 0, "rec": None,
+                "cur": (_lib.SamplerState * B)(), "keep": (d_ids, d_trow, d_tt, d_tpos, d_tlen, d_aid, d_arow, d_at,
+                                                          d_apos, d_alen, d_last)}
+
+    def _decode_chunk(self, ctx, chunk: int, use_graph: bool, stream) -> bool:
+        """Enqueue up to ``chunk`` graph-replayed decode steps, then read the row states
+        (one host sync). Returns True when every row is done."""
+        n = max(1, min(chunk, ctx["max_steps"] + 1 - ctx["steps"]))
+        _lib.check(self.L.t5g_decode(self.h, n, 1 if use_graph else 0, stream), "decode")
+        ctx["steps"] += n
+        return self._poll(ctx, stream)
+
+    def _poll(self, ctx, stream) -> bool:
+        B, cur = ctx["B"], ctx["cur"]
+        _lib.check(self.L.t5g_read_state(self.h, cur, B, stream), "read_state")
+        if all(cur[b].done for b in range(B)):
+            return True
+        if ctx["steps"] > ctx["max_steps"] + 2:
+            raise RuntimeError("decode did not terminate within the time budget")
+        return False
+
+    def _run_parity(self, ctx, stream, record_logits: bool) -> None:
+        L, B, cfg = self.L, ctx["B"], self.cfg
+        rows, tk, sl, noise = ctx["rows"], ctx["tk"], ctx["sl"], ctx["noise"]
+        eos = cfg.eog_inference
         rec = [] if record_logits else None
-        ambiguous_fixed = 0
-        steps = 0
-        if parity:
-            cur = (_lib.SamplerState * B)()
+        cur = ctx["cur"]
+        _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
+        flags = (C.c_int32 * B)()
+        while not all(cur[b].done for b in range(B)):
+            if rec is not None:
+                rec.append(self.logits(B).clone())
+            pre = (_lib.SamplerState * B)()
+            C.memmove(pre, cur, C.sizeof(cur))
+            _lib.check(L.t5g_sample_only(self.h, B, C.c_void_p(self._logits_ptr), self.logits_ld, stream), "sample")
+            _lib.check(L.t5g_read_flags(self.h, flags, B, stream), "read_flags")
+            for b in range(B):
+                if pre[b].done or not (flags[b] & 1):
+                    continue
+                lg = self.logits(B)[b].contiguous().cpu()
+                nz = noise[b, pre[b].cur_num_gen].contiguous().cpu()
+                out_st = _lib.SamplerState()
+                tok = C.c_int32()
+                _lib.check(L.t5g_host_sample(
+                    _ptr(lg), self.V, C.byref(rows[b]), tk, sl, C.byref(pre[b]), _ptr(nz), eos,
+                    self._cfg.eos_guard, self._cfg.budget_extra, self._cfg.text_guard,
+                    self._cfg.progress_scale, self.max_gen, C.byref(out_st), C.byref(tok)), "host_sample")
+                out_st.ambiguous_steps = pre[b].ambiguous_steps + 1
+                _lib.check(L.t5g_write_state(self.h, C.byref(out_st), b, pre[b].cur_num_gen, tok.value,
+                                             stream), "write_state")
+                ctx["ambiguous_fixed"] += 1
             _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
-            flags = (C.c_int32 * B)()
-            while not all(cur[b].done for b in range(B)):
-                if rec is not None:
-                    rec.append(self.logits(B).clone())
-                pre = (_lib.SamplerState * B)()
-                C.memmove(pre, cur, C.sizeof(cur))
-                _lib.check(L.t5g_sample_only(self.h, B, C.c_void_p(self._logits_ptr), self.logits_ld, stream),
-                           "sample")
-                _lib.check(L.t5g_read_flags(self.h, flags, B, stream), "read_flags")
-                for b in range(B):
-                    if pre[b].done or not (flags[b] & 1):
-                        continue
-                    lg = self.logits(B)[b].contiguous().cpu()
-                    nz = noise[b, pre[b].cur_num_gen].contiguous().cpu()
-                    out_st = _lib.SamplerState()
-                    tok = C.c_int32()
-                    _lib.check(L.t5g_host_sample(
-                        _ptr(lg), self.V, C.byref(rows[b]), tk, sl, C.byref(pre[b]), _ptr(nz), eos,
-                        self._cfg.eos_guard, self._cfg.budget_extra, self._cfg.text_guard,
-                        self._cfg.progress_scale, self.max_gen, C.byref(out_st), C.byref(tok)), "host_sample")
-                    out_st.ambiguous_steps = pre[b].ambiguous_steps + 1
-                    _lib.check(L.t5g_write_state(self.h, C.byref(out_st), b, pre[b].cur_num_gen, tok.value,
-                                                 stream), "write_state")
-                    ambiguous_fixed += 1
-                _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
-                steps += 1
-                if not all(cur[b].done for b in range(B)):
-                    _lib.check(L.t5g_step_only(self.h, stream), "step")
-        else:
-            cur = (_lib.SamplerState * B)()
-            while True:
-                n = min(chunk, max_steps + 1 - steps)
-                n = max(n, 1)
-                _lib.check(L.t5g_decode(self.h, n, 1 if use_graph else 0, stream), "decode")
-                steps += n
-                _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
-                if all(cur[b].done for b in range(B)):
-                    break
-                if steps > max_steps + 2:
-                    raise RuntimeError("decode did not terminate within the time budget")
+            ctx["steps"] += 1
+            if not all(cur[b].done for b in range(B)):
+                _lib.check(L.t5g_step_only(self.h, stream), "step")
+        ctx["rec"] = rec
+
+    def _collect(self, ctx, stream):
+        cfg, B, cur = self.cfg, ctx["B"], ctx["cur"]
         toks = (C.c_int32 * (B * self.max_gen))()
-        _lib.check(L.t5g_read_tokens(self.h, toks, B, stream), "read_tokens")
+        _lib.check(self.L.t5g_read_tokens(self.h, toks, B, stream), "read_tokens")
         res, gen = [], []
         for b in range(B):
             n = cur[b].cur_num_gen
             g = [toks[b * self.max_gen + i] for i in range(n)]
             gt = torch.tensor(g, dtype=torch.long)
-            rt = torch.cat([torch.tensor(y_rows[b], dtype=torch.long), gt])
+            rt = torch.cat([torch.tensor(ctx["y_rows"][b], dtype=torch.long), gt])
             if cfg.special_first:
                 rt = rt - int(cfg.n_special)
                 gt = gt - int(cfg.n_special)
             res.append(rt)
             gen.append(gt)
-        out = {"res": res, "gen": gen, "steps": steps,
-               "ambiguous": [cur[b].ambiguous_steps for b in range(B)], "ambiguous_fixed": ambiguous_fixed}
-        if rec is not None:
-            out["logits"] = rec
+        out = {"res": res, "gen": gen, "steps": ctx["steps"],
+               "ambiguous": [cur[b].ambiguous_steps for b in range(B)], "ambiguous_fixed": ctx["ambiguous_fixed"]}
+        if ctx["rec"] is not None:
+            out["logits"] = ctx["rec"]
         return out
 
 

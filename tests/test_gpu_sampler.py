@@ -1,0 +1,131 @@
+"""Randomised parity of the on-device sampler (SURVEY a13/a14/a14') at V = 65 541.
+
+* Every row's device token (multi-block fast path for top-k <= 64, single-block kernel
+  otherwise) must equal the exact host restatement of the reference sampler
+  (t5g_host_sample, libstdc++ std::sort tie order) fed the same bf16 logits and the
+  same reference noise draw -- except rows the kernel itself flags ambiguous (a tie
+  group straddling the top-p cut), which parity mode resolves on the host.
+* With production (Philox) noise, the fast path and the single-block kernel
+  (T5G_SAMPLER_FAST=0) must pick the same tokens.
+"""
+import ctypes as C
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+BF16 = torch.bfloat16
+V = 65541
+EOS = 65539
+
+
+def _engine(B):
+    import t5gemma_tts_amd  # noqa: F401
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import T5GemmaTTSEngine
+    from t5gemma_tts_amd.weights import synthetic_weights
+    cfg = named_config("tiny")
+    cfg.audio_vocab_size = 65536
+    cfg.empty_token, cfg.eog, cfg.audio_pad_token, cfg.eos, cfg.y_sep_token = 65536, 65537, 65538, 65539, 65540
+    return T5GemmaTTSEngine(cfg, synthetic_weights(cfg, 3), device="cuda:0", max_batch=B, max_text=16,
+                            max_audio=256, max_gen=128)
+
+
+def _logits(g, B, mode):
+    x = torch.randn(B, V, generator=g) * (2.0 if mode != "flat" else 0.3)
+    if mode == "quant":      # heavy ties everywhere (incl. at the top-k / top-p cuts)
+        x = (x * 4).round() / 4
+    if mode == "peaky":
+        x[:, torch.randint(0, V, (5,), generator=g)] += 8.0
+    return x.to(BF16)
+
+
+PARAMS = [(30, 0.9, 0.8), (30, 1.0, 1.0), (1, 1.0, 1.0), (5, 0.5, 1.3), (64, 0.95, 0.7), (50, 0.3, 1.0),
+          (100, 0.9, 0.8), (0, 0.9, 1.0), (10, 0.99, 2.0)]
+
+
+def _rows_states(B, plist, noise_seeded):
+    from t5gemma_tts_amd import _lib
+    rows = (_lib.SamplerRow * B)()
+    sts = (_lib.SamplerState * B)()
+    for b in range(B):
+        k, p, t = plist[b % len(plist)]
+        rows[b] = _lib.SamplerRow(top_k=k, top_p=p, temperature=t, seed_lo=1000 + b)
+        sts[b] = _lib.SamplerState(cur_num_gen=100, current_length=200, prompt_offset=1, target_total=-1,
+                                   est_total=1000, prev_token=-1, first_input_len=5)
+    return rows, sts
+
+
+def _run(eng, B, lg, rows, sts, noise=None, steps=0):
+    from t5gemma_tts_amd import _lib
+    L = eng.L
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    tk = (C.c_int32 * 1)()
+    _lib.check(L.t5g_sampler_setup(eng.h, B, rows, sts, tk, 0, tk, 0,
+                                   C.c_void_p(noise.data_ptr()) if noise is not None else None, steps, st), "setup")
+    dlg = torch.zeros(B, V + 11, dtype=BF16, device="cuda")
+    dlg[:, :V] = lg.cuda()
+    _lib.check(L.t5g_sample_only(eng.h, B, C.c_void_p(dlg.data_ptr()), V + 11, st), "sample")
+    out = (_lib.SamplerState * B)()
+    _lib.check(L.t5g_read_state(eng.h, out, B, st), "read")
+    flags = (C.c_int32 * B)()
+    L.t5g_read_flags(eng.h, flags, B, st)
+    return [out[b].last_token for b in range(B)], [flags[b] for b in range(B)]
+
+
+@pytest.mark.parametrize("mode", ["normal", "quant", "peaky", "flat"])
+def test_device_sampler_equals_host_reference(mode):
+    from t5gemma_tts_amd import _lib
+    from t5gemma_tts_amd.engine import reference_noise
+    B = 8
+    eng = _engine(B)
+    g = torch.Generator().manual_seed({"normal": 1, "quant": 2, "peaky": 3, "flat": 4}[mode])
+    tk = (C.c_int32 * 1)()
+    checked = amb = 0
+    for it in range(6):
+        lg = _logits(g, B, mode)
+        plist = PARAMS[it % len(PARAMS):] + PARAMS[:it % len(PARAMS)]
+        rows, sts = _rows_states(B, plist, True)
+        noise = torch.ones(B, 101, V, dtype=BF16)
+        for b in range(B):
+            noise[b, 100] = reference_noise(7919 * it + b, 1, V)[0]
+        toks, flags = _run(eng, B, lg, rows, sts, noise.cuda(), 101)
+        for b in range(B):
+            hs = _lib.SamplerState()
+            ht = C.c_int32()
+            lh = lg[b].contiguous()
+            nh = noise[b, 100].contiguous()
+            _lib.check(eng.L.t5g_host_sample(C.c_void_p(lh.data_ptr()), V, C.byref(rows[b]), tk, tk,
+                                             C.byref(sts[b]), C.c_void_p(nh.data_ptr()), EOS, 10, 250.0, 0, 2000.0,
+                                             128, C.byref(hs), C.byref(ht)), "host")
+            if flags[b] & 1:
+                amb += 1
+                continue
+            checked += 1
+            assert toks[b] == ht.value, (mode, it, b, rows[b].top_k, rows[b].top_p, rows[b].temperature)
+    print(f"{mode}: {checked} rows exact, {amb} ambiguous (host-resolved)")
+    assert checked >= 16
+
+
+def test_fast_path_equals_single_block_kernel_philox():
+    B = 8
+    eng_fast = _engine(B)
+    os.environ["T5G_SAMPLER_FAST"] = "0"
+    try:
+        eng_slow = _engine(B)
+    finally:
+        del os.environ["T5G_SAMPLER_FAST"]
+    g = torch.Generator().manual_seed(11)
+    diff = total = 0
+    for it in range(8):
+        lg = _logits(g, B, ["normal", "peaky", "quant", "flat"][it % 4])
+        rows, sts = _rows_states(B, PARAMS[:B], False)
+        a, fa = _run(eng_fast, B, lg, rows, sts)
+        rows, sts = _rows_states(B, PARAMS[:B], False)
+        b, fb = _run(eng_slow, B, lg, rows, sts)
+        for i in range(B):
+            total += 1
+            diff += a[i] != b[i]
+    print(f"fast vs single-block: {total - diff}/{total} equal")
+    assert diff == 0
