@@ -189,7 +189,7 @@ def main():
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(achieved / 8000.0, 4), "traffic": traffic,
-                "kernel": "gemm_p16_kernel<1,2,2,GEGLU> (decode gate/up, M=8, 84.9 MB weights)",
+                "kernel": "gemm_p16_kernel<1,2,2,GEGLU,XLDS> (decode gate/up, M=8, 84.9 MB weights)",
                 "avg_us": round(us.value, 2)}
         step_us = C.c_float()
         _lib.check(L.t5g_time_decode_step(eng.h, 20, st, C.byref(step_us)), "time_step")

@@ -27,20 +27,21 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
     if (idx >= nh * H2) return;
     const int h = idx / H2, i = idx % H2;
     const int row = a.tok_row ? a.tok_row[m] : m;
+    const bool isq = h < a.nq, isk = !isq && h < a.nq + a.nk;
+    const int slot = isq ? 0 : (a.tok_t ? a.tok_t[m] : a.kv_len[row] - 1);   // issued first
     float x1, x2;
     if (a.Xpart) {
         float p1[8], p2[8];
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
-            if (s < a.nsplit) {
-                const float* ps = a.Xpart + ((long)s * a.M + m) * a.ldx + a.col0 + h * D;
-                p1[s] = ps[i];
-                p2[s] = ps[i + H2];
-            }
-        x1 = 0.f;
-        x2 = 0.f;
+        for (int s = 0; s < 8; ++s) {   // clamped, unconditional (see attn_decode_kernel)
+            const float* ps = a.Xpart + ((long)min(s, a.nsplit - 1) * a.M + m) * a.ldx + a.col0 + h * D;
+            p1[s] = ps[i];
+            p2[s] = ps[i + H2];
+        }
+        x1 = p1[0];
+        x2 = p2[0];
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
+        for (int s = 1; s < 8; ++s)
             if (s < a.nsplit) {
                 x1 += p1[s];
                 x2 += p2[s];
@@ -52,7 +53,6 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
         x1 = bf2f(xh[i]);
         x2 = bf2f(xh[i + H2]);
     }
-    const bool isq = h < a.nq, isk = !isq && h < a.nq + a.nk;
     float o1 = x1, o2 = x2;
     if ((isq && a.rope_q) || (isk && a.rope_k)) {
         float c, sn;
@@ -71,7 +71,6 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
     if (isq) {
         dst = a.Qout + (long)m * a.ldq + h * D;
     } else {
-        const int slot = a.tok_t ? a.tok_t[m] : a.kv_len[row] - 1;
         dst = (isk ? a.Kc + (h - a.nq) * a.c_hstride : a.Vc + (h - a.nq - a.nk) * a.c_hstride) +
               row * a.c_bstride + (long)slot * D;
     }
@@ -98,7 +97,7 @@ int rope_store(const RopeArgs& a, hipStream_t st) {
     if (a.M <= 0) return 0;
     if (a.nq && a.Qout == a.X && a.ldq != a.ldx) return -1;
     if (!a.X && !a.Xpart) return -1;
-    if (a.Xpart && a.nsplit > 8) return -1;
+    if (a.Xpart && (a.nsplit < 1 || a.nsplit > 8)) return -1;
     const int pairs = (a.nq + a.nk + a.nv) * (a.D / 2);
     // in-place q rope is safe: each (h, i) pair is read and written by one thread
     hipLaunchKernelGGL(rope_store_kernel, dim3((unsigned)a.M, (unsigned)((pairs + 255) / 256)), dim3(256), 0, st, a);
@@ -324,6 +323,8 @@ __device__ __forceinline__ void merge_splits(const AttnArgs& a, const float* bas
     *(uint2*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 4 * d4) = o;
 }
 
+constexpr int QSMAX = 4;   // q / appended-k/v projection slabs read by the decode kernel
+
 template <int D, int G>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     constexpr int CH = 64;
@@ -338,11 +339,29 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     __shared__ float Linv[G];
     __shared__ int last_flag;
     __shared__ float qs[G][D];
+    __shared__ float kvnew[2][D];   // appended key (pre-RoPE) / value of position t
 
     const int qi = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int kg = lane / LPK, dl = lane % LPK;
     const int row = a.q_row ? a.q_row[qi] : qi;
+    // row length / query position first: the oldest outstanding load is the first one a
+    // wave can wait for, so these must not queue behind the K/V stream
+    const int len = a.kv_len[row];
+    const int t = a.q_pos ? a.q_pos[qi] : len - 1;
+    int lo = 0, hi = len;
+    if (a.causal) {
+        hi = min(t + 1, len);
+        if (a.window > 0) lo = max(0, t - a.window + 1);
+    } else if (a.window > 0) {
+        lo = max(0, t - a.window);
+        hi = min(len, t + a.window + 1);
+    }
+    const int c0 = lo + sp * CH;
+    const int c1 = min(hi, c0 + CH);
+    const int n = c1 - c0;
+    // the block whose keys include t appends the step's own key/value (a.append)
+    const bool has_t = a.append && a.Qpart && t >= c0 && t < c1;
     const bf16_t* Kb = a.K + row * a.kv_bstride + kvh * a.kv_hstride;
     const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
     // Without a sliding window the block's keys start at sp*CH whatever the row
@@ -352,11 +371,9 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     if (spec) {
 #pragma unroll
         for (int i = 0; i < NIT; ++i) {
-            const int j = sp * CH + i * KPB + wave * KPW + kg;
-            if (j < a.kv_cap) {
-                kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
-                vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
-            }
+            const int j = min(sp * CH + i * KPB + wave * KPW + kg, a.kv_cap - 1);
+            kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
+            vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
         }
     }
     // q (+ PM-RoPE) does not depend on the row length either: load it now too.
@@ -367,17 +384,36 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     if (a.Qpart) {
         for (int idx = threadIdx.x; idx < G * D / 4; idx += 256) {
             const int g = idx / (D / 4), c4 = idx % (D / 4);
-            f32x4 u[8];
+            // unconditional loads (clamped slab index): a predicated load per slab turns
+            // into a branch whose join waits for every load in flight, K/V included
+            f32x4 u[QSMAX];
 #pragma unroll
-            for (int s = 0; s < 8; ++s)
-                if (s < a.q_nsplit)
-                    u[s] = *(const f32x4*)(a.Qpart + ((long)s * a.Mq + qi) * a.ldqp + (kvh * G + g) * D + 4 * c4);
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int s = 0; s < QSMAX; ++s)
+                u[s] = *(const f32x4*)(a.Qpart + ((long)min(s, a.q_nsplit - 1) * a.Mq + qi) * a.ldqp +
+                                       (kvh * G + g) * D + 4 * c4);
+            f32x4 acc = u[0];
 #pragma unroll
-            for (int s = 0; s < 8; ++s)
+            for (int s = 1; s < QSMAX; ++s)
                 if (s < a.q_nsplit) acc += u[s];
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) qs[g][4 * c4 + jj] = rbf(acc[jj]);
+        }
+        if (has_t) {
+            const int idx = (int)threadIdx.x - G * D / 4;   // threads past the q quads
+            if (idx >= 0 && idx < 2 * (D / 4)) {
+                const int which = idx / (D / 4), c4 = idx % (D / 4);
+                const int col = (which ? a.v_col0 : a.k_col0) + kvh * D + 4 * c4;
+                f32x4 u[QSMAX];
+#pragma unroll
+                for (int s = 0; s < QSMAX; ++s)
+                    u[s] = *(const f32x4*)(a.Qpart + ((long)min(s, a.q_nsplit - 1) * a.Mq + qi) * a.ldqp + col);
+                f32x4 acc = u[0];
+#pragma unroll
+                for (int s = 1; s < QSMAX; ++s)
+                    if (s < a.q_nsplit) acc += u[s];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) kvnew[which][4 * c4 + jj] = rbf(acc[jj]);
+            }
         }
         float c8[8], s8[8];
         if (a.rope_tab) {
@@ -420,19 +456,6 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             }
         }
     }
-    const int len = a.kv_len[row];
-    const int t = a.q_pos ? a.q_pos[qi] : len - 1;
-    int lo = 0, hi = len;
-    if (a.causal) {
-        hi = min(t + 1, len);
-        if (a.window > 0) lo = max(0, t - a.window + 1);
-    } else if (a.window > 0) {
-        lo = max(0, t - a.window);
-        hi = min(len, t + a.window + 1);
-    }
-    const int c0 = lo + sp * CH;
-    const int c1 = min(hi, c0 + CH);
-    const int n = c1 - c0;
     const long pstride = (long)G * (D + 2);
     float* pbase = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * pstride;
     float* part = pbase + sp * pstride;
@@ -447,6 +470,31 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             if (j >= c1) {
                 kr[i] = (u32x4){0u, 0u, 0u, 0u};
                 vr[i] = (u32x4){0u, 0u, 0u, 0u};
+            }
+            if (has_t && j == t) {
+                // key t: PM-RoPE of the new key (rope_store_kernel's arithmetic), then append
+                const bool lower = dl < LPK / 2;
+                const float* tr = a.rope_tab + (long)row * D;
+                u32x4 kw, vw;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    float ko[2], vo[2];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int dd = 8 * dl + 2 * jj + e;
+                        const int fi = dd % (D / 2);
+                        const float c = tr[fi], sn = tr[D / 2 + fi];
+                        const float x = kvnew[0][dd], pr = kvnew[0][(dd + D / 2) % D];
+                        ko[e] = lower ? rbf(rbf(x * c) + rbf(-pr * sn)) : rbf(rbf(x * c) + rbf(pr * sn));
+                        vo[e] = kvnew[1][dd];
+                    }
+                    kw[jj] = pack2(ko[0], ko[1]);
+                    vw[jj] = pack2(vo[0], vo[1]);
+                }
+                kr[i] = kw;
+                vr[i] = vw;
+                *(u32x4*)(const_cast<bf16_t*>(Kb) + (long)t * D + 8 * dl) = kw;
+                *(u32x4*)(const_cast<bf16_t*>(Vb) + (long)t * D + 8 * dl) = vw;
             }
         }
 #pragma unroll
@@ -588,6 +636,8 @@ static int launch_decode(const AttnArgs& a, hipStream_t st) {
 int attention_decode(const AttnArgs& a, hipStream_t st) {
     if (a.Mq <= 0) return 0;
     if (a.nsplit < 1 || a.nsplit > 64 || !a.part || a.eager) return -1;
+    if (a.append && (!a.Qpart || !a.rope_tab || (a.G + 2) * a.D / 4 > 256)) return -1;
+    if (a.Qpart && (a.q_nsplit < 1 || a.q_nsplit > QSMAX)) return -1;
     if (a.D == 256 && a.G == 2) return launch_decode<256, 2>(a, st);
     if (a.D == 64 && a.G == 2) return launch_decode<64, 2>(a, st);
     if (a.D == 128 && a.G == 2) return launch_decode<128, 2>(a, st);

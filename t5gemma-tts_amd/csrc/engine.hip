@@ -432,7 +432,9 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         r.Vc = e->sv[l];
         r.c_hstride = (long)c.max_audio * D;
         r.c_bstride = r.c_hstride * c.n_kv_heads;
-        RC(rope_store(r, st));
+        // sdpa decode: the attention kernel appends k/v itself (AttnArgs::append)
+        const bool fused_append = decode && !(c.softcap > 0.f) && s_qkv > 1;
+        if (!fused_append) RC(rope_store(r, st));
         {
             AttnArgs a;
             memset(&a, 0, sizeof(a));
@@ -469,6 +471,9 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
                     a.pos = pos;
                     a.inv_freq = e->w.inv_freq;
                     a.rope_tab = tab;
+                    a.append = fused_append ? 1 : 0;
+                    a.k_col0 = e->q_dim;
+                    a.v_col0 = e->q_dim + e->kv_dim;
                 } else {
                     return T5G_EINVAL;
                 }

@@ -40,15 +40,29 @@ __global__ void pack_p16_kernel(const bf16_t* __restrict__ src, int N, int K, lo
 template <int MT>
 __device__ __forceinline__ void load_x(const bf16_t* __restrict__ X, int ldx, int M, int m0, int kb,
                                        int lane, bf16x8_s (&xf)[MT]) {
+    // unconditional (clamped row) loads + select: a load under a branch makes the
+    // compiler wait for every load in flight at the join
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-        int m = m0 + mt * 16 + (lane & 15);
-        if (m < M) {
-            xf[mt] = *(const bf16x8_s*)(X + (long)m * ldx + kb * 32 + 8 * (lane >> 4));
-        } else {
-            xf[mt] = (bf16x8_s){0, 0, 0, 0, 0, 0, 0, 0};
-        }
+        const int m = m0 + mt * 16 + (lane & 15);
+        const bf16x8_s v = *(const bf16x8_s*)(X + (long)min(m, M - 1) * ldx + kb * 32 + 8 * (lane >> 4));
+        xf[mt] = m < M ? v : (bf16x8_s){0, 0, 0, 0, 0, 0, 0, 0};
     }
+}
+
+// Buffer descriptor over one row group's fragment stream: loads past `bytes` return 0
+// and move no data (hardware range check), so the weight stream needs no predication.
+// Inputs are made provably wave-uniform (readfirstlane) so no waterfall loop appears.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frag_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t p = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ bf16x8_s frag_load(__amdgpu_buffer_rsrc_t r, int kb, int lane) {
+    // aux 2 = nt: streamed once (decode weights)
+    return __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(r, (kb * 64 + lane) * 16, 0, 2));
 }
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
@@ -62,12 +76,13 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
 // whether a slice runs on its own wave (WPG == KS, decode) or all slices of a row
 // group run on one wave (WPG == 1, prefill) -- a row's logits do not depend on
 // which other rows share the batch.
-template <int MT, int WPG, int KS, int EPI>
+template <int MT, int WPG, int KS, int EPI, bool XLDS>
 __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
     static_assert(WPG == KS || WPG == 1, "slice mapping");
     constexpr int RG = 4 / WPG;  // row groups per block
     constexpr int SPW = KS / WPG;  // slices per wave
     constexpr int UN = (WPG == 1) ? KS : 8;  // k-steps in flight per wave per iteration
+    constexpr int XCH = 18;  // X-staging chunks per thread (XLDS: rows * K_slice / 8 <= 256 * XCH)
     __shared__ f32x4 red[4][MT][64];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -85,27 +100,89 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
         for (int mt = 0; mt < MT; ++mt) acc[s][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     const bf16x8_s* wp = (const bf16x8_s*)a.W + ((long)g * a.KB) * 64 + lane;
-    if constexpr (WPG == KS) {
-        // one slice per wave: kb = kb_lo + ks, +KS, ...
+    if (kb_hi <= kb_lo) {
+        // empty K slice (splits not dividing K): contributes zeros
+    } else if constexpr (WPG == KS && MT == 1 && XLDS) {
+        // Decode (M <= 16): the block's X rows for its K range are staged once in LDS, so
+        // the vector-memory path carries only the weight stream (one 1 KiB fragment per
+        // MFMA). Weight fragments are register double-buffered: group g+1 (UN steps) is in
+        // flight while group g is multiplied; the first group is issued before the X
+        // staging barrier.
+        extern __shared__ bf16_t xs[];
+        const int rows = min(16, a.M - m0);
+        const int kspan = kb_hi - kb_lo;
+        const int ldsx = kspan * 32 + 8;   // +16 B row pad spreads the 16 row reads over banks
+        constexpr int STEP = UN * KS;
         int kb = kb_lo + ks;
-        for (; kb + (UN - 1) * KS < kb_hi; kb += UN * KS) {
-            bf16x8_s wf[UN];
-            bf16x8_s xf[UN][MT];
+        // fragments kb >= kb_hi fall outside the descriptor: zero, no traffic
+        const __amdgpu_buffer_rsrc_t wr = frag_rsrc(a.W + (long)g * a.KB * 512, (uint32_t)kb_hi * 1024u);
+        bf16x8_s wcur[UN];
 #pragma unroll
-            for (int u = 0; u < UN; ++u) wf[u] = __builtin_nontemporal_load(wp + (long)(kb + u * KS) * 64);
+        for (int u = 0; u < UN; ++u) wcur[u] = frag_load(wr, kb + u * KS, lane);
+        {
+            // all X chunks of the thread are requested at once (buffer loads: slots past
+            // the block's rows fall outside the descriptor -> 0, no traffic), then written
+            const int total = rows * kspan * 4;
+            const __amdgpu_buffer_rsrc_t xrs = frag_rsrc(a.X + (long)m0 * a.ldx, (uint32_t)rows * a.ldx * 2u);
+            bf16x8_s xv[XCH];
 #pragma unroll
-            for (int u = 0; u < UN; ++u) load_x<MT>(a.X, a.ldx, a.M, m0, kb + u * KS, lane, xf[u]);
+            for (int i = 0; i < XCH; ++i) {
+                const int idx = threadIdx.x + 256 * i;
+                const int r = idx / (kspan * 4), c = idx - r * (kspan * 4);
+                const int off = idx < total ? (r * a.ldx + kb_lo * 32 + 8 * c) * 2 : 0x7ffffff0;
+                xv[i] = __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+            }
+#pragma unroll
+            for (int i = 0; i < XCH; ++i) {
+                const int idx = threadIdx.x + 256 * i;
+                const int r = idx / (kspan * 4), c = idx - r * (kspan * 4);
+                if (idx < total) *(bf16x8_s*)(xs + r * ldsx + 8 * c) = xv[i];
+            }
+        }
+        __syncthreads();
+        const int xr = lane & 15;
+        const bf16_t* xrow = xs + min(xr, rows - 1) * ldsx + 8 * (lane >> 4) - kb_lo * 32;
+        for (; kb < kb_hi; kb += STEP) {
+            bf16x8_s wnext[UN];
+            const int kn = kb + STEP;
+#pragma unroll
+            for (int u = 0; u < UN; ++u) wnext[u] = frag_load(wr, kn + u * KS, lane);
 #pragma unroll
             for (int u = 0; u < UN; ++u)
+                if (kb + u * KS < kb_hi) {   // uniform: the same for every lane of the wave
+                    const bf16x8_s xv = *(const bf16x8_s*)(xrow + (kb + u * KS) * 32);
+                    const bf16x8_s xf = xr < rows ? xv : (bf16x8_s){0, 0, 0, 0, 0, 0, 0, 0};
+                    acc[0][0] = mfma16(wcur[u], xf, acc[0][0]);
+                }
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) acc[0][mt] = mfma16(wf[u], xf[u][mt], acc[0][mt]);
+            for (int u = 0; u < UN; ++u) wcur[u] = wnext[u];
         }
-        for (; kb < kb_hi; kb += KS) {
-            bf16x8_s wf = __builtin_nontemporal_load(wp + (long)kb * 64);
-            bf16x8_s xf[MT];
-            load_x<MT>(a.X, a.ldx, a.M, m0, kb, lane, xf);
+    } else if constexpr (WPG == KS) {
+        // one slice per wave: kb = kb_lo + ks, +KS, ...; every group of UD k-steps is
+        // issued at once (predicated), so a short slice costs a single memory round trip
+        constexpr int UD = (MT == 1) ? 16 : 8;
+        for (int kb = kb_lo + ks; kb < kb_hi; kb += UD * KS) {
+            bf16x8_s wf[UD];
+            bf16x8_s xf[UD][MT];
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[0][mt] = mfma16(wf, xf[mt], acc[0][mt]);
+            for (int u = 0; u < UD; ++u) {
+                // predicated: a short slice issues only its own fragments (all loads are
+                // waited for together before the MFMAs anyway)
+                const bool ok = kb + u * KS < kb_hi;
+                wf[u] = ok ? __builtin_nontemporal_load(wp + (long)(kb + u * KS) * 64)
+                           : (bf16x8_s){0, 0, 0, 0, 0, 0, 0, 0};
+                if (ok) {
+                    load_x<MT>(a.X, a.ldx, a.M, m0, kb + u * KS, lane, xf[u]);
+                } else {
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) xf[u][mt] = (bf16x8_s){0, 0, 0, 0, 0, 0, 0, 0};
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UD; ++u)
+                if (kb + u * KS < kb_hi)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) acc[0][mt] = mfma16(wf[u], xf[u][mt], acc[0][mt]);
         }
     } else {
         // all KS slices on this wave: step u of a group of KS k-steps is slice u
@@ -214,7 +291,15 @@ template <int MT, int WPG, int KS, int EPI>
 static void launch_t(const GemmArgs& a, int mblocks, hipStream_t st) {
     constexpr int RG = 4 / WPG;
     dim3 grid((unsigned)(a.NG / RG), (unsigned)a.splits, (unsigned)mblocks);
-    hipLaunchKernelGGL((gemm_p16_kernel<MT, WPG, KS, EPI>), grid, dim3(256), 0, st, a);
+    const int per = (a.KB + a.splits - 1) / a.splits;
+    // decode with a long K stream per wave: stage the X rows in LDS once per block (the
+    // staging barrier costs ~1 us, repaid only when each wave streams >= 16 fragments)
+    if (WPG == KS && MT == 1 && per / KS >= 16 && min(16, a.M) * per * 4 <= 256 * 18) {
+        const size_t shm = (size_t)min(16, a.M) * (per * 32 + 8) * sizeof(bf16_t);
+        hipLaunchKernelGGL((gemm_p16_kernel<MT, WPG, KS, EPI, true>), grid, dim3(256), shm, st, a);
+    } else {
+        hipLaunchKernelGGL((gemm_p16_kernel<MT, WPG, KS, EPI, false>), grid, dim3(256), 0, st, a);
+    }
 }
 
 // decode (WPG = KS) and prefill (WPG = 1) instantiate the same slice order

@@ -95,6 +95,9 @@ struct AttnArgs {
     int* counters;           // [Mq][Hkv] arrival tickets: the last split block merges (zeroed)
     const float* rope_tab;   // optional per-row cos/sin table (see rope_table)
     int kv_cap;              // allocated keys per (row, head): speculative loads stay below it
+    // decode self-attention: the block holding key t = kv_len-1 builds it from the
+    // projection slabs (k rotated by PM-RoPE, v as is), uses it and appends it to K/V
+    int append, k_col0, v_col0;
 };
 int attention(const AttnArgs& a, hipStream_t st);
 // decode-shaped (64-key blocks, split over blockIdx.z, sdpa numerics); nsplit = ceil(keys/64)

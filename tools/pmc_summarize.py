@@ -7,7 +7,7 @@ import json
 import os
 import sys
 
-KERNEL = "gemm_p16_kernel<1, 2, 2, 3>"
+KERNEL = "gemm_p16_kernel<1, 2, 2, 3, true>"
 
 
 def mean_counter(path):
