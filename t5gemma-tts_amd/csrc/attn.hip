@@ -364,67 +364,74 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     const bool has_t = a.append && a.Qpart && t >= c0 && t < c1;
     const bf16_t* Kb = a.K + row * a.kv_bstride + kvh * a.kv_hstride;
     const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
-    // Without a sliding window the block's keys start at sp*CH whatever the row
-    // length: request K/V before kv_len arrives (one memory round trip per block).
-    const bool spec = a.window == 0;
-    u32x4 kr[NIT], vr[NIT];
-    if (spec) {
+    // Issue order = wait order (vmcnt is in-order): first what the q path needs (the
+    // projection's split-K slabs, the PM-RoPE table), then the K/V stream, so q can be
+    // summed, staged and rotated while K/V are still in flight. All loads are
+    // unconditional (clamped addresses): a load under a branch makes the compiler
+    // wait for everything in flight at the join.
+    // Thread roles in the slab stage: quads [0, G*D/4) are q, the next 2*D/4 the
+    // appended k and v (block holding key t only); the rest re-read quad 0.
+    f32x4 u[QSMAX];
+    int role = -1, c4 = 0, g_own = 0;
+    if (a.Qpart) {
+        const int tq = (int)threadIdx.x;
+        int col = kvh * G * D;   // idle threads: quad 0 of q
+        if (tq < G * D / 4) {
+            role = 0;
+            g_own = tq / (D / 4);
+            c4 = tq % (D / 4);
+            col = (kvh * G + g_own) * D + 4 * c4;
+        } else if (has_t && tq < (G + 2) * D / 4) {
+            const int idx = tq - G * D / 4;
+            role = 1 + idx / (D / 4);   // 1: key, 2: value
+            c4 = idx % (D / 4);
+            col = (role == 1 ? a.k_col0 : a.v_col0) + kvh * D + 4 * c4;
+        }
 #pragma unroll
-        for (int i = 0; i < NIT; ++i) {
-            const int j = min(sp * CH + i * KPB + wave * KPW + kg, a.kv_cap - 1);
-            kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
-            vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
+        for (int s = 0; s < QSMAX; ++s)
+            u[s] = *(const f32x4*)(a.Qpart + ((long)min(s, a.q_nsplit - 1) * a.Mq + qi) * a.ldqp + col);
+    }
+    // this lane's 8 cos / 8 sin of the row's PM-RoPE table (dims 8*dl .. 8*dl+7 never wrap
+    // D/2): four 16-B loads
+    float c8[8], s8[8];
+    if (a.rope_tab) {
+        const float* tr = a.rope_tab + (long)row * D + (8 * dl) % (D / 2);
+        const f32x4 ca = *(const f32x4*)tr, cb = *(const f32x4*)(tr + 4);
+        const f32x4 sa = *(const f32x4*)(tr + D / 2), sb = *(const f32x4*)(tr + D / 2 + 4);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            c8[jj] = ca[jj];
+            c8[4 + jj] = cb[jj];
+            s8[jj] = sa[jj];
+            s8[4 + jj] = sb[jj];
         }
     }
-    // q (+ PM-RoPE) does not depend on the row length either: load it now too.
-    // Split-K slabs are summed once per block into LDS (one f32x4 per slab per thread,
-    // issued alongside the K/V loads), then every lane rotates its 8 q values reading the
-    // rotate_half partner from LDS -- no shuffles, no slab fan-out per lane.
+    // Unless a sliding window has moved the first key (lo > 0) the block's keys start at
+    // sp*CH whatever the row length: request K/V now (one memory round trip per block).
+    // Always issued (a guarded batch would make the compiler merge wait counts at the
+    // join); the rare lo > 0 block re-reads its keys below.
+    const bool spec = lo == 0;
+    u32x4 kr[NIT], vr[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        const int j = min(sp * CH + i * KPB + wave * KPW + kg, a.kv_cap - 1);
+        kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
+        vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
+    }
     float q[G][8];
     if (a.Qpart) {
-        for (int idx = threadIdx.x; idx < G * D / 4; idx += 256) {
-            const int g = idx / (D / 4), c4 = idx % (D / 4);
-            // unconditional loads (clamped slab index): a predicated load per slab turns
-            // into a branch whose join waits for every load in flight, K/V included
-            f32x4 u[QSMAX];
+        f32x4 acc = u[0];
 #pragma unroll
-            for (int s = 0; s < QSMAX; ++s)
-                u[s] = *(const f32x4*)(a.Qpart + ((long)min(s, a.q_nsplit - 1) * a.Mq + qi) * a.ldqp +
-                                       (kvh * G + g) * D + 4 * c4);
-            f32x4 acc = u[0];
+        for (int s = 1; s < QSMAX; ++s)
+            if (s < a.q_nsplit) acc += u[s];
+        if (role == 0) {
 #pragma unroll
-            for (int s = 1; s < QSMAX; ++s)
-                if (s < a.q_nsplit) acc += u[s];
+            for (int jj = 0; jj < 4; ++jj) qs[g_own][4 * c4 + jj] = rbf(acc[jj]);
+        } else if (role > 0) {
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) qs[g][4 * c4 + jj] = rbf(acc[jj]);
+            for (int jj = 0; jj < 4; ++jj) kvnew[role - 1][4 * c4 + jj] = rbf(acc[jj]);
         }
-        if (has_t) {
-            const int idx = (int)threadIdx.x - G * D / 4;   // threads past the q quads
-            if (idx >= 0 && idx < 2 * (D / 4)) {
-                const int which = idx / (D / 4), c4 = idx % (D / 4);
-                const int col = (which ? a.v_col0 : a.k_col0) + kvh * D + 4 * c4;
-                f32x4 u[QSMAX];
-#pragma unroll
-                for (int s = 0; s < QSMAX; ++s)
-                    u[s] = *(const f32x4*)(a.Qpart + ((long)min(s, a.q_nsplit - 1) * a.Mq + qi) * a.ldqp + col);
-                f32x4 acc = u[0];
-#pragma unroll
-                for (int s = 1; s < QSMAX; ++s)
-                    if (s < a.q_nsplit) acc += u[s];
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) kvnew[which][4 * c4 + jj] = rbf(acc[jj]);
-            }
-        }
-        float c8[8], s8[8];
-        if (a.rope_tab) {
-            const float* tr = a.rope_tab + (long)row * D;
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-                const int fi = (8 * dl + jj) % (D / 2);
-                c8[jj] = tr[fi];
-                s8[jj] = tr[D / 2 + fi];
-            }
-        } else {
+        if (!a.rope_tab) {
             const float ps = a.pos[row];
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
@@ -434,16 +441,16 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             }
         }
         __syncthreads();
-        const bool lower = dl < LPK / 2;
+        // lower half: x*c + (-x2)*s ; upper half: x*c + x1*s (one branch-free formula)
+        const float sg = dl < LPK / 2 ? -1.0f : 1.0f;
+        const int pbase = (8 * dl + D / 2) % D;
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
-                const int dd = 8 * dl + jj;
-                const float x = qs[g][dd];
-                const float pr = qs[g][(dd + D / 2) % D];
-                // lower half: x*c + (-x2)*s ; upper half: x*c + x1*s
-                q[g][jj] = lower ? rbf(rbf(x * c8[jj]) + rbf(-pr * s8[jj])) : rbf(rbf(x * c8[jj]) + rbf(pr * s8[jj]));
+                const float x = qs[g][8 * dl + jj];
+                const float pr = qs[g][pbase + jj];
+                q[g][jj] = rbf(rbf(x * c8[jj]) + rbf((sg * pr) * s8[jj]));
             }
     } else {
 #pragma unroll
@@ -473,8 +480,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             }
             if (has_t && j == t) {
                 // key t: PM-RoPE of the new key (rope_store_kernel's arithmetic), then append
-                const bool lower = dl < LPK / 2;
-                const float* tr = a.rope_tab + (long)row * D;
+                const float sg = dl < LPK / 2 ? -1.0f : 1.0f;
+                const int pbase = (8 * dl + D / 2) % D;
                 u32x4 kw, vw;
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
@@ -482,10 +489,9 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
                         const int dd = 8 * dl + 2 * jj + e;
-                        const int fi = dd % (D / 2);
-                        const float c = tr[fi], sn = tr[D / 2 + fi];
-                        const float x = kvnew[0][dd], pr = kvnew[0][(dd + D / 2) % D];
-                        ko[e] = lower ? rbf(rbf(x * c) + rbf(-pr * sn)) : rbf(rbf(x * c) + rbf(pr * sn));
+                        const float c = c8[2 * jj + e], sn = s8[2 * jj + e];
+                        const float x = kvnew[0][dd], pr = kvnew[0][pbase + 2 * jj + e];
+                        ko[e] = rbf(rbf(x * c) + rbf((sg * pr) * sn));
                         vo[e] = kvnew[1][dd];
                     }
                     kw[jj] = pack2(ko[0], ko[1]);

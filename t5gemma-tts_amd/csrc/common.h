@@ -19,12 +19,13 @@ __device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float(h << 
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// RNE fp32 -> bf16 (NaN preserved as quiet NaN)
+// RNE fp32 -> bf16 (NaN preserved as quiet NaN). Branch-free: both results are
+// computed and selected (v_cndmask), so unrolled callers stay straight-line code.
 __device__ __forceinline__ bf16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (bf16_t)(u >> 16);
+    const uint32_t u = __float_as_uint(f);
+    const uint32_t rne = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+    const uint32_t qnan = (u >> 16) | 0x40u;
+    return (bf16_t)(((u & 0x7fffffffu) > 0x7f800000u) ? qnan : rne);
 }
 // round an fp32 value to the nearest bf16 value, returned as fp32
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
