@@ -46,14 +46,17 @@ class Config(C.Structure):
 class LayerWeights(C.Structure):
     _fields_ = [("qkv", C.c_void_p), ("o", C.c_void_p), ("gate_up", C.c_void_p), ("down", C.c_void_p),
                 ("cross_q", C.c_void_p), ("cross_kv", C.c_void_p), ("cross_o", C.c_void_p),
-                ("norms", C.c_void_p * 6)]
+                ("norms", C.c_void_p * 6), ("rm_qkv", C.c_void_p), ("rm_o", C.c_void_p),
+                ("rm_gate_up", C.c_void_p), ("rm_down", C.c_void_p), ("rm_cross_q", C.c_void_p),
+                ("rm_cross_o", C.c_void_p)]
 
 
 class Weights(C.Structure):
     _fields_ = [("enc_embed", C.c_void_p), ("audio_embed", C.c_void_p), ("enc_final_norm", C.c_void_p),
                 ("dec_final_norm", C.c_void_p), ("head1", C.c_void_p), ("head1_bias", C.c_void_p),
                 ("head2", C.c_void_p), ("head2_bias", C.c_void_p), ("inv_freq", C.c_void_p),
-                ("enc_layers", C.POINTER(LayerWeights)), ("dec_layers", C.POINTER(LayerWeights))]
+                ("enc_layers", C.POINTER(LayerWeights)), ("dec_layers", C.POINTER(LayerWeights)),
+                ("rm_head1", C.c_void_p)]
 
 
 class SamplerRow(C.Structure):
@@ -68,6 +71,16 @@ class SamplerState(C.Structure):
                 ("target_total", C.c_int32), ("est_total", C.c_int32), ("prev_token", C.c_int32),
                 ("consec_silence", C.c_int32), ("first_input_len", C.c_int32), ("done", C.c_int32),
                 ("ambiguous_steps", C.c_int32), ("last_token", C.c_int32), ("next_pos", C.c_float)]
+
+
+class GemvArgs(C.Structure):
+    _fields_ = [("M", C.c_int32), ("K", C.c_int32), ("N", C.c_int32), ("epi", C.c_int32), ("pro", C.c_int32),
+                ("nw", C.c_int32), ("W", C.c_void_p), ("bias", C.c_void_p), ("Y", C.c_void_p),
+                ("ldy", C.c_int32), ("ldx", C.c_int32), ("X", C.c_void_p), ("v", C.c_void_p),
+                ("h_in", C.c_void_p), ("ids", C.c_void_p), ("table", C.c_void_p), ("scale", C.c_float),
+                ("eps", C.c_float), ("post_w", C.c_void_p), ("pre_w", C.c_void_p), ("h_out", C.c_void_p),
+                ("x_out", C.c_void_p), ("un", C.c_int32), ("max_grid", C.c_int32),
+                ("splits", C.c_int32), ("layout", C.c_int32)]
 
 
 # name -> (restype, argtypes); exactly the functions include/t5gtts.h declares
@@ -96,6 +109,8 @@ SIGNATURES = {
     "t5g_gemm": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _I, _I, _P]),
     "t5g_time_gemm": (C.c_int, [_P, _I, _I, C.POINTER(_P), _I, _I, _I, _I, _P, _I, _I, _I, _P, C.POINTER(_F)]),
     "t5g_time_decode_step": (C.c_int, [_P, _I, _P, C.POINTER(_F)]),
+    "t5g_gemv": (C.c_int, [C.POINTER(GemvArgs), _P]),
+    "t5g_time_gemv": (C.c_int, [C.POINTER(GemvArgs), C.POINTER(_P), _I, _I, _P, C.POINTER(_F)]),
 }
 
 _lib = None

@@ -19,25 +19,44 @@ __device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float(h << 
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// RNE fp32 -> bf16 (NaN preserved as quiet NaN). Branch-free: both results are
-// computed and selected (v_cndmask), so unrolled callers stay straight-line code.
-__device__ __forceinline__ bf16_t f2bf(float f) {
-    const uint32_t u = __float_as_uint(f);
-    const uint32_t rne = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
-    const uint32_t qnan = (u >> 16) | 0x40u;
-    return (bf16_t)(((u & 0x7fffffffu) > 0x7f800000u) ? qnan : rne);
-}
+// RNE fp32 -> bf16: gfx950's v_cvt_pk_bf16_f32 (round-to-nearest-even, NaN stays
+// NaN), one instruction for two values -- the reference's CPU bf16 casts round the
+// same way (torch c10::BFloat16 round_to_nearest_even).
+typedef __bf16 bf16x2_b __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 // round an fp32 value to the nearest bf16 value, returned as fp32
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-    return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    const bf16x2_b v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+// two values rounded to bf16 (one conversion), back as fp32
+__device__ __forceinline__ f32x2 rbf2(f32x2 x) {
+    const uint32_t w = pack2(x[0], x[1]);
+    return (f32x2){__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
 }
 
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+// wave64 sum on the DPP network (4 in-row steps, no LDS) + 2 cross-row shuffles; fixed
+// order, every lane ends with the total
+__device__ __forceinline__ float row16_sum(float v) {
+    v += __builtin_amdgcn_update_dpp(0.f, v, 0xB1, 0xf, 0xf, false);    // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0.f, v, 0x4E, 0xf, 0xf, false);    // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0.f, v, 0x141, 0xf, 0xf, false);   // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(0.f, v, 0x140, 0xf, 0xf, false);   // row_mirror
+    return v;
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v = row16_sum(v);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
     return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
@@ -78,4 +97,24 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 }
 __device__ __forceinline__ float gelu_erf(float x) {
     return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+
+// Buffer descriptor over one row group's fragment stream: loads past `bytes` return 0
+// and move no data (hardware range check), so the weight stream needs no predication.
+// Inputs are made provably wave-uniform (readfirstlane) so no waterfall loop appears.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frag_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t p = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ bf16x8_s frag_load(__amdgpu_buffer_rsrc_t r, int kb, int lane) {
+    // aux 2 = nt: streamed once (decode weights)
+    return __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(r, (kb * 64 + lane) * 16, 0, 2));
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_b, a),
+                                                   __builtin_bit_cast(bf16x8_b, b), c, 0, 0, 0);
 }

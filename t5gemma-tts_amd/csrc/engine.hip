@@ -51,6 +51,13 @@ struct t5g_engine {
     int* enc_len;                          // [B] text lengths
     // decode (rows = max_batch)
     bf16_t *dh, *dxn, *dq, *datt, *dact, *dhh, *logits;
+    bf16_t *dh2, *dv;     // fused decode: second residual buffer, sub-block output rows
+    // Decode-step GEMV variant, chosen at creation by T5G_FUSED_DECODE (measured on MI355X,
+    // tools/micro_gemv.py): unset/0 = split-K MFMA GEMVs + separate norm
+    // kernels (fastest); 1 = norm prologues fused into row-major VALU GEMVs; 2 = fused
+    // prologues on the P16 MFMA GEMVs.
+    bool fused_decode = false;
+    bool fused_p16 = false;
     int logits_ld;
     // sampler
     SamplerRow* rows;
@@ -179,6 +186,8 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->datt, (int64_t)B * e->q_dim);
     rc |= alloc(e, &e->dact, (int64_t)B * f);
     rc |= alloc(e, &e->dhh, (int64_t)B * d);
+    rc |= alloc(e, &e->dh2, (int64_t)B * d);
+    rc |= alloc(e, &e->dv, (int64_t)B * d);
     e->logits_ld = e->Vpad;
     rc |= alloc(e, &e->logits, (int64_t)B * e->logits_ld);
     rc |= alloc(e, &e->rows, B);
@@ -203,6 +212,9 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     {
         const char* fsv = getenv("T5G_SAMPLER_FAST");
         e->fast_sampler = !(fsv && fsv[0] == '0');
+        const char* fdv = getenv("T5G_FUSED_DECODE");
+        e->fused_decode = fdv && (fdv[0] == '1' || fdv[0] == '2');
+        e->fused_p16 = fdv && fdv[0] == '2';
     }
     if (rc) {
         t5g_engine_destroy(e);
@@ -617,6 +629,210 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
     return T5G_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Fused single-token decoder step (sdpa numerics, M <= 16 rows): 9 launches per layer.
+//   qkv   : [norm prologue: previous down output + residual, post_ff/pre_self] -> fp32 q|k|v
+//   attn  : self attention (PM-RoPE of q/k, k/v append) + split merge
+//   o     : att -> bf16 v
+//   cq    : [norm prologue: post_self/pre_cross] -> fp32 q
+//   cattn : cross attention over the cached encoder K/V
+//   co    : att -> bf16 v
+//   gu    : [norm prologue: post_cross/pre_ff] -> GeGLU -> act
+//   down  : act (direct from L2) -> bf16 v
+// then head1 with the final-norm prologue, head2 (PMDecoderLayer.forward :256-323,
+// decoder final norm [tf] :818, predict_layer :469-478).
+static bool fused_ok(const t5g_engine* e, int M) {
+    const t5g_config& c = e->c;
+    return e->fused_decode && !(c.softcap > 0.f) && M >= 1 && M <= 16 && c.hidden % 32 == 0 &&
+           c.hidden <= 4096 && (c.hidden <= 2560 || M <= 8) && c.intermediate % 32 == 0;
+}
+
+// row-major VALU GEMVs: every decoder projection has its plain copy, batch <= 8 rows
+static bool rm_ok(const t5g_engine* e, int M) {
+    if (!fused_ok(e, M) || e->fused_p16 || M > 8 || e->c.hidden > 2560 || !e->w.rm_head1) return false;
+    for (const t5g_layer_weights& L : e->dec)
+        if (!L.rm_qkv || !L.rm_o || !L.rm_gate_up || !L.rm_down || !L.rm_cross_q || !L.rm_cross_o) return false;
+    return true;
+}
+
+static DecGemmArgs dec_args(int M, const void* W, int N, int K, void* Y, int ldy, int nw) {
+    DecGemmArgs g;
+    memset(&g, 0, sizeof(g));
+    g.M = M;
+    g.K = K;
+    g.W = (const bf16_t*)W;
+    g.N = N;
+    g.NG = ng_pad(N);
+    g.KB = K / 32;
+    g.Y = Y;
+    g.ldy = ldy;
+    g.nw = nw;
+    g.splits = 1;
+    return g;
+}
+
+static int decode_fused(t5g_engine* e, bool rm, hipStream_t st) {
+    const t5g_config& c = e->c;
+    // rm: plain row-major weights on the VALU GEMV (exact rows per CU); else P16 on MFMA
+    auto gv = [&](DecGemmArgs& g, const void* w_rm, int epi, int pro) -> int {
+        if (!rm) return gemv_dec(g, epi, pro, st);
+        g.W = (const bf16_t*)w_rm;
+        return gemv_rm(g, epi, pro, st);
+    };
+    const int M = e->B, d = c.hidden, f = c.intermediate, D = c.head_dim;
+    const int G = c.n_heads / c.n_kv_heads;
+    const int nw_norm = M <= 8 ? 4 : 8;       // prologue rows per wave <= 2
+    const int nw_wide = M <= 8 ? 8 : 8;
+    bf16_t* hb[2] = {e->dh, e->dh2};
+    int hc = 0;
+    RC(rope_table(e->next_pos, e->w.inv_freq, M, D, e->rope_tab, st));
+    auto norm_pro = [&](DecGemmArgs& g, const void* post_w, const void* pre_w, bool keep) {
+        g.v = e->dv;
+        g.h_in = hb[hc];
+        g.post_w = (const bf16_t*)post_w;
+        g.pre_w = (const bf16_t*)pre_w;
+        g.eps = c.rms_eps;
+        g.h_out = keep ? hb[hc ^ 1] : nullptr;
+        hc ^= 1;
+    };
+    for (int l = 0; l < c.n_dec_layers; ++l) {
+        const t5g_layer_weights& L = e->dec[l];
+        // --- self attention
+        {
+            DecGemmArgs g = dec_args(M, L.qkv, e->qkv_dim, d, e->part, e->qkv_dim, nw_wide);
+            int pro;
+            if (l == 0) {
+                pro = PRO_EMBED;
+                g.ids = e->next_token;
+                g.table = (const bf16_t*)e->w.audio_embed;
+                g.scale = c.normalizer;
+                g.pre_w = (const bf16_t*)L.norms[0];
+                g.eps = c.rms_eps;
+                g.h_out = hb[0];
+                hc = 0;
+            } else {
+                pro = PRO_NORM;
+                norm_pro(g, e->dec[l - 1].norms[5], L.norms[0], true);
+            }
+            RC(gv(g, L.rm_qkv, EPI_F32, pro));
+        }
+        {
+            AttnArgs a;
+            memset(&a, 0, sizeof(a));
+            a.Q = e->dq;
+            a.ldq = e->q_dim;
+            a.Mq = M;
+            a.K = e->sk[l];
+            a.V = e->sv[l];
+            a.kv_hstride = (long)c.max_audio * D;
+            a.kv_bstride = a.kv_hstride * c.n_kv_heads;
+            a.kv_len = e->kv_len;
+            a.Hkv = c.n_kv_heads;
+            a.D = D;
+            a.G = G;
+            a.causal = 1;
+            a.window = c.dec_sliding[l] ? c.sliding_window : 0;
+            a.scale = c.attn_scale;
+            a.O = e->datt;
+            a.ldo = e->q_dim;
+            a.chunk = 64;
+            a.nsplit = (c.max_audio + 63) / 64;
+            a.kv_cap = c.max_audio;
+            a.part = e->apart;
+            a.Qpart = e->part;
+            a.q_nsplit = 1;
+            a.ldqp = e->qkv_dim;
+            a.pos = e->next_pos;
+            a.inv_freq = e->w.inv_freq;
+            a.rope_tab = e->rope_tab;
+            a.append = 1;
+            a.k_col0 = e->q_dim;
+            a.v_col0 = e->q_dim + e->kv_dim;
+            RC(attention_decode(a, st));
+        }
+        {
+            DecGemmArgs g = dec_args(M, L.o, d, e->q_dim, e->dv, d, nw_wide);
+            g.X = e->datt;
+            g.ldx = e->q_dim;
+            RC(gv(g, L.rm_o, EPI_BF16, rm ? PRO_DIRECT : PRO_LOAD));
+        }
+        // --- PM cross attention
+        {
+            DecGemmArgs g = dec_args(M, L.cross_q, e->q_dim, d, e->part, e->q_dim, nw_wide);
+            norm_pro(g, L.norms[1], L.norms[2], true);
+            RC(gv(g, L.rm_cross_q, EPI_F32, PRO_NORM));
+        }
+        {
+            AttnArgs a;
+            memset(&a, 0, sizeof(a));
+            a.Q = e->dq;
+            a.ldq = e->q_dim;
+            a.Mq = M;
+            a.K = e->ck[l];
+            a.V = e->cv[l];
+            a.kv_hstride = (long)c.max_text * D;
+            a.kv_bstride = a.kv_hstride * c.n_kv_heads;
+            a.kv_len = e->enc_len;
+            a.Hkv = c.n_kv_heads;
+            a.D = D;
+            a.G = G;
+            a.causal = 0;
+            a.scale = c.attn_scale;
+            a.O = e->datt;
+            a.ldo = e->q_dim;
+            a.chunk = 64;
+            a.nsplit = (c.max_text + 63) / 64;
+            a.kv_cap = c.max_text;
+            a.part = e->apart;
+            a.Qpart = e->part;
+            a.q_nsplit = 1;
+            a.ldqp = e->q_dim;
+            a.pos = e->next_pos;
+            a.inv_freq = e->w.inv_freq;
+            a.rope_tab = e->rope_tab;
+            RC(attention_decode(a, st));
+        }
+        {
+            DecGemmArgs g = dec_args(M, L.cross_o, d, e->q_dim, e->dv, d, nw_wide);
+            g.X = e->datt;
+            g.ldx = e->q_dim;
+            RC(gv(g, L.rm_cross_o, EPI_BF16, rm ? PRO_DIRECT : PRO_LOAD));
+        }
+        // --- GeGLU MLP
+        {
+            DecGemmArgs g = dec_args(M, L.gate_up, 2 * f, d, e->dact, f, nw_norm);
+            norm_pro(g, L.norms[3], L.norms[4], true);
+            RC(gv(g, L.rm_gate_up, EPI_GEGLU, PRO_NORM));
+        }
+        {
+            DecGemmArgs g = dec_args(M, L.down, d, f, e->dv, d, nw_wide);
+            g.X = e->dact;
+            g.ldx = f;
+            RC(gv(g, L.rm_down, EPI_BF16, PRO_DIRECT));
+        }
+    }
+    // predict head: final decoder norm fused into head1's prologue
+    {
+        DecGemmArgs g = dec_args(M, e->w.head1, d, d, e->dhh, d, nw_wide);
+        norm_pro(g, e->dec[c.n_dec_layers - 1].norms[5], e->w.dec_final_norm, false);
+        g.x_out = e->dxn;
+        g.bias = (const bf16_t*)e->w.head1_bias;
+        RC(gv(g, e->w.rm_head1, EPI_BIAS_GELU, PRO_NORM));
+    }
+    RC(gemm(e->dhh, d, M, e->w.head2, e->V, d, 1, e->w.head2_bias, e->logits, e->logits_ld, EPI_BIAS_BF16, st));
+    return T5G_OK;
+}
+
+// one decoder step + predict head for the e->B rows fed by the sampler buffers
+static int head(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st);
+static int decode_forward(t5g_engine* e, hipStream_t st) {
+    if (rm_ok(e, e->B)) return decode_fused(e, true, st);
+    if (fused_ok(e, e->B) && e->fused_p16) return decode_fused(e, false, st);
+    int rc = decoder_pass(e, e->B, e->next_token, nullptr, nullptr, e->next_pos, true, st);
+    if (rc) return rc;
+    return head(e, e->dxn, e->B, st);
+}
+
 static int head(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st) {
     const t5g_config& c = e->c;
     const int d = c.hidden;
@@ -717,9 +933,7 @@ static SamplerArgs sampler_args(t5g_engine* e, const bf16_t* logits, int ld, int
 static int decode_iter(t5g_engine* e, hipStream_t st) {
     const int B = e->B;
     RC(sample(sampler_args(e, e->logits, e->logits_ld, B), st));
-    int rc = decoder_pass(e, B, e->next_token, nullptr, nullptr, e->next_pos, true, st);
-    if (rc) return rc;
-    return head(e, e->dxn, B, st);
+    return decode_forward(e, st);
 }
 
 extern "C" int t5g_decode(t5g_engine* e, int32_t n_steps, int32_t use_graph, void* stream) {
@@ -795,10 +1009,7 @@ extern "C" int t5g_write_state(t5g_engine* e, const t5g_sampler_state* s, int32_
 
 extern "C" int t5g_step_only(t5g_engine* e, void* stream) {
     if (!e || e->B <= 0) return T5G_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
-    int rc = decoder_pass(e, e->B, e->next_token, nullptr, nullptr, e->next_pos, true, st);
-    if (rc) return rc;
-    return head(e, e->dxn, e->B, st);
+    return decode_forward(e, (hipStream_t)stream);
 }
 
 extern "C" int t5g_read_flags(t5g_engine* e, int32_t* out, int32_t B, void* stream) {
@@ -867,11 +1078,71 @@ extern "C" int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, 
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, st));
     for (int i = 0; i < iters; ++i) {
-        int rc = decoder_pass(e, e->B, e->next_token, nullptr, nullptr, e->next_pos, true, st);
-        if (rc) return rc;
-        rc = head(e, e->dxn, e->B, st);
+        int rc = decode_forward(e, st);
         if (rc) return rc;
     }
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    *avg_us = ms * 1000.f / iters;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return T5G_OK;
+}
+
+static_assert(sizeof(t5g_gemv_args) == 152, "t5g_gemv_args layout");
+
+static int gemv_from_abi(const t5g_gemv_args* g, const void* W, DecGemmArgs* out) {
+    if (!g || !W || !g->Y || g->M <= 0 || g->N <= 0 || g->K <= 0 || g->K % 32) return T5G_EINVAL;
+    DecGemmArgs a = dec_args(g->M, W, g->N, g->K, g->Y, g->ldy, g->nw);
+    a.X = (const bf16_t*)g->X;
+    a.ldx = g->ldx;
+    a.v = (const bf16_t*)g->v;
+    a.h_in = (const bf16_t*)g->h_in;
+    a.ids = g->ids;
+    a.table = (const bf16_t*)g->table;
+    a.scale = g->scale;
+    a.eps = g->eps;
+    a.post_w = (const bf16_t*)g->post_w;
+    a.pre_w = (const bf16_t*)g->pre_w;
+    a.bias = (const bf16_t*)g->bias;
+    a.h_out = (bf16_t*)g->h_out;
+    a.x_out = (bf16_t*)g->x_out;
+    a.un = g->un;
+    a.max_grid = g->max_grid;
+    a.splits = g->splits > 1 ? g->splits : 1;
+    *out = a;
+    return T5G_OK;
+}
+
+static int gemv_any(const DecGemmArgs& a, const t5g_gemv_args* g, hipStream_t st) {
+    return g->layout == 1 ? gemv_rm(a, g->epi, g->pro, st) : gemv_dec(a, g->epi, g->pro, st);
+}
+
+extern "C" int t5g_gemv(const t5g_gemv_args* g, void* stream) {
+    DecGemmArgs a;
+    int rc = gemv_from_abi(g, g ? g->W : nullptr, &a);
+    if (rc) return rc;
+    RC(gemv_any(a, g, (hipStream_t)stream));
+    return T5G_OK;
+}
+
+extern "C" int t5g_time_gemv(const t5g_gemv_args* g, const void* const* Wp_list, int32_t n_w, int32_t iters,
+                             void* stream, float* avg_us) {
+    if (!g || !Wp_list || n_w <= 0 || iters <= 0 || !avg_us) return T5G_EINVAL;
+    std::vector<DecGemmArgs> as((size_t)n_w);
+    for (int i = 0; i < n_w; ++i) {
+        int rc = gemv_from_abi(g, Wp_list[i], &as[i]);
+        if (rc) return rc;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    RC(gemv_any(as[0], g, st));  // warm
+    HIPCHK(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i) RC(gemv_any(as[i % n_w], g, st));
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;

@@ -50,26 +50,6 @@ __device__ __forceinline__ void load_x(const bf16_t* __restrict__ X, int ldx, in
     }
 }
 
-// Buffer descriptor over one row group's fragment stream: loads past `bytes` return 0
-// and move no data (hardware range check), so the weight stream needs no predication.
-// Inputs are made provably wave-uniform (readfirstlane) so no waterfall loop appears.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t frag_rsrc(const void* base, uint32_t bytes) {
-    const uint64_t p = (uint64_t)base;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
-                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-__device__ __forceinline__ bf16x8_s frag_load(__amdgpu_buffer_rsrc_t r, int kb, int lane) {
-    // aux 2 = nt: streamed once (decode weights)
-    return __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(r, (kb * 64 + lane) * 16, 0, 2));
-}
-
-__device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_b, a),
-                                                   __builtin_bit_cast(bf16x8_b, b), c, 0, 0, 0);
-}
-
 // KS = K-interleave factor of the accumulation: k-step kb belongs to slice
 // (kb - kb_lo) % KS, each slice is accumulated in k order, and the slices are
 // summed in slice order at the end. The result is therefore bit-identical

@@ -24,6 +24,41 @@ struct GemmArgs {
 int pack_p16(const bf16_t* src, int N, int K, long ld, bf16_t* dst, int NGpad, hipStream_t st);
 int gemm_p16(const GemmArgs& a, int epi, hipStream_t st);
 
+// ---- decode-step GEMV family (M <= 16) with fused row prologues (gemv.hip) ----
+// The X rows are produced inside the GEMM, in every block, from the previous
+// sub-block's bf16 output: residual add + the two RMSNorms of PMDecoderLayer
+// (PRO_NORM), or the audio embedding gather (PRO_EMBED). Outputs are whole (no
+// split-K), so the next consumer can run the same prologue on them.
+enum { PRO_LOAD = 0, PRO_NORM = 1, PRO_EMBED = 2, PRO_DIRECT = 3 };
+struct DecGemmArgs {
+    int M, K;                 // rows (<= 16), reduction length (= X row width)
+    const bf16_t* W;          // packed P16
+    int N, NG, KB;
+    const bf16_t* bias;
+    void* Y;                  // bf16 or fp32 [M][ldy]
+    int ldy;
+    const bf16_t* X;          // PRO_LOAD / PRO_DIRECT: [M][ldx]
+    int ldx;
+    const bf16_t* v;          // PRO_NORM: sub-block output [M][K] (bf16)
+    const bf16_t* h_in;       // PRO_NORM: residual stream [M][K]
+    const int* ids;           // PRO_EMBED: token ids [M]
+    const bf16_t* table;      // PRO_EMBED: embedding [vocab][K]
+    float scale;              // PRO_EMBED: normalizer
+    const bf16_t* post_w;     // PRO_NORM: RMSNorm(1+w) applied to v before the residual add
+    const bf16_t* pre_w;      // PRO_NORM / PRO_EMBED: RMSNorm(1+w) producing X
+    float eps;
+    bf16_t* h_out;            // block 0 writes the updated residual (may be null)
+    bf16_t* x_out;            // block 0 writes the normed X rows (may be null)
+    int nw;                   // waves per block (4, 8 or 16)
+    int un;                   // fragments in flight per wave (8 / 16), 0 = default
+    int max_grid;             // blocks per launch cap, 0 = one per CU
+    int splits;               // split-K over blockIdx.y (EPI_F32 slabs [splits][M][ldy]; PRO_LOAD/DIRECT)
+};
+int gemv_dec(const DecGemmArgs& a, int epi, int pro, hipStream_t st);
+size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int pro, int rg);
+// row-major VALU variant (W = plain [N][K]; GeGLU: gate rows then up rows), M <= 8
+int gemv_rm(const DecGemmArgs& a, int epi, int pro, hipStream_t st);
+
 // ---- row-wise residual / RMSNorm / embedding -------------------------------
 struct NormArgs {
     int M, d;

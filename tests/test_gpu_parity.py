@@ -306,3 +306,29 @@ def test_sampler_kernel_vs_reference_golden():
                   tok, c["token"])
     print(f"sampler: {ok}/{len(meta['cases'])} exact, {amb} ambiguous")
     assert ok == len(meta["cases"])
+
+
+@pytest.mark.parametrize("variant", ["1", "2"])
+@pytest.mark.parametrize("case", ["golden_tiny", "golden_mid"])
+def test_decode_variants_teacher_forced(variant, case, monkeypatch):
+    """The opt-in decode-step GEMV variants (T5G_FUSED_DECODE=1: norm prologues fused into
+    row-major VALU GEMVs; 2: fused prologues on the P16 MFMA GEMVs) against the CPU
+    oracle, teacher-forced, on the tiny golden cases and at true 2b-2b widths."""
+    _need_gpu()
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import Utterance
+    from t5gemma_tts_amd.weights import synthetic_weights
+    monkeypatch.setenv("T5G_FUSED_DECODE", variant)
+    meta, _ = _load(case)
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    eng = _engine(cfg, sd, max_batch=4, max_text=64, max_audio=256 if case == "golden_tiny" else 128,
+                  max_gen=200 if case == "golden_tiny" else 64)
+    cases = meta["cases"][:3]
+    utts = [Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"]) for c in cases]
+    out = eng.generate(utts, [_params(c) for c in cases], seeds=[c["seed"] for c in cases], parity=True,
+                       record_logits=True)
+    for b, c in enumerate(cases):
+        one = {"gen": [out["gen"][b]], "logits": [[l[b]] for l in out["logits"]]}
+        w, ex = teacher_forced_check(cfg, sd, utts[b], _oparams(c), c["seed"], one, rtol=0.02)
+        print(f"variant {variant} {case} row {b}: max rel logit err {w:.3g}, exact rows {ex}/{len(out['gen'][b])}")
