@@ -7,7 +7,7 @@ import json
 import os
 import sys
 
-KERNEL = "gemv_dec_kernel<4, 2, 3, 1, 1, 5>"
+KERNEL = "gemm_p16_kernel<1, 2, 2, 3, true>"
 
 
 def mean_counter(path):
@@ -20,8 +20,8 @@ def main(out_dir="gpurun_out", dst="profiles/pmc_gate_up.json"):
     f, nf, cf = mean_counter(os.path.join(out_dir, "pmc_fetch", "pmc_counter_collection.csv"))
     w, nw, cw = mean_counter(os.path.join(out_dir, "pmc_write", "pmc_counter_collection.csv"))
     hbm = f * 1024 * 2 + w * 1024
-    alg = 2 * 9216 * 2304 * 2 + 2 * 8 * 2304 * 2 + 8 * 9216 * 2
-    res = {"kernel": KERNEL + " (decode gate/up GEGLU + norm prologue, M=8, N=18432, K=2304)",
+    alg = 2 * 9216 * 2304 * 2 + 8 * 2304 * 2 + 8 * 9216 * 2
+    res = {"kernel": KERNEL + " (decode gate/up GEGLU, M=8, N=18432, K=2304)",
            "launches": nf, "FETCH_SIZE_KiB_mean": f, "WRITE_SIZE_KiB_mean": w,
            "correction": "bytes = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (gfx950: FETCH_SIZE is half of 16B/lane reads)",
            "hbm_bytes_per_launch": int(hbm), "algorithmic_bytes_per_launch": alg,
