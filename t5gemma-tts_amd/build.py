@@ -35,12 +35,12 @@ def _newest_dep() -> float:
     return max(os.path.getmtime(p) for p in deps if os.path.exists(p))
 
 
-def _compile(src: str, force: bool) -> str:
+def _compile(src: str, force: bool, dbg: bool = False) -> str:
     s = os.path.join(CSRC, src)
-    o = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+    o = os.path.join(OBJ, ("dbg_" if dbg else "") + os.path.splitext(src)[0] + ".o")
     if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), _newest_dep()):
         return o
-    cmd = [_hipcc()] + FLAGS + ["-c", s, "-o", o]
+    cmd = [_hipcc()] + FLAGS + (["-DT5G_DBG_TS=1"] if dbg else []) + ["-c", s, "-o", o]
     if src.endswith(".cpp"):
         cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-I",
                os.path.join(REPO, "include"), "-c", s, "-o", o]
@@ -50,21 +50,24 @@ def _compile(src: str, force: bool) -> str:
     return o
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
+def build(force: bool = False, verbose: bool = True, dbg: bool = False) -> str:
+    """dbg=True builds the diagnostic variant lib/libt5gtts_dbg.so (per-block timestamps,
+    common.h T5G_TS; used only by tools/micro_timeline.cpp, never by the product)."""
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    lib = LIB.replace(".so", "_dbg.so") if dbg else LIB
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        objs = list(ex.map(lambda s: _compile(s, force, dbg), srcs))
+    if force or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
         if verbose:
-            print(f"[t5gtts] built {LIB}")
-    return LIB
+            print(f"[t5gtts] built {lib}")
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, dbg="--dbg" in sys.argv)

@@ -17,6 +17,8 @@
 
 namespace t5g {
 
+T5G_TS_UNIT(attn)
+
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
     // grid: (token, pair-block); thread = one (head, i) rotation pair (i, i + D/2)
@@ -285,6 +287,16 @@ __device__ __forceinline__ void merge_splits(const AttnArgs& a, const float* bas
                                              float* Linv) {
     constexpr int ZMAX = 16;  // splits held in registers; more are streamed
     const int S = a.nsplit;
+    // Slabs are read with sc1 loads (L1 bypass): in the in-launch merge they were
+    // written moments ago by other workgroups with sc1 (write-through) stores, the
+    // CDNA guide G16 row-1 hand-off (no acquire fence needed).
+    const __amdgpu_buffer_rsrc_t rs = frag_rsrc(base, (uint32_t)S * G * (D + 2) * 4u);
+    auto ld4 = [&](int off) __attribute__((always_inline)) {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off * 4, 0, 16));
+    };
+    auto ld1 = [&](int off) __attribute__((always_inline)) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off * 4, 0, 16));
+    };
     // every thread owns <= 1 (g, d4) quad when G*D/4 <= blockDim (D = 256, G = 2: 128 quads)
     const int idx = threadIdx.x;
     const bool own = idx < G * D / 4;
@@ -292,11 +304,11 @@ __device__ __forceinline__ void merge_splits(const AttnArgs& a, const float* bas
     f32x4 pv[ZMAX];
 #pragma unroll
     for (int z = 0; z < ZMAX; ++z)
-        if (own && z < S) pv[z] = *(const f32x4*)(base + (long)z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
+        if (own && z < S) pv[z] = ld4(z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
     if (threadIdx.x < 64 * G) {
         const int gg = threadIdx.x / 64, z = threadIdx.x % 64;
-        const float m = z < S ? base[(long)z * G * (D + 2) + gg * (D + 2)] : -INFINITY;
-        const float l = z < S ? base[(long)z * G * (D + 2) + gg * (D + 2) + 1] : 0.f;
+        const float m = z < S ? ld1(z * G * (D + 2) + gg * (D + 2)) : -INFINITY;
+        const float l = z < S ? ld1(z * G * (D + 2) + gg * (D + 2) + 1) : 0.f;
         const float M = wave_max(m);
         const float w = (m == -INFINITY) ? 0.f : expf(m - M);
         const float L = wave_sum(w * l);
@@ -314,7 +326,7 @@ __device__ __forceinline__ void merge_splits(const AttnArgs& a, const float* bas
         }
     for (int z = ZMAX; z < S; ++z) {
         const float w = wz[g * 64 + z];
-        if (w != 0.f) acc += w * *(const f32x4*)(base + (long)z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
+        if (w != 0.f) acc += w * ld4(z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
     }
     const float inv = Linv[g];
     uint2 o;
@@ -344,6 +356,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     const int qi = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int kg = lane / LPK, dl = lane % LPK;
+    T5G_TS(0);
     const int row = a.q_row ? a.q_row[qi] : qi;
     // row length / query position first: the oldest outstanding load is the first one a
     // wave can wait for, so these must not queue behind the K/V stream
@@ -357,8 +370,13 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         lo = max(0, t - a.window);
         hi = min(len, t + a.window + 1);
     }
-    const int c0 = lo + sp * CH;
-    const int c1 = min(hi, c0 + CH);
+    // The row's keys [lo, hi) are split into nsplit equal chunks (<= CH keys each, since
+    // nsplit * CH >= kv_cap): every block streams the same share whatever the row length,
+    // and no block loads keys past it (the old fixed 64-key chunks streamed whole chunks
+    // for blocks past the length: 31 MB instead of 17 MB per layer at L = 527).
+    const int chunk = (max(hi - lo, 0) + a.nsplit - 1) / a.nsplit;
+    const int c0 = lo + sp * chunk;
+    const int c1 = min(hi, c0 + chunk);
     const int n = c1 - c0;
     // the block whose keys include t appends the step's own key/value (a.append)
     const bool has_t = a.append && a.Qpart && t >= c0 && t < c1;
@@ -406,17 +424,18 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             s8[4 + jj] = sb[jj];
         }
     }
-    // Unless a sliding window has moved the first key (lo > 0) the block's keys start at
-    // sp*CH whatever the row length: request K/V now (one memory round trip per block).
-    // Always issued (a guarded batch would make the compiler merge wait counts at the
-    // join); the rare lo > 0 block re-reads its keys below.
-    const bool spec = lo == 0;
+    // K/V of the block's keys, requested right behind the q slabs: buffer loads, keys
+    // past c1 fall outside the descriptor (zeros, no traffic) -- no branch, so the
+    // compiler keeps one in-order wait per use
+    const __amdgpu_buffer_rsrc_t krs = frag_rsrc(Kb, (uint32_t)a.kv_cap * D * 2u);
+    const __amdgpu_buffer_rsrc_t vrs = frag_rsrc(Vb, (uint32_t)a.kv_cap * D * 2u);
     u32x4 kr[NIT], vr[NIT];
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-        const int j = min(sp * CH + i * KPB + wave * KPW + kg, a.kv_cap - 1);
-        kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
-        vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
+        const int j = c0 + i * KPB + wave * KPW + kg;
+        const int off = j < c1 ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
+        kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
+        vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
     }
     float q[G][8];
     if (a.Qpart) {
@@ -441,6 +460,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             }
         }
         __syncthreads();
+        T5G_TS(1);
         // lower half: x*c + (-x2)*s ; upper half: x*c + x1*s (one branch-free formula)
         const float sg = dl < LPK / 2 ? -1.0f : 1.0f;
         const int pbase = (8 * dl + D / 2) % D;
@@ -465,15 +485,11 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     }
     const long pstride = (long)G * (D + 2);
     float* pbase = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * pstride;
-    float* part = pbase + sp * pstride;
+    const __amdgpu_buffer_rsrc_t prs = frag_rsrc(pbase, (uint32_t)(a.nsplit * pstride * 4));
     if (n > 0) {
 #pragma unroll
         for (int i = 0; i < NIT; ++i) {
             const int j = c0 + i * KPB + wave * KPW + kg;
-            if (!spec && j < c1) {
-                kr[i] = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
-                vr[i] = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
-            }
             if (j >= c1) {
                 kr[i] = (u32x4){0u, 0u, 0u, 0u};
                 vr[i] = (u32x4){0u, 0u, 0u, 0u};
@@ -525,6 +541,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             }
         }
         __syncthreads();
+        T5G_TS(2);
         if (wave < G) {
             const int g = wave;
             const float s = lane < n ? sm[g][lane] : -INFINITY;
@@ -570,18 +587,20 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             }
         }
         __syncthreads();
+        T5G_TS(4);
         for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
             const int g = idx / LPK, d8 = idx % LPK;
             const f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
             const f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
             if (a.nsplit > 1) {
-                float* pg = part + g * (D + 2);
+                // sc1 (write-through) slab stores: the merging block may sit on another XCD
+                const int pg = sp * (int)pstride + g * (D + 2);
                 if (d8 == 0) {
-                    pg[0] = stat[g][0];
-                    pg[1] = stat[g][1];
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(stat[g][0]), prs, pg * 4, 0, 16);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(stat[g][1]), prs, (pg + 1) * 4, 0, 16);
                 }
-                *(f32x4*)(pg + 2 + 8 * d8) = lo4;
-                *(f32x4*)(pg + 6 + 8 * d8) = hi4;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo4), prs, (pg + 2 + 8 * d8) * 4, 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi4), prs, (pg + 6 + 8 * d8) * 4, 0, 16);
             } else {
                 const float inv = 1.0f / stat[g][1];
                 u32x4 w;
@@ -593,29 +612,29 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             }
         }
     } else if (a.nsplit > 1 && threadIdx.x < G) {
-        part[threadIdx.x * (D + 2)] = -INFINITY;
-        part[threadIdx.x * (D + 2) + 1] = 0.f;
+        const int pg = sp * (int)pstride + threadIdx.x * (D + 2);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(-INFINITY), prs, pg * 4, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(0u, prs, (pg + 1) * 4, 0, 16);
     }
+    T5G_TS(5);
     if (a.nsplit == 1 || !a.counters) return;
-    // ---- in-launch merge: release this block's slab, take a ticket; the last merges
+    // ---- in-launch merge (CDNA guide G16, valid form row 1): every storing wave drains
+    // its sc1 slab stores, then one lane adds to the (row, kv head) ticket; the block
+    // whose add returns nsplit-1 merges, reading the slabs with sc1 loads. No fences.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int* ctr = a.counters + qi * a.Hkv + kvh;
         const int ticket = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = ticket == a.nsplit - 1;
-        if (last) {
-            __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next launch
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
         last_flag = last;
     }
     __syncthreads();
     if (!last_flag) return;
+    T5G_TS(3);
     merge_splits<D, G>(a, pbase, qi, kvh, wz, Linv);
+    T5G_TS(6);
 }
 
 // merge of the key-split partials (used when no ticket counters are supplied):
@@ -625,8 +644,10 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a) {
     __shared__ float wz[G * 64];
     __shared__ float Linv[G];
     const int qi = blockIdx.x, kvh = blockIdx.y;
+    T5G_TS(3);
     const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2));
     merge_splits<D, G>(a, base, qi, kvh, wz, Linv);
+    T5G_TS(6);
 }
 
 template <int D, int G>
@@ -642,6 +663,7 @@ static int launch_decode(const AttnArgs& a, hipStream_t st) {
 int attention_decode(const AttnArgs& a, hipStream_t st) {
     if (a.Mq <= 0) return 0;
     if (a.nsplit < 1 || a.nsplit > 64 || !a.part || a.eager) return -1;
+    if ((long)a.nsplit * 64 < a.kv_cap || a.kv_cap <= 0) return -1;   // chunks of <= 64 keys
     if (a.append && (!a.Qpart || !a.rope_tab || (a.G + 2) * a.D / 4 > 256)) return -1;
     if (a.Qpart && (a.q_nsplit < 1 || a.q_nsplit > QSMAX)) return -1;
     if (a.D == 256 && a.G == 2) return launch_decode<256, 2>(a, st);

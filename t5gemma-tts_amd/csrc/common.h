@@ -118,3 +118,31 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_b, a),
                                                    __builtin_bit_cast(bf16x8_b, b), c, 0, 0, 0);
 }
+
+// ---- diagnostic block timelines (built only into the T5G_DBG_TS library variant,
+// tools/micro_timeline.cpp): thread 0 of every block stores the 100 MHz device clock
+// at numbered points of its kernel, slot 7 = (XCC id << 32) | HW_ID (CU placement).
+// Each translation unit has its own buffer pointer, set by t5g_dbg_set_<unit>(); records
+// of launch `a.dbg_seq` (args field, 0 in the product) start at block slot dbg_seq * 4096.
+#ifdef T5G_DBG_TS
+#define T5G_TS_UNIT(unit)                                                          \
+    __device__ unsigned long long* t5g_dbg_ts_buf;                                 \
+    extern "C" int t5g_dbg_set_##unit(void* p) {                                   \
+        return hipMemcpyToSymbol(HIP_SYMBOL(t5g_dbg_ts_buf), &p, sizeof(p)) == hipSuccess ? 0 : -1; \
+    }
+#define T5G_TS(k)                                                                                  \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && t5g_dbg_ts_buf) {                                                 \
+            const size_t blin_ = (size_t)a.dbg_seq * 4096 +                                         \
+                                 blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);   \
+            t5g_dbg_ts_buf[blin_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                    \
+            if ((k) == 0)                                                                          \
+                t5g_dbg_ts_buf[blin_ * 8 + 7] =                                                    \
+                    ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |       \
+                    __builtin_amdgcn_s_getreg((31 << 11) | 4);                                     \
+        }                                                                                          \
+    } while (0)
+#else
+#define T5G_TS_UNIT(unit)
+#define T5G_TS(k) do { } while (0)
+#endif

@@ -70,7 +70,7 @@ struct t5g_engine {
     int* next_token;
     int* flags;
     int* last_rows;
-    int* attn_tickets;  // [max_batch][Hkv] in-launch split-merge counters (self-re-arming)
+    int* attn_tickets_buf;  // [max_batch][Hkv] in-launch split-merge counters (self-re-arming)
     float* rope_tab;    // [max_batch][D] per-row cos|sin of the decode step's PM position
     // multi-block sampler scratch (sampler.hip fast path)
     float* fs_val;
@@ -81,6 +81,12 @@ struct t5g_engine {
     unsigned* fs_ticket;
     int* fs_slow;
     bool fast_sampler = true;   // T5G_SAMPLER_FAST=0 at creation: single-block sampler only
+    // decode attention: key-split partials merged in-launch by the last block of each
+    // (row, kv head) (T5G_ATTN_TICKETS=1) instead of a combine launch; cross attention
+    // keys split over T5G_XATTN_SPLIT blocks per (row, kv head). Both off by default:
+    // measured on MI355X (tools/micro_timeline.cpp) neither beats the combine launch.
+    bool attn_tickets = false;
+    int xsplit = 1;
     int B = 0;            // rows of the current call
     const bf16_t* noise = nullptr;
     int noise_steps = 0;
@@ -162,7 +168,8 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->part, e->part_elems);
     const int G = c.n_heads / c.n_kv_heads;
     const int nsplit_dec = (c.max_audio + 63) / 64;
-    const int nsplit_x = (c.max_text + 63) / 64;
+    // cross-attention key splits: up to max(ceil(max_text / 64), 16) (T5G_XATTN_SPLIT cap)
+    const int nsplit_x = (c.max_text + 63) / 64 > 16 ? (c.max_text + 63) / 64 : 16;
     e->apart_elems = (int64_t)B * Hkv * (nsplit_dec > nsplit_x ? nsplit_dec : nsplit_x) * G * (D + 2);
     rc |= alloc(e, &e->apart, e->apart_elems);
     const int64_t enc_cache = (int64_t)B * Hkv * c.max_text * D;
@@ -200,7 +207,7 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->next_token, B);
     rc |= alloc(e, &e->flags, B);
     rc |= alloc(e, &e->last_rows, B);
-    rc |= alloc(e, &e->attn_tickets, (int64_t)B * Hkv);
+    rc |= alloc(e, &e->attn_tickets_buf, (int64_t)B * Hkv);
     rc |= alloc(e, &e->rope_tab, (int64_t)B * D);
     rc |= alloc(e, &e->fs_val, (int64_t)B * FS_NB * FS_CAP);
     rc |= alloc(e, &e->fs_idx, (int64_t)B * FS_NB * FS_CAP);
@@ -215,6 +222,13 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
         const char* fdv = getenv("T5G_FUSED_DECODE");
         e->fused_decode = fdv && (fdv[0] == '1' || fdv[0] == '2');
         e->fused_p16 = fdv && fdv[0] == '2';
+        const char* atv = getenv("T5G_ATTN_TICKETS");
+        e->attn_tickets = atv && atv[0] == '1';
+        const char* xsv = getenv("T5G_XATTN_SPLIT");
+        e->xsplit = xsv ? atoi(xsv) : 1;
+        const int xmax = (c.max_text + 63) / 64 > 16 ? (c.max_text + 63) / 64 : 16;
+        if (e->xsplit < (c.max_text + 63) / 64) e->xsplit = (c.max_text + 63) / 64;
+        if (e->xsplit > xmax) e->xsplit = xmax;
     }
     if (rc) {
         t5g_engine_destroy(e);
@@ -228,6 +242,7 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
 static int gemm(const bf16_t* X, int ldx, int M, const void* W, int N, int K, int splits, const void* bias,
                 void* Y, int ldy, int epi, hipStream_t st) {
     GemmArgs a;
+    memset(&a, 0, sizeof(a));
     a.X = X;
     a.ldx = ldx;
     a.M = M;
@@ -475,7 +490,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
                 a.nsplit = (c.max_audio + 63) / 64;
                 a.kv_cap = c.max_audio;
                 a.part = e->apart;
-                a.counters = nullptr;  // separate combine launch (cheaper than in-launch tickets)
+                a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
                 if (s_qkv > 1) {
                     a.Qpart = e->part;
                     a.q_nsplit = s_qkv;
@@ -569,10 +584,10 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             a.ldo = e->q_dim;
             if (fuse_q) {
                 a.chunk = 64;
-                a.nsplit = (c.max_text + 63) / 64;
+                a.nsplit = e->xsplit;
                 a.kv_cap = c.max_text;
                 a.part = e->apart;
-                a.counters = nullptr;  // separate combine launch (cheaper than in-launch tickets)
+                a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
                 a.Qpart = e->part;
                 a.q_nsplit = s_cq;
                 a.ldqp = e->q_dim;
@@ -739,6 +754,7 @@ static int decode_fused(t5g_engine* e, bool rm, hipStream_t st) {
             a.nsplit = (c.max_audio + 63) / 64;
             a.kv_cap = c.max_audio;
             a.part = e->apart;
+            a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
             a.Qpart = e->part;
             a.q_nsplit = 1;
             a.ldqp = e->qkv_dim;
@@ -781,9 +797,10 @@ static int decode_fused(t5g_engine* e, bool rm, hipStream_t st) {
             a.O = e->datt;
             a.ldo = e->q_dim;
             a.chunk = 64;
-            a.nsplit = (c.max_text + 63) / 64;
+            a.nsplit = e->xsplit;
             a.kv_cap = c.max_text;
             a.part = e->apart;
+            a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
             a.Qpart = e->part;
             a.q_nsplit = 1;
             a.ldqp = e->q_dim;

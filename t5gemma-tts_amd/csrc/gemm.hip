@@ -23,6 +23,8 @@
 
 namespace t5g {
 
+T5G_TS_UNIT(gemm)
+
 __global__ void pack_p16_kernel(const bf16_t* __restrict__ src, int N, int K, long ld,
                                 bf16_t* __restrict__ dst, int KB, long nfrag) {
     long frag = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -66,6 +68,7 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
     __shared__ f32x4 red[4][MT][64];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    T5G_TS(0);
     const int g = blockIdx.x * RG + wave / WPG;
     const int ks = wave % WPG;
     const int m0 = blockIdx.z * 16 * MT;
@@ -120,6 +123,7 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
             }
         }
         __syncthreads();
+        T5G_TS(1);
         const int xr = lane & 15;
         const bf16_t* xrow = xs + min(xr, rows - 1) * ldsx + 8 * (lane >> 4) - kb_lo * 32;
         for (; kb < kb_hi; kb += STEP) {
@@ -188,26 +192,31 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
     }
 
 #pragma unroll
+    T5G_TS(2);
     for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[0][mt];
     __syncthreads();
 
-    constexpr int OG = (EPI == EPI_GEGLU) ? RG / 2 : RG;  // output groups per block
-    if (wave >= OG) return;
+    // GeGLU: a row group is 8 gate rows then the same 8 features' up rows (so one group
+    // is one output group and the decode grid has 2F/16 blocks): lanes 0-31 hold the
+    // gate sums, lanes 32-63 the up sums of the same (feature, batch row)
+    constexpr int OG = RG;  // output groups per block
+    constexpr bool GLU = EPI == EPI_GEGLU;
+    if (wave >= OG || (GLU && lane >= 32)) return;
     const int og = wave;
-    const int n_out = (EPI == EPI_GEGLU) ? a.N / 2 : a.N;
+    const int n_out = GLU ? a.N / 2 : a.N;
     const int gout = blockIdx.x * OG + og;
-    const int n0 = gout * 16 + 4 * (lane >> 4);
+    const int n0 = gout * (GLU ? 8 : 16) + 4 * (lane >> 4);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
         const int m = m0 + mt * 16 + (lane & 15);
         if (m >= a.M) continue;
         float v[4];
-        if constexpr (EPI == EPI_GEGLU) {
+        if constexpr (GLU) {
             f32x4 gs = {0.f, 0.f, 0.f, 0.f}, us = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < WPG; ++s) {
-                gs += red[(2 * og) * WPG + s][mt][lane];
-                us += red[(2 * og + 1) * WPG + s][mt][lane];
+                gs += red[og * WPG + s][mt][lane];
+                us += red[og * WPG + s][mt][lane + 32];
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -255,6 +264,7 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
             }
         }
     }
+    T5G_TS(3);
 }
 
 // ---------------------------------------------------------------------------

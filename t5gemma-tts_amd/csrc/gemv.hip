@@ -288,21 +288,25 @@ __global__ __launch_bounds__(NW * 64) void gemv_dec_kernel(DecGemmArgs a) {
     }
     __syncthreads();
 
-    constexpr int OG = (EPI == EPI_GEGLU) ? RG / 2 : RG;   // output groups per unit
+    // GeGLU: a row group is 8 gate rows then the same 8 features' up rows, so one row
+    // group is one output group of 8 features: lanes 0-31 hold its gate sums, lanes 32-63
+    // the up sums of the same (feature, batch row)
+    constexpr bool GLU = EPI == EPI_GEGLU;
+    constexpr int OG = RG;   // output groups per unit
     const int m = xr;
-    if (m >= a.M) return;
-    const int n_out = (EPI == EPI_GEGLU) ? a.N / 2 : a.N;
+    if (m >= a.M || (GLU && lane >= 32)) return;
+    const int n_out = GLU ? a.N / 2 : a.N;
     for (int t = wave; t < nu * OG; t += NW) {
         const int i = t / OG, og = t - i * OG;
         const f32x4* ri = red + (size_t)i * NW * 64 + lane;
-        const int n0 = (((int)blockIdx.x + i * nb) * OG + og) * 16 + 4 * (lane >> 4);
+        const int n0 = (((int)blockIdx.x + i * nb) * OG + og) * (GLU ? 8 : 16) + 4 * (lane >> 4);
         float v[4];
-        if constexpr (EPI == EPI_GEGLU) {
+        if constexpr (GLU) {
             f32x4 gs = {0.f, 0.f, 0.f, 0.f}, us = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < WPG; ++s) {
-                gs += ri[((2 * og) * WPG + s) * 64];
-                us += ri[((2 * og + 1) * WPG + s) * 64];
+                gs += ri[(og * WPG + s) * 64];
+                us += ri[(og * WPG + s) * 64 + 32];
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_tanh(rbf(gs[r]))) * rbf(us[r]);

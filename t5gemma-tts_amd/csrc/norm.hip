@@ -17,6 +17,8 @@
 
 namespace t5g {
 
+T5G_TS_UNIT(norm)
+
 constexpr int NSPLIT_MAX = 8;
 
 __device__ __forceinline__ void unpack8(u32x4 w, float (&v)[8]) {
@@ -54,6 +56,7 @@ __device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, u32x4 w8
 template <int NS, int SRC>   // NS: split-K slabs of the part path; SRC: 0 delta, 1 ids, 2 part
 __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_post, int has_resid, int has_pre) {
     __shared__ float red[32];
+    T5G_TS(0);
     const int mi = blockIdx.x;
     const int m = a.out_rows ? a.out_rows[mi] : mi;
     const int d = a.d;
@@ -90,6 +93,7 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
         unpack8(*(const u32x4*)(a.delta + (long)m * d + 8 * cc), v);
     }
     if (has_post) rms8(v, active, d, w_post, a.eps, red);
+    T5G_TS(1);
     if (has_resid) {
         float r8[8];
         unpack8(rw, r8);
@@ -102,6 +106,7 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
         rms8(v, active, d, w_pre, a.eps, red);
         if (active) *(u32x4*)(a.normed_out + orow * d + 8 * c) = pack8(v);
     }
+    T5G_TS(2);
 }
 
 int resid_norm(const NormArgs& a_in, hipStream_t st) {

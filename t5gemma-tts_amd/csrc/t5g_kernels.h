@@ -20,6 +20,7 @@ struct GemmArgs {
     const bf16_t* bias;
     void* Y;          // bf16 [M][ldy] or f32 [splits][M][ldy]
     int ldy;
+    int dbg_seq;      // diagnostic timeline slot (T5G_DBG_TS builds only)
 };
 int pack_p16(const bf16_t* src, int N, int K, long ld, bf16_t* dst, int NGpad, hipStream_t st);
 int gemm_p16(const GemmArgs& a, int epi, hipStream_t st);
@@ -75,6 +76,7 @@ struct NormArgs {
     bf16_t* resid_out;       // [M][d] or null
     bf16_t* normed_out;      // [M][d] or null
     const int* out_rows;     // optional: process only rows out_rows[i] (i < M), write compact
+    int dbg_seq;             // diagnostic timeline slot (T5G_DBG_TS builds only)
 };
 int resid_norm(const NormArgs& a, hipStream_t st);
 
@@ -133,6 +135,7 @@ struct AttnArgs {
     // decode self-attention: the block holding key t = kv_len-1 builds it from the
     // projection slabs (k rotated by PM-RoPE, v as is), uses it and appends it to K/V
     int append, k_col0, v_col0;
+    int dbg_seq;             // diagnostic timeline slot (T5G_DBG_TS builds only)
 };
 int attention(const AttnArgs& a, hipStream_t st);
 // decode-shaped (64-key blocks, split over blockIdx.z, sdpa numerics); nsplit = ceil(keys/64)

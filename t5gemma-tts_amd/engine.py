@@ -119,7 +119,9 @@ class T5GemmaTTSEngine:
         d, f = bb.hidden_size, bb.intermediate_size
 
         def interleave_gate_up(gate, up):
-            return torch.stack([gate.view(f // 16, 16, d), up.view(f // 16, 16, d)], dim=1).reshape(2 * f, d)
+            # 16-row P16 groups of 8 gate rows then the same 8 features' up rows: one
+            # MFMA tile holds gate and up of its features (GeGLU epilogue, gemm.hip)
+            return torch.stack([gate.view(f // 8, 8, d), up.view(f // 8, 8, d)], dim=1).reshape(2 * f, d)
 
         def layer(side: str, i: int) -> _lib.LayerWeights:
             p = f"backbone.model.{side}.layers.{i}"

@@ -33,7 +33,7 @@ def _epilogue(acc, epi, bias):
         return (acc + bias.float()).to(BF16).float()
     if epi == 2:
         return torch.nn.functional.gelu((acc + bias.float()).to(BF16).float()).to(BF16).float()
-    a3 = acc.view(M, N // 32, 2, 16)
+    a3 = acc.view(M, N // 16, 2, 8)   # 8 gate rows, then the same 8 features' up rows
     gate, up = a3[:, :, 0].reshape(M, -1), a3[:, :, 1].reshape(M, -1)
     act = torch.nn.functional.gelu(gate.to(BF16).float(), approximate="tanh").to(BF16).float()
     return (act * up.to(BF16).float()).to(BF16).float()

@@ -71,8 +71,8 @@ def test_gemm_p16_vs_fp32(M, N, K, epi, splits):
         ref = (acc + bias.float()).to(BF16).float()
     elif epi == 2:
         ref = torch.nn.functional.gelu((acc + bias.float()).to(BF16).float()).to(BF16).float()
-    else:  # GeGLU over interleaved 16-row groups (gate, up, gate, up, ...)
-        a3 = acc.view(M, N // 32, 2, 16)
+    else:  # GeGLU over interleaved 8-row groups (gate, up, gate, up, ...)
+        a3 = acc.view(M, N // 16, 2, 8)
         gate, up = a3[:, :, 0].reshape(M, -1), a3[:, :, 1].reshape(M, -1)
         act = torch.nn.functional.gelu(gate.to(BF16).float(), approximate="tanh").to(BF16).float()
         ref = (act * up.to(BF16).float()).to(BF16).float()
