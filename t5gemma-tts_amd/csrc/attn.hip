@@ -373,8 +373,11 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     // The row's keys [lo, hi) are split into nsplit equal chunks (<= CH keys each, since
     // nsplit * CH >= kv_cap): every block streams the same share whatever the row length,
     // and no block loads keys past it (the old fixed 64-key chunks streamed whole chunks
-    // for blocks past the length: 31 MB instead of 17 MB per layer at L = 527).
-    const int chunk = (max(hi - lo, 0) + a.nsplit - 1) / a.nsplit;
+    // for blocks past the length: 31 MB instead of 17 MB per layer at L = 527). A row of
+    // <= CH keys stays one chunk (one softmax pass, no merge: closest to the reference's
+    // single-pass sdpa on short rows).
+    const int span = max(hi - lo, 0);
+    const int chunk = span <= CH ? span : (span + a.nsplit - 1) / a.nsplit;
     const int c0 = lo + sp * chunk;
     const int c1 = min(hi, c0 + chunk);
     const int n = c1 - c0;

@@ -18,6 +18,8 @@
 // (WPG = 4: decode, 1 row group / block; WPG = 1: prefill, 4 row groups / block
 // reading the same X fragments through L1). blockIdx.y splits K across blocks
 // (fp32 partial slabs reduced by the consumer kernel, in fixed order).
+#include <stdlib.h>
+
 #include "common.h"
 #include "t5g_kernels.h"
 
@@ -100,11 +102,12 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
         // fragments kb >= kb_hi fall outside the descriptor: zero, no traffic
         const __amdgpu_buffer_rsrc_t wr = frag_rsrc(a.W + (long)g * a.KB * 512, (uint32_t)kb_hi * 1024u);
         bf16x8_s wcur[UN];
-#pragma unroll
-        for (int u = 0; u < UN; ++u) wcur[u] = frag_load(wr, kb + u * KS, lane);
         {
             // all X chunks of the thread are requested at once (buffer loads: slots past
-            // the block's rows fall outside the descriptor -> 0, no traffic), then written
+            // the block's rows fall outside the descriptor -> 0, no traffic), then the first
+            // weight group: vmcnt retires in issue order, so the LDS writes below wait for
+            // the X rows only, not behind the weight group (HBM) they were queued after
+            // before (5 us of the gate/up block spent here, tools/micro_timeline.cpp)
             const int total = rows * kspan * 4;
             const __amdgpu_buffer_rsrc_t xrs = frag_rsrc(a.X + (long)m0 * a.ldx, (uint32_t)rows * a.ldx * 2u);
             bf16x8_s xv[XCH];
@@ -115,6 +118,8 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
                 const int off = idx < total ? (r * a.ldx + kb_lo * 32 + 8 * c) * 2 : 0x7ffffff0;
                 xv[i] = __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
             }
+#pragma unroll
+            for (int u = 0; u < UN; ++u) wcur[u] = frag_load(wr, kb + u * KS, lane);
 #pragma unroll
             for (int i = 0; i < XCH; ++i) {
                 const int idx = threadIdx.x + 256 * i;
@@ -292,6 +297,17 @@ static void launch_t(const GemmArgs& a, int mblocks, hipStream_t st) {
     }
 }
 
+// GeGLU K-interleave: 2 (default; decode block = 2 row groups x 2 waves) or 4
+// (T5G_GEGLU_KS4=1: decode block = 1 row group x 4 waves, twice the blocks). Read once.
+static int geglu_ks() {
+    static int ks = 0;
+    if (!ks) {
+        const char* v = getenv("T5G_GEGLU_KS4");
+        ks = (v && v[0] == '1') ? 4 : 2;
+    }
+    return ks;
+}
+
 // decode (WPG = KS) and prefill (WPG = 1) instantiate the same slice order
 template <int MT, bool PREFILL>
 static int launch_epi(const GemmArgs& a, int epi, int mblocks, hipStream_t st) {
@@ -301,7 +317,10 @@ static int launch_epi(const GemmArgs& a, int epi, int mblocks, hipStream_t st) {
         case EPI_BF16: launch_t<MT, W4, 4, EPI_BF16>(a, mblocks, st); break;
         case EPI_BIAS_BF16: launch_t<MT, W4, 4, EPI_BIAS_BF16>(a, mblocks, st); break;
         case EPI_BIAS_GELU: launch_t<MT, W4, 4, EPI_BIAS_GELU>(a, mblocks, st); break;
-        case EPI_GEGLU: launch_t<MT, W2, 2, EPI_GEGLU>(a, mblocks, st); break;
+        case EPI_GEGLU:
+            if (geglu_ks() == 4) launch_t<MT, W4, 4, EPI_GEGLU>(a, mblocks, st);
+            else launch_t<MT, W2, 2, EPI_GEGLU>(a, mblocks, st);
+            break;
         case EPI_F32: launch_t<MT, W4, 4, EPI_F32>(a, mblocks, st); break;
         default: return -4;
     }

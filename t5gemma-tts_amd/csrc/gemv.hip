@@ -189,7 +189,10 @@ __global__ __launch_bounds__(NW * 64) void gemv_dec_kernel(DecGemmArgs a) {
     // after the MFMA of (ic, jc): a finished unit's partial sums go to LDS
     auto retire = [&]() __attribute__((always_inline)) {
         if (jc == spu - 1) {   // wave-uniform
-            red[(ic * NW + wave) * 64 + lane] = acc;
+            // the padded tail of the stream (steps past nu units, loop rounds to 2*UN)
+            // must not store: red holds umax units and the staged X rows follow it in
+            // LDS, still being read by the other waves (intermittent wrong outputs)
+            if (ic < nu) red[(ic * NW + wave) * 64 + lane] = acc;
             acc = (f32x4){0.f, 0.f, 0.f, 0.f};
         }
         adv(ic, jc);

@@ -35,10 +35,27 @@ static T* dalloc(size_t n, float fill = 0.f) {
 
 static const int SEQ_PER_LAYER = 16, MAXB = 4096;
 
+// side-branch prefetch: block b reads its share of [p, p + bytes) with default-policy
+// loads (allocating in the Infinity Cache) and folds it into a never-taken store
+__global__ __launch_bounds__(256) void prefetch_kernel(const uint4* __restrict__ p, size_t n16, uint4* sink) {
+    const size_t per = (n16 + gridDim.x - 1) / gridDim.x;
+    const size_t lo = (size_t)blockIdx.x * per, hi = lo + per < n16 ? lo + per : n16;
+    uint32_t acc = 0;
+    for (size_t i = lo + threadIdx.x; i < hi; i += 256 * 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const size_t j = i + 256 * u;
+            if (j < hi) { const uint4 v = p[j]; acc ^= v.x ^ v.w; }
+        }
+    }
+    if (acc == 0x9e3779b9u) sink[blockIdx.x] = make_uint4(acc, 0, 0, 0);
+}
+
 int main(int argc, char** argv) {
     const int L_self = argc > 1 ? atoi(argv[1]) : 527;
     const int tickets = argc > 2 ? atoi(argv[2]) : 0;     // in-launch attention merge
     const int x_split = argc > 3 ? atoi(argv[3]) : 1;     // cross-attention key splits
+    const int pf_blocks = argc > 4 ? atoi(argv[4]) : 0;   // side-branch MALL prefetch of the MLP weights
     hipStream_t st;
     hipStreamCreate(&st);
     const int B = 8, d = 2304, f = 9216, D = 256, Hq = 8, Hkv = 4, G = 2, Lmax = 911, Tx = 64, nl = 4;
@@ -114,9 +131,28 @@ int main(int argc, char** argv) {
         a.dbg_seq = seq;
         if (attention_decode(a, st)) printf("attn launch failed\n");
     };
+    hipStream_t side;
+    hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
+    hipEvent_t evf[8], evj[8];
+    for (int i = 0; i < 8; ++i) {
+        hipEventCreateWithFlags(&evf[i], hipEventDisableTiming);
+        hipEventCreateWithFlags(&evj[i], hipEventDisableTiming);
+    }
+    uint4* sink = dalloc<uint4>(4096);
     auto layer = [&](int l) {
         const LW& w = lw[l];
         const int s = l * SEQ_PER_LAYER;
+        if (pf_blocks > 0) {
+            // fork: the side stream streams this layer's gate/up + down weights into the
+            // Infinity Cache while the attention half of the layer runs
+            hipEventRecord(evf[l], st);
+            hipStreamWaitEvent(side, evf[l], 0);
+            hipLaunchKernelGGL(prefetch_kernel, dim3(pf_blocks), dim3(256), 0, side, (const uint4*)w.gu,
+                               (size_t)ng(2 * f) * 16 * d * 2 / 16, sink);
+            hipLaunchKernelGGL(prefetch_kernel, dim3(pf_blocks), dim3(256), 0, side, (const uint4*)w.down,
+                               (size_t)ng(d) * 16 * f * 2 / 16, sink);
+            hipEventRecord(evj[l], side);
+        }
         gemm(xn, d, w.qkv, qkv, d, 2, part, qkv, EPI_F32, s + 0);
         attn(false, w, s + 1);
         gemm(att, qdim, w.o, d, qdim, 4, part, d, EPI_F32, s + 2);
@@ -128,6 +164,7 @@ int main(int argc, char** argv) {
         gemm(xn, d, w.gu, 2 * f, d, 1, act, f, EPI_GEGLU, s + 8);
         gemm(act, f, w.down, d, f, 8, part, d, EPI_F32, s + 9);
         norm(8, w, s + 10);
+        if (pf_blocks > 0) hipStreamWaitEvent(st, evj[l], 0);   // join before the next layer
     };
     hipGraph_t g;
     hipGraphExec_t ge;
@@ -147,6 +184,7 @@ int main(int argc, char** argv) {
     hipEventSynchronize(e1);
     float ms = 0.f;
     hipEventElapsedTime(&ms, e0, e1);
+    printf("prefetch blocks %d, ", pf_blocks);
     printf("L_self %d tickets %d x_split %d: %.1f us per layer (graph of %d layers, event-timed)\n", L_self, tickets,
            x_split, ms * 1000.f / (reps * nl), nl);
     for (auto* p : {tg, tn, ta}) hipMemsetAsync(p, 0, words * 8, st);
