@@ -200,7 +200,9 @@ int t5g_copy_logits(t5g_engine* e, void* dst_dev, int32_t B, void* stream);
 /* --- single-op entry points (parity tests, kernel benchmarks) ------------------ */
 /* One sampler step on caller logits (bf16 [B][ld]) using the engine's sampler state. */
 int t5g_sample_only(t5g_engine* e, int32_t B, const void* logits_dev, int32_t ld, void* stream);
-/* Y = X . W^T on a packed W; epi: 0 bf16, 1 +bias bf16, 2 +bias GELU(erf) bf16, 3 GeGLU(tanh), 4 fp32 slabs */
+/* Y = X . W^T on a packed W; epi: 0 bf16, 1 +bias bf16, 2 +bias GELU(erf) bf16, 3 GeGLU(tanh), 4 fp32 slabs;
+ * epi | T5G_GEMM_PREFILL selects the many-token (encoder / prefill) kernel the engine uses for those phases */
+#define T5G_GEMM_PREFILL 0x100
 int t5g_gemm(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K, int32_t splits,
              const void* bias_dev, void* Y_dev, int32_t ldy, int32_t epi, void* stream);
 /* Time `iters` launches of one GEMM shape with hipEvents on `stream`; launch i uses packed

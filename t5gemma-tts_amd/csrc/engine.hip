@@ -240,9 +240,10 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
 
 // ---------------------------------------------------------------------------
 static int gemm(const bf16_t* X, int ldx, int M, const void* W, int N, int K, int splits, const void* bias,
-                void* Y, int ldy, int epi, hipStream_t st) {
+                void* Y, int ldy, int epi, hipStream_t st, bool prefill = false) {
     GemmArgs a;
     memset(&a, 0, sizeof(a));
+    a.prefill = prefill ? 1 : 0;
     a.X = X;
     a.ldx = ldx;
     a.M = M;
@@ -323,7 +324,7 @@ extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t*
         n.resid_out = e->h;
         n.normed_out = e->xn;
         RC(resid_norm(n, st));
-        RC(gemm(e->xn, d, ntok, L.qkv, e->qkv_dim, d, 1, nullptr, e->qkv, e->qkv_dim, EPI_BF16, st));
+        RC(gemm(e->xn, d, ntok, L.qkv, e->qkv_dim, d, 1, nullptr, e->qkv, e->qkv_dim, EPI_BF16, st, true));
         RopeArgs r;
         memset(&r, 0, sizeof(r));
         r.X = e->qkv;
@@ -347,7 +348,7 @@ extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t*
         RC(rope_store(r, st));
         RC(attn_packed(e, ntok, e->q, tok_row, tok_t, e->enc_k, e->enc_v, c.max_text, e->enc_len, 0,
                        c.enc_sliding[l] ? c.sliding_window : 0, e->att, st));
-        RC(gemm(e->att, e->q_dim, ntok, L.o, d, e->q_dim, 1, nullptr, e->tmp, d, EPI_BF16, st));
+        RC(gemm(e->att, e->q_dim, ntok, L.o, d, e->q_dim, 1, nullptr, e->tmp, d, EPI_BF16, st, true));
         n = norm_args(ntok, d, c.rms_eps);
         n.delta = e->tmp;
         n.post_w = (const bf16_t*)L.norms[1];
@@ -356,8 +357,8 @@ extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t*
         n.resid_out = e->h;
         n.normed_out = e->xn;
         RC(resid_norm(n, st));
-        RC(gemm(e->xn, d, ntok, L.gate_up, 2 * f, d, 1, nullptr, e->act, f, EPI_GEGLU, st));
-        RC(gemm(e->act, f, ntok, L.down, d, f, 1, nullptr, e->tmp, d, EPI_BF16, st));
+        RC(gemm(e->xn, d, ntok, L.gate_up, 2 * f, d, 1, nullptr, e->act, f, EPI_GEGLU, st, true));
+        RC(gemm(e->act, f, ntok, L.down, d, f, 1, nullptr, e->tmp, d, EPI_BF16, st, true));
     }
     // final: h + post_ff(down) -> encoder norm -> memory
     NormArgs n = norm_args(ntok, d, c.rms_eps);
@@ -371,7 +372,7 @@ extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t*
     // cross-attention K/V of every decoder layer from memory (PM-RoPE on K)
     for (int l = 0; l < c.n_dec_layers; ++l) {
         RC(gemm(e->mem, d, ntok, e->dec[l].cross_kv, 2 * e->kv_dim, d, 1, nullptr, e->qkv, 2 * e->kv_dim,
-                EPI_BF16, st));
+                EPI_BF16, st, true));
         RopeArgs r;
         memset(&r, 0, sizeof(r));
         r.X = e->qkv;
@@ -431,11 +432,11 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         RopeArgs r;
         memset(&r, 0, sizeof(r));
         if (s_qkv > 1) {
-            RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, s_qkv, nullptr, e->part, e->qkv_dim, EPI_F32, st));
+            RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, s_qkv, nullptr, e->part, e->qkv_dim, EPI_F32, st, !decode));
             r.Xpart = e->part;
             r.nsplit = s_qkv;
         } else {
-            RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, 1, nullptr, e->qkv, e->qkv_dim, EPI_BF16, st));
+            RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, 1, nullptr, e->qkv, e->qkv_dim, EPI_BF16, st, !decode));
             r.X = e->qkv;
         }
         r.ldx = e->qkv_dim;
@@ -519,7 +520,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             }
         }
         RC(gemm(att, e->q_dim, M, L.o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
-                s_o > 1 ? EPI_F32 : EPI_BF16, st));
+                s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode));
         {
             NormArgs n = norm_args(M, d, c.rms_eps);
             if (s_o > 1) {
@@ -539,11 +540,11 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         // --- PM cross attention
         memset(&r, 0, sizeof(r));
         if (s_cq > 1) {
-            RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, s_cq, nullptr, e->part, e->q_dim, EPI_F32, st));
+            RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, s_cq, nullptr, e->part, e->q_dim, EPI_F32, st, !decode));
             r.Xpart = e->part;
             r.nsplit = s_cq;
         } else {
-            RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, 1, nullptr, q, e->q_dim, EPI_BF16, st));
+            RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, 1, nullptr, q, e->q_dim, EPI_BF16, st, !decode));
             r.X = q;
         }
         r.ldx = e->q_dim;
@@ -602,7 +603,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             }
         }
         RC(gemm(att, e->q_dim, M, L.cross_o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
-                s_o > 1 ? EPI_F32 : EPI_BF16, st));
+                s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode));
         {
             NormArgs n = norm_args(M, d, c.rms_eps);
             if (s_o > 1) {
@@ -620,9 +621,9 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             RC(resid_norm(n, st));
         }
         // --- GeGLU MLP
-        RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st));
+        RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st, !decode));
         RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, s_down > 1 ? (void*)e->part : (void*)tmp, d,
-                s_down > 1 ? EPI_F32 : EPI_BF16, st));
+                s_down > 1 ? EPI_F32 : EPI_BF16, st, !decode));
         {
             NormArgs n = norm_args(M, d, c.rms_eps);
             if (s_down > 1) {
@@ -1059,7 +1060,8 @@ extern "C" int t5g_sample_only(t5g_engine* e, int32_t B, const void* logits, int
 extern "C" int t5g_gemm(const void* X, int32_t ldx, int32_t M, const void* Wp, int32_t N, int32_t K, int32_t splits,
                         const void* bias, void* Y, int32_t ldy, int32_t epi, void* stream) {
     if (!X || !Wp || !Y || M <= 0 || N <= 0 || K % 32) return T5G_EINVAL;
-    RC(gemm((const bf16_t*)X, ldx, M, Wp, N, K, splits, bias, Y, ldy, epi, (hipStream_t)stream));
+    const bool prefill = (epi & T5G_GEMM_PREFILL) != 0;
+    RC(gemm((const bf16_t*)X, ldx, M, Wp, N, K, splits, bias, Y, ldy, epi & 0xff, (hipStream_t)stream, prefill));
     return T5G_OK;
 }
 
@@ -1073,10 +1075,12 @@ extern "C" int t5g_time_gemm(const void* X, int32_t ldx, int32_t M, const void* 
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    RC(gemm((const bf16_t*)X, ldx, M, Wp_list[0], N, K, splits, nullptr, Y, ldy, epi, st));  // warm
+    const bool pf = (epi & T5G_GEMM_PREFILL) != 0;
+    epi &= 0xff;
+    RC(gemm((const bf16_t*)X, ldx, M, Wp_list[0], N, K, splits, nullptr, Y, ldy, epi, st, pf));  // warm
     HIPCHK(hipEventRecord(e0, st));
     for (int i = 0; i < iters; ++i)
-        RC(gemm((const bf16_t*)X, ldx, M, Wp_list[i % n_w], N, K, splits, nullptr, Y, ldy, epi, st));
+        RC(gemm((const bf16_t*)X, ldx, M, Wp_list[i % n_w], N, K, splits, nullptr, Y, ldy, epi, st, pf));
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;

@@ -327,6 +327,132 @@ static int launch_epi(const GemmArgs& a, int epi, int mblocks, hipStream_t st) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Prefill / encoder GEMM (many tokens: the encoder's B*T_x rows, the decoder prefill's
+// B*(T_p+1) rows). Block = 4 waves in a 2 x 2 arrangement over a 128-output x 128-token
+// tile; each wave owns 4 row groups (64 outputs) x 4 token tiles (64 tokens) = 16 MFMA
+// accumulators, so every 1 KiB weight fragment and every 1 KiB activation fragment a wave
+// loads feeds 4 MFMAs (the decode kernel's 1:1 ratio made the old prefill path 7 % of
+// the MFMA peak). Weight fragments come straight from the P16 layout (A operand lane
+// order), activation fragments straight from row-major X (B operand: lane l reads row
+// l&15, k 8*(l>>4)..+7); the two waves sharing a row set (or a token set) hit each
+// other's lines in L1. Next k-step's fragments are in flight while this one multiplies.
+// Accumulation is one MFMA chain in k order per output: deterministic, and a token's
+// result does not depend on the other tokens of the launch (batch-invariant).
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_pf_kernel(GemmArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int g0 = blockIdx.x * 8 + wr * 4;                 // first row group of this wave
+    const int mb = blockIdx.y * 128 + wc * 64;              // first token of this wave
+    const int KB = a.KB;
+    const __amdgpu_buffer_rsrc_t wrs = frag_rsrc(a.W, (uint32_t)a.NG * (uint32_t)KB * 1024u);
+    const __amdgpu_buffer_rsrc_t xrs = frag_rsrc(a.X, (uint32_t)a.M * (uint32_t)a.ldx * 2u);
+    const int xk = 8 * (lane >> 4);
+    int xrow[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) xrow[mt] = (mb + mt * 16 + (lane & 15)) * a.ldx;   // rows >= M: out of range
+    auto load = [&](bf16x8_s(&w)[4], bf16x8_s(&x)[4], int kb) __attribute__((always_inline)) {
+        const bool ok = kb < KB;
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+            w[rg] = __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     wrs, ok ? (((g0 + rg) * KB + kb) * 64 + lane) * 16 : (int)0xfffffff0u, 0, 0));
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+            x[mt] = __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     xrs, ok ? (xrow[mt] + kb * 32 + xk) * 2 : (int)0xfffffff0u, 0, 0));
+    };
+    // two accumulator chains (even / odd k-steps) summed at the end: half-length MFMA
+    // chains (K = 9216: 144 instead of 288), so the fp32 accumulation error stays at the
+    // level of the sliced decode kernel
+    f32x4 acc[4][4], acc2[4][4];
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[rg][mt] = acc2[rg][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    auto mma = [&](const bf16x8_s(&w)[4], const bf16x8_s(&x)[4], f32x4(&c)[4][4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) c[rg][mt] = mfma16(w[rg], x[mt], c[rg][mt]);
+    };
+    bf16x8_s wa[4], xa[4], wb[4], xb[4];
+    load(wa, xa, 0);
+    for (int kb = 0; kb < KB; kb += 2) {
+        load(wb, xb, kb + 1);
+        mma(wa, xa, acc);
+        load(wa, xa, kb + 2);
+        mma(wb, xb, acc2);
+    }
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[rg][mt] += acc2[rg][mt];
+    // epilogue: lane l holds outputs 4*(l>>4)..+3 of each row group for token l&15
+    constexpr bool GLU = EPI == EPI_GEGLU;
+    const int n_out = GLU ? a.N / 2 : a.N;
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+        const int g = g0 + rg;
+        if (g >= a.NG) break;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const int m = mb + mt * 16 + (lane & 15);
+            float v[4];
+            int n0;
+            if constexpr (GLU) {
+                // 8 gate rows then the same 8 features' up rows: the up sums sit 32 lanes up
+                f32x4 up;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) up[r] = __shfl_down(acc[rg][mt][r], 32, 64);
+                if (lane >= 32) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_tanh(rbf(acc[rg][mt][r]))) * rbf(up[r]);
+                n0 = g * 8 + 4 * (lane >> 4);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = acc[rg][mt][r];
+                n0 = g * 16 + 4 * (lane >> 4);
+            }
+            if (m >= a.M) continue;
+            bf16_t o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float x = v[r];
+                if constexpr (EPI == EPI_BIAS_BF16 || EPI == EPI_BIAS_GELU) {
+                    if (n0 + r < n_out) x = x + bf2f(a.bias[n0 + r]);
+                }
+                if constexpr (EPI == EPI_BIAS_GELU) x = gelu_erf(rbf(x));
+                o[r] = f2bf(x);
+            }
+            bf16_t* y = (bf16_t*)a.Y + (long)m * a.ldy;
+            if (n0 + 3 < n_out && (a.ldy & 3) == 0) {
+                uint2 w2;
+                w2.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+                w2.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+                *(uint2*)(y + n0) = w2;
+            } else {
+                for (int r = 0; r < 4; ++r)
+                    if (n0 + r < n_out) y[n0 + r] = o[r];
+            }
+        }
+    }
+}
+
+static int gemm_prefill(const GemmArgs& a, int epi, hipStream_t st) {
+    if ((long)a.M * a.ldx * 2 >= 0x7fffffffL || (long)a.NG * a.KB * 1024 >= 0x7fffffffL) return -1;
+    const dim3 grid((unsigned)((a.NG + 7) / 8), (unsigned)((a.M + 127) / 128));
+    switch (epi) {
+        case EPI_BF16: hipLaunchKernelGGL(gemm_pf_kernel<EPI_BF16>, grid, dim3(256), 0, st, a); break;
+        case EPI_BIAS_BF16: hipLaunchKernelGGL(gemm_pf_kernel<EPI_BIAS_BF16>, grid, dim3(256), 0, st, a); break;
+        case EPI_BIAS_GELU: hipLaunchKernelGGL(gemm_pf_kernel<EPI_BIAS_GELU>, grid, dim3(256), 0, st, a); break;
+        case EPI_GEGLU: hipLaunchKernelGGL(gemm_pf_kernel<EPI_GEGLU>, grid, dim3(256), 0, st, a); break;
+        default: return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // Dispatch: decode-shaped (M <= 64) streams weights with K split over the
 // block's 4 waves (GEGLU: 2 waves per gate/up group); larger M uses 4 row groups
 // per block sharing X fragments.
@@ -336,6 +462,8 @@ int gemm_p16(const GemmArgs& a_in, int epi, hipStream_t st) {
     if (a.NG % 4 != 0 || a.splits < 1) return -1;
     if (epi == EPI_GEGLU && a.splits != 1) return -1;
     if (epi != EPI_F32 && a.splits != 1) return -1;
+    // many-token phases (encoder, decoder prefill): the register-tiled MFMA kernel
+    if (a.prefill && epi != EPI_F32) return gemm_prefill(a, epi, st);
     int rc;
     if (a.M <= 16) {
         rc = launch_epi<1, false>(a, epi, 1, st);

@@ -21,6 +21,7 @@ struct GemmArgs {
     void* Y;          // bf16 [M][ldy] or f32 [splits][M][ldy]
     int ldy;
     int dbg_seq;      // diagnostic timeline slot (T5G_DBG_TS builds only)
+    int prefill;      // 1: many-token phase (encoder / prefill) -> register-tiled MFMA kernel
 };
 int pack_p16(const bf16_t* src, int N, int K, long ld, bf16_t* dst, int NGpad, hipStream_t st);
 int gemm_p16(const GemmArgs& a, int epi, hipStream_t st);
