@@ -65,7 +65,7 @@ typedef struct {
 typedef struct {
     const void* qkv;       /* packed [q_dim + 2 kv_dim][hidden]: q_proj | k_proj | v_proj rows */
     const void* o;         /* packed [hidden][q_dim] */
-    const void* gate_up;   /* packed [2 inter][hidden]: 16-row groups gate,up,gate,up,... */
+    const void* gate_up;   /* packed [2 inter][hidden]: 16-row groups of 8 gate + the same 8 up rows */
     const void* down;      /* packed [hidden][inter] */
     const void* cross_q;   /* decoder only: packed [q_dim][hidden] */
     const void* cross_kv;  /* decoder only: packed [2 kv_dim][hidden]: k_proj | v_proj */

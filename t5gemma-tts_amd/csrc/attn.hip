@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 // ticket, CDNA guide G16), so no combine launch.
 template <int D, int G>
 __device__ __forceinline__ void merge_splits(const AttnArgs& a, const float* base, int qi, int kvh, float* wz,
-                                             float* Linv) {
+                                             float* Linv, int q0 = 0, int nq = G * D / 4) {
     constexpr int ZMAX = 16;  // splits held in registers; more are streamed
     const int S = a.nsplit;
     // Slabs are read with sc1 loads (L1 bypass): in the in-launch merge they were
@@ -297,10 +297,12 @@ __device__ __forceinline__ void merge_splits(const AttnArgs& a, const float* bas
     auto ld1 = [&](int off) __attribute__((always_inline)) {
         return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off * 4, 0, 16));
     };
-    // every thread owns <= 1 (g, d4) quad when G*D/4 <= blockDim (D = 256, G = 2: 128 quads)
+    // thread idx owns (g, d4) quad q0 + idx of this block's nq quads (all G*D/4 of them in
+    // the in-launch merge; a slice of them per combine block)
     const int idx = threadIdx.x;
-    const bool own = idx < G * D / 4;
-    const int g = own ? idx / (D / 4) : 0, d4 = own ? idx % (D / 4) : 0;
+    const bool own = idx < nq;
+    const int quad = q0 + (own ? idx : 0);
+    const int g = quad / (D / 4), d4 = quad % (D / 4);
     f32x4 pv[ZMAX];
 #pragma unroll
     for (int z = 0; z < ZMAX; ++z)
@@ -642,14 +644,22 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
 
 // merge of the key-split partials (used when no ticket counters are supplied):
 // O = sum_z e^(m_z - M) o_z / sum_z e^(m_z - M) l_z
+// Each (row, kv head) is merged by CZ blocks of 64*G threads, one slice of 32 (g, d4) quads
+// each: a block reads 1/CZ of the slabs, so the merge is spread over 4x the CUs (a single
+// block per (row, kv head) was per-CU-bandwidth bound: 31 KB of slabs at 15 splits).
 template <int D, int G>
-__global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a) {
+constexpr int combine_cz() { return (G * D / 4 + 31) / 32; }
+
+template <int D, int G>
+__global__ __launch_bounds__(64 * G) void attn_combine_kernel(AttnArgs a) {
     __shared__ float wz[G * 64];
     __shared__ float Linv[G];
     const int qi = blockIdx.x, kvh = blockIdx.y;
     T5G_TS(3);
     const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2));
-    merge_splits<D, G>(a, base, qi, kvh, wz, Linv);
+    constexpr int QPB = (G * D / 4 + combine_cz<D, G>() - 1) / combine_cz<D, G>();
+    const int q0 = (int)blockIdx.z * QPB;
+    merge_splits<D, G>(a, base, qi, kvh, wz, Linv, q0, min(QPB, G * D / 4 - q0));
     T5G_TS(6);
 }
 
@@ -658,7 +668,8 @@ static int launch_decode(const AttnArgs& a, hipStream_t st) {
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
     hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, a);
     if (a.nsplit > 1 && !a.counters)
-        hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv), dim3(256), 0,
+        hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, combine_cz<D, G>()),
+                           dim3(64 * G), 0,
                            st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -685,7 +696,8 @@ static int launch_attn(const AttnArgs& a, hipStream_t st) {
     else
         hipLaunchKernelGGL((attn_kernel<D, G, false>), grid, dim3(256), shm, st, a);
     if (a.nsplit > 1)
-        hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv), dim3(256), 0,
+        hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, combine_cz<D, G>()),
+                           dim3(64 * G), 0,
                            st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -282,6 +282,16 @@ int pack_p16(const bf16_t* src, int N, int K, long ld, bf16_t* dst, int NGpad, h
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// shortest per-wave k-stream that stages X in LDS (T5G_XLDS_MIN, default 16). Read once.
+static int xlds_min() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("T5G_XLDS_MIN");
+        v = e ? atoi(e) : 16;
+    }
+    return v;
+}
+
 template <int MT, int WPG, int KS, int EPI>
 static void launch_t(const GemmArgs& a, int mblocks, hipStream_t st) {
     constexpr int RG = 4 / WPG;
@@ -289,7 +299,7 @@ static void launch_t(const GemmArgs& a, int mblocks, hipStream_t st) {
     const int per = (a.KB + a.splits - 1) / a.splits;
     // decode with a long K stream per wave: stage the X rows in LDS once per block (the
     // staging barrier costs ~1 us, repaid only when each wave streams >= 16 fragments)
-    if (WPG == KS && MT == 1 && per / KS >= 16 && min(16, a.M) * per * 4 <= 256 * 18) {
+    if (WPG == KS && MT == 1 && per / KS >= xlds_min() && min(16, a.M) * per * 4 <= 256 * 18) {
         const size_t shm = (size_t)min(16, a.M) * (per * 32 + 8) * sizeof(bf16_t);
         hipLaunchKernelGGL((gemm_p16_kernel<MT, WPG, KS, EPI, true>), grid, dim3(256), shm, st, a);
     } else {

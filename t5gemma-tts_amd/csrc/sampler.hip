@@ -30,6 +30,8 @@
 
 namespace t5g {
 
+T5G_TS_UNIT(sampler)
+
 constexpr int SN = 1024;
 constexpr int NW = SN / 64;
 constexpr int SPER = 66;                // V <= SN * SPER = 67584
@@ -558,6 +560,15 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
 // Rows the fast path cannot take (min_p, top-k off or > FS_KMAX, a slice with more
 // than FS_CAP candidates, more than FS_SMAX survivors) are flagged in fs_slow and
 // finished by the single-block kernel launched right after.
+// sc1 (write-through store / L1-bypassing load) accessors for the fast path's cross-block
+// candidate hand-off (relaxed agent-scope atomics lower to global_store/load ... sc1)
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int FT = 256;
 __device__ __forceinline__ bool lane_ok(int t) { return t < FS_NB; }
 constexpr int FEPT = 24;   // V <= FS_NB * FT * FEPT = 98304
@@ -596,6 +607,16 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
     __shared__ int is_last;
 
     const int sl = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, wid = tid >> 6;
+    T5G_TS(0);
+    // the slice's logits depend on nothing: request them first (clamped addresses, no
+    // branch), so the row's state / parameters / silence list arrive meanwhile
+    const int V = a.V;
+    const int SL = (V + FS_NB - 1) / FS_NB;
+    const int i0 = sl * SL, i1 = min(V, i0 + SL);
+    const bf16_t* lg = a.logits + (long)b * a.ldl;
+    bf16_t raw[FEPT];
+#pragma unroll
+    for (int j = 0; j < FEPT; ++j) raw[j] = lg[max(0, min(i0 + tid + FT * j, i1 - 1))];
     SamplerState st = a.state[b];
     if (st.done) return;
     const SamplerRow pr = a.rows[b];
@@ -606,11 +627,7 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
         if (sl == 0 && tid == 0) a.fs_slow[b] = 1;
         return;
     }
-    const int V = a.V;
     const int k = min(kk, V);
-    const int SL = (V + FS_NB - 1) / FS_NB;
-    const int i0 = sl * SL, i1 = min(V, i0 + SL);
-    const bf16_t* lg = a.logits + (long)b * a.ldl;
     // ---- 1-3. edits, argmax of the edited logits, temperature (as sampler_kernel)
     const int eff_len = max(0, st.current_length - st.prompt_offset);
     bool in_sil_prev = false;
@@ -625,7 +642,7 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
         const int i = i0 + tid + FT * j;
         x[j] = -INFINITY;
         if (i < i1) {
-            float v = bf2f(lg[i]);
+            float v = bf2f(raw[j]);
             if (i == a.eos) {
                 if (eff_len == 0) v = rbf(-1e9f);
                 if (st.cur_num_gen <= a.eos_guard) v = rbf(-10000.0f);
@@ -638,6 +655,7 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
         }
     }
     const float amv = block_argmax_v(bv, bi, redv, redi);
+    T5G_TS(1);
     // ---- 5a. local top-k candidates (k-th largest of the slice, ties kept)
     float thr = -INFINITY;
     if (i1 - i0 > k) {
@@ -672,32 +690,39 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
         if (i < i1 && x[j] >= thr) {
             const int p = atomicAdd(&sh_int[4], 1);
             if (p < FS_CAP) {
-                gv[p] = x[j];
-                gi[p] = i;
+                st_sc1(gv + p, x[j]);
+                st_sc1(gi + p, i);
             }
         }
     }
     __syncthreads();
     if (tid == 0) {
-        a.fs_cnt[b * FS_NB + sl] = sh_int[4] > FS_CAP ? -1 : sh_int[4];
-        a.fs_amv[b * FS_NB + sl] = amv;
-        a.fs_ami[b * FS_NB + sl] = bi;
+        st_sc1(a.fs_cnt + b * FS_NB + sl, sh_int[4] > FS_CAP ? -1 : sh_int[4]);
+        st_sc1(a.fs_amv + b * FS_NB + sl, amv);
+        st_sc1(a.fs_ami + b * FS_NB + sl, bi);
     }
-    // ---- arrival ticket: the last slice block of the row finishes it
-    __threadfence();
+    T5G_TS(2);
+    // ---- arrival ticket: the last slice block of the row finishes it. CDNA guide G16
+    // valid form row 1: the candidates went out as sc1 (write-through) stores, every
+    // storing wave drains them, one lane adds to the row's ticket, the block whose add
+    // returns FS_NB-1 reads them back with sc1 loads -- no fences (the two all-thread
+    // __threadfence()s this replaces cost ~8 us per step).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) is_last = atomicAdd(&a.fs_ticket[b], 1u) == (unsigned)(FS_NB - 1);
+    if (tid == 0)
+        is_last = __hip_atomic_fetch_add(&a.fs_ticket[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  (unsigned)(FS_NB - 1);
     __syncthreads();
     if (!is_last) return;
-    __threadfence();
+    T5G_TS(3);
     // slice counts / argmaxes: one load per lane of wave 0, scan + argmax in registers
     if (wid == 0) {
         int c = 0, mi = 0x7fffffff;
         float mv = -INFINITY;
         if (lane_ok(tid)) {
-            c = a.fs_cnt[b * FS_NB + tid];
-            mv = a.fs_amv[b * FS_NB + tid];
-            mi = a.fs_ami[b * FS_NB + tid];
+            c = ld_sc1(a.fs_cnt + b * FS_NB + tid);
+            mv = ld_sc1(a.fs_amv + b * FS_NB + tid);
+            mi = ld_sc1(a.fs_ami + b * FS_NB + tid);
         }
         const unsigned long long badm = __ballot(c < 0);
         int inc = max(c, 0);
@@ -732,10 +757,11 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
 #pragma unroll
         for (int t = 1; t < FS_NB; ++t) sidx += (q >= soff[t]);
         const long src = ((long)b * FS_NB + sidx) * FS_CAP + (q - soff[sidx]);
-        cv[q] = a.fs_val[src];
-        ci[q] = a.fs_idx[src];
+        cv[q] = ld_sc1(a.fs_val + src);
+        ci[q] = ld_sc1(a.fs_idx + src);
     }
     __syncthreads();
+    T5G_TS(4);
     // ---- 5b. global k-th largest over the merged candidates
     float gthr = -INFINITY;
     if (n > k) {
@@ -783,37 +809,51 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
     }
     __syncthreads();
     const float m = cv[0];
+    T5G_TS(5);
     // ---- 6. top-p walk over distinct values (:118-129)
     int nkeep = ns, ambiguous = 0;
     if (pr.top_p < 1.0f) {
         float ls = 0.f;
         if (tid < ns && cv[tid] > -INFINITY) ls = expf(cv[tid] - m);
         const float inv = 1.0f / block_sum(ls, redv);
-        if (tid == 0) {
+        if (wid == 0) {
+            // wave 0: every survivor's bf16 probability in parallel (lane q%64, slot q/64),
+            // then the cumsum walk in survivor order with register reads (v_readlane,
+            // uniform index): sequential fp32 accumulation, each prefix rounded to bf16,
+            // exactly the reference's order; a cut inside a tie group is ambiguous
+            constexpr int NS = FS_SMAX / 64;
+            float vr[NS], pr_[NS];
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2) {
+                const int q = tid + 64 * s2;
+                vr[s2] = q < ns ? cv[q] : -INFINITY;
+                pr_[s2] = vr[s2] > -INFINITY ? rbf(expf(vr[s2] - m) * inv) : 0.f;
+            }
+            auto lane_get = [&](const float(&r)[NS], int q) __attribute__((always_inline)) {
+                float out = -INFINITY;
+#pragma unroll
+                for (int s2 = 0; s2 < NS; ++s2)
+                    if ((q >> 6) == s2)
+                        out = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r[s2]), q & 63));
+                return out;
+            };
             const float pthr = rbf(pr.top_p);
             float acc = 0.f;
             int keep_n = ns, amb = 0;
-            for (int q = 0; q < ns;) {
-                const float v = cv[q];
-                int c = 1;
-                while (q + c < ns && cv[q + c] == v) ++c;
+            for (int q = 0; q < ns; ++q) {
+                const float v = lane_get(vr, q);
                 if (v == -INFINITY) break;
-                const float pv = rbf(expf(v - m) * inv);
-                bool cut = false;
-                for (int r = 0; r < c; ++r) {
-                    acc += pv;
-                    if (rbf(acc) > pthr) {
-                        keep_n = q + r + 1;
-                        amb = (r + 1 < c);
-                        cut = true;
-                        break;
-                    }
+                acc += lane_get(pr_, q);
+                if (rbf(acc) > pthr) {
+                    keep_n = q + 1;
+                    amb = q + 1 < ns && lane_get(vr, q + 1) == v;
+                    break;
                 }
-                if (cut) break;
-                q += c;
             }
-            sh_int[0] = keep_n;
-            sh_int[1] = amb;
+            if (tid == 0) {
+                sh_int[0] = keep_n;
+                sh_int[1] = amb;
+            }
         }
         __syncthreads();
         nkeep = sh_int[0];
@@ -839,6 +879,7 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
         a.fs_slow[b] = 0;
         finish_row(a, pr, st, b, token, amax, ambiguous, eff_len);
     }
+    T5G_TS(6);
 }
 
 size_t sampler_fast_ws_bytes(int B) {

@@ -196,6 +196,7 @@ struct SamplerArgs {
     int* fs_ami;              // [B][FS_NB] slice argmax index
     unsigned* fs_ticket;      // [B] arrival counters (reset by the last block)
     int* fs_slow;             // [B] 1: row left to the single-block kernel this step
+    int dbg_seq;             // diagnostic timeline slot (T5G_DBG_TS builds only)
 };
 constexpr int FS_NB = 16;     // slices (blocks) per row
 constexpr int FS_CAP = 128;   // candidates per slice
