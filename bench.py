@@ -174,23 +174,21 @@ def main():
         d, f = cfg.backbone.hidden_size, cfg.backbone.intermediate_size
         # rotate over every decoder layer's gate/up weights (2.2 GB >> 256 MiB Infinity
         # Cache) so each launch streams its weights from HBM, as inside a decode step
-        wl = (C.c_void_p * len(eng._dec))(*[lw.gate_up for lw in eng._dec])
         X = torch.randn(B, d, device=dev).to(torch.bfloat16)
         Y = torch.empty(B, f, dtype=torch.bfloat16, device=dev)
-        us = C.c_float()
         st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        _lib.check(L.t5g_time_gemm(C.c_void_p(X.data_ptr()), d, B, wl, len(eng._dec), 2 * f, d, 1,
-                                   C.c_void_p(Y.data_ptr()), f, 3, 208, st, C.byref(us)), "time_gemm")
+        us_gu = _lib.time_gate_up(X.data_ptr(), d, B, [lw.gate_up for lw in eng._dec], 2 * f, d, Y.data_ptr(),
+                                  208, st)
         alg_bytes = 2 * f * d * 2 + B * d * 2 + B * f * 2
-        achieved = alg_bytes / (us.value * 1e-6) / 1e9
+        achieved = alg_bytes / (us_gu * 1e-6) / 1e9
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_gate_up.json")
         if os.path.exists(pmc):
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(achieved / 8000.0, 4), "traffic": traffic,
-                "kernel": "gemm_p16_kernel<1,2,2,GEGLU,XLDS> (decode gate/up, M=8, 84.9 MB weights)",
-                "avg_us": round(us.value, 2)}
+                "kernel": _lib.GATE_UP_KERNEL,
+                "avg_us": round(us_gu, 2)}
         step_us = C.c_float()
         _lib.check(L.t5g_time_decode_step(eng.h, 20, st, C.byref(step_us)), "time_step")
         roof["decode_step_us"] = round(step_us.value, 1)

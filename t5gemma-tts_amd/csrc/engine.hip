@@ -86,6 +86,9 @@ struct t5g_engine {
     // keys split over T5G_XATTN_SPLIT blocks per (row, kv head). Both off by default:
     // measured on MI355X (tools/micro_timeline.cpp) neither beats the combine launch.
     bool attn_tickets = false;
+    // decode gate/up on gemv_dec (one block per CU, 1152 single-group units dealt
+    // round-robin: 18.3 us vs 19.7 us for the 576-block P16 GEMM); T5G_GU_GEMV=0 reverts
+    bool gu_gemv = true;
     int xsplit = 1;
     int B = 0;            // rows of the current call
     const bf16_t* noise = nullptr;
@@ -224,6 +227,8 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
         e->fused_p16 = fdv && fdv[0] == '2';
         const char* atv = getenv("T5G_ATTN_TICKETS");
         e->attn_tickets = atv && atv[0] == '1';
+        const char* guv = getenv("T5G_GU_GEMV");
+        e->gu_gemv = !(guv && guv[0] == '0');
         const char* xsv = getenv("T5G_XATTN_SPLIT");
         e->xsplit = xsv ? atoi(xsv) : 1;
         const int xmax = (c.max_text + 63) / 64 > 16 ? (c.max_text + 63) / 64 : 16;
@@ -397,6 +402,8 @@ extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t*
 
 // One decoder pass over `M` tokens. Packed mode (tok_row != null): prefill;
 // decode mode: M = B rows, positions/slots/tokens from the sampler buffers.
+static DecGemmArgs dec_args(int M, const void* W, int N, int K, void* Y, int ldy, int nw);
+
 static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row, const int* tok_t, const float* pos,
                         bool decode, hipStream_t st) {
     const t5g_config& c = e->c;
@@ -620,8 +627,16 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             n.normed_out = xn;
             RC(resid_norm(n, st));
         }
-        // --- GeGLU MLP
-        RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st, !decode));
+        // --- GeGLU MLP (decode: the one-block-per-CU GEMV unless T5G_GU_GEMV=0)
+        if (decode && e->gu_gemv && M <= 16) {
+            DecGemmArgs g = dec_args(M, L.gate_up, 2 * f, d, act, f, 8);
+            g.X = xn;
+            g.ldx = d;
+            g.un = 8;
+            RC(gemv_dec(g, EPI_GEGLU, PRO_LOAD, st));
+        } else {
+            RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st, !decode));
+        }
         RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, s_down > 1 ? (void*)e->part : (void*)tmp, d,
                 s_down > 1 ? EPI_F32 : EPI_BF16, st, !decode));
         {

@@ -430,8 +430,10 @@ static int launch_nw(const DecGemmArgs& a, size_t shm, hipStream_t st) {
     if constexpr (!gd_allowed<EPI, PRO>()) {
         return -3;
     } else if constexpr (EPI == EPI_GEGLU) {
-        if (a.nw == 4) return launch_rows<4, 2, EPI, PRO>(a, shm, st);
-        if (a.nw == 8) return launch_rows<8, 2, EPI, PRO>(a, shm, st);
+        // one row group (8 gate + the same 8 up rows) per unit: 1152 units at 2b-2b
+        // balance over the CUs (4.5 per block) far better than 576 two-group units
+        if (a.nw == 4) return launch_rows<4, 1, EPI, PRO>(a, shm, st);
+        if (a.nw == 8) return launch_rows<8, 1, EPI, PRO>(a, shm, st);
         return -1;
     } else {
         if (a.nw == 4) return launch_rows<4, 1, EPI, PRO>(a, shm, st);
@@ -458,7 +460,7 @@ int gemv_dec(const DecGemmArgs& a, int epi, int pro, hipStream_t st) {
     if (a.splits < 1 || a.splits > 64 || (a.splits > 1 && (epi != EPI_F32 || pro == PRO_NORM || pro == PRO_EMBED)))
         return -1;
     if (a.nw != 4 && a.nw != 8 && a.nw != 16) return -1;
-    const int rg = epi == EPI_GEGLU ? 2 : 1;
+    const int rg = 1;
     if (a.NG % rg) return -1;
     if ((pro == PRO_LOAD || pro == PRO_DIRECT) && (!a.X || a.ldx < a.K || a.ldx % 8)) return -1;
     if (pro == PRO_NORM && (!a.v || !a.h_in || !a.post_w || !a.pre_w)) return -1;

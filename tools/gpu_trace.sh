@@ -1,9 +1,7 @@
-# GPU tests + per-step kernel timelines of the decode graph (default path and the
-# fused-prologue variants). Usage: tools/gpucall.sh tools/gpu_trace.sh 1200
+# Per-step kernel timelines of the decode graph (default path and the fused-prologue P16 variant).
 source tools/gpu_run.sh
 export TMPDIR=/tmp
 rm -rf gpurun_out/prof_*
-run t_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 trace() {  # name, T5G_FUSED_DECODE value
   export T5G_FUSED_DECODE=$2
   run prof_$1 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$1 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
@@ -12,4 +10,3 @@ trace() {  # name, T5G_FUSED_DECODE value
 }
 trace default 0
 trace fusedp16 2
-trace fusedrm 1

@@ -28,14 +28,11 @@ def main():
         packed.append(dst)
         del w
     torch.cuda.synchronize()
-    wl = (C.c_void_p * n_layers)(*[p.data_ptr() for p in packed])
     X = torch.randn(B, d, device=dev).to(torch.bfloat16)
     Y = torch.empty(B, f, dtype=torch.bfloat16, device=dev)
-    us = C.c_float()
-    _lib.check(L.t5g_time_gemm(C.c_void_p(X.data_ptr()), d, B, wl, n_layers, 2 * f, d, 1, C.c_void_p(Y.data_ptr()),
-                               f, 3, 2 * n_layers, st, C.byref(us)), "time_gemm")
+    us = _lib.time_gate_up(X.data_ptr(), d, B, [p.data_ptr() for p in packed], 2 * f, d, Y.data_ptr(), 2 * n_layers, st)
     alg = 2 * f * d * 2 + B * d * 2 + B * f * 2
-    print(f"gate_up avg {us.value:.2f} us/launch, algorithmic {alg} B -> {alg / us.value / 1e3:.1f} GB/s", flush=True)
+    print(f"gate_up avg {us:.2f} us/launch, algorithmic {alg} B -> {alg / us / 1e3:.1f} GB/s", flush=True)
 
 
 if __name__ == "__main__":

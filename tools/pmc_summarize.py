@@ -7,7 +7,7 @@ import json
 import os
 import sys
 
-KERNEL = "gemm_p16_kernel<1, 2, 2, 3, true>"
+KERNEL = "gemv_dec_kernel<8, 1, 3, 0, 1, 1, 8>"
 
 
 def mean_counter(path):
