@@ -30,6 +30,7 @@ extern "C" {
 #define T5G_EUNSUPPORTED (-3)
 #define T5G_ENOMEM (-4)
 #define T5G_ECAPACITY (-5)   /* exceeds engine capacity (max_batch / max_text / max_audio) */
+#define T5G_ESYNC (-6)       /* an in-launch row hand-off poll gave up (decode results invalid) */
 
 #define T5G_MAX_LAYERS 64
 
@@ -172,7 +173,8 @@ int t5g_sampler_setup(t5g_engine* e, int32_t B, const t5g_sampler_row* rows, con
  * one iteration. Asynchronous. */
 int t5g_decode(t5g_engine* e, int32_t n_steps, int32_t use_graph, void* stream);
 
-/* Synchronous readback: state[B] and tokens [B][max_gen] (host buffers). */
+/* Synchronous readback: state[B] and tokens [B][max_gen] (host buffers).
+ * t5g_read_tokens returns T5G_ESYNC if a decode launch's bounded row-flag poll gave up. */
 int t5g_read_state(t5g_engine* e, t5g_sampler_state* state_out, int32_t B, void* stream);
 int t5g_read_tokens(t5g_engine* e, int32_t* tokens_out, int32_t B, void* stream);
 /* Host write of one row's state (parity-mode correction of an ambiguous step). */

@@ -13,7 +13,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("T5G_LIB", os.path.join(_PKG, "lib", "libt5gtts.so"))
 MAX_LAYERS = 64
 
-T5G_ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "EUNSUPPORTED", -4: "ENOMEM", -5: "ECAPACITY"}
+T5G_ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "EUNSUPPORTED", -4: "ENOMEM", -5: "ECAPACITY", -6: "ESYNC"}
 
 
 class T5GError(RuntimeError):

@@ -80,8 +80,11 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
     dst[i + H2] = f2bf(o2);
 }
 
-__global__ void rope_table_kernel(const float* pos, const float* inv_freq, int D, float* tab) {
+__global__ void rope_table_kernel(const float* pos, const float* inv_freq, int D, float* tab, unsigned* epoch) {
     const int r = blockIdx.x, H2 = D / 2;
+    // the decode step's first kernel also advances the step epoch that the PRO_LEAD row
+    // hand-offs of this step publish and poll (gemv.hip): no per-step flag reset
+    if (epoch && r == 0 && threadIdx.x == 0) *epoch = *epoch + 1u == 0u ? 1u : *epoch + 1u;
     for (int i = threadIdx.x; i < H2; i += blockDim.x) {
         const float ang = inv_freq[i] * pos[r];
         tab[(long)r * D + i] = rbf(cosf(ang));
@@ -89,9 +92,10 @@ __global__ void rope_table_kernel(const float* pos, const float* inv_freq, int D
     }
 }
 
-int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st) {
+int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st,
+               unsigned* epoch) {
     if (rows <= 0) return 0;
-    hipLaunchKernelGGL(rope_table_kernel, dim3((unsigned)rows), dim3(128), 0, st, pos, inv_freq, D, tab);
+    hipLaunchKernelGGL(rope_table_kernel, dim3((unsigned)rows), dim3(128), 0, st, pos, inv_freq, D, tab, epoch);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

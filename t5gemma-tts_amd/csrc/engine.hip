@@ -89,6 +89,16 @@ struct t5g_engine {
     // decode gate/up on gemv_dec (one block per CU, 1152 single-group units dealt
     // round-robin: 18.3 us vs 19.7 us for the 576-block P16 GEMM); T5G_GU_GEMV=0 reverts
     bool gu_gemv = true;
+    // decode norms folded into the consuming GEMV (PRO_LEAD: blocks 0..M-1 finish and
+    // publish the rows, the others poll per-row flags): one launch fewer per site.
+    // T5G_LEAD_NORM = site mask (1 next-layer qkv, 2 cross-q, 4 gate/up). Off by default:
+    // measured on MI355X the in-launch hand-off costs what the launch boundary did
+    // (gate/up 23.2 us vs 18.0 + 4.9 norm; all sites 3019 vs 3411 tok/s).
+    int lead_sites = 0;
+    unsigned* lead_flags = nullptr;   // [n_dec_layers][3 sites][16 rows]: last published epoch
+    unsigned* lead_epoch = nullptr;   // step epoch, advanced by the step's rope_table launch
+    unsigned* lead_tmo = nullptr;     // poll give-up word (t5g_engine_status)
+    float* qslab = nullptr;           // [max_batch][qkv_dim] fp32 q|k|v of the lead GEMVs
     int xsplit = 1;
     int B = 0;            // rows of the current call
     const bf16_t* noise = nullptr;
@@ -169,6 +179,10 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     // split-K slabs: decode uses up to 8 splits of [B][max(d, qkv)]
     e->part_elems = (int64_t)8 * B * widest(widest(d, e->qkv_dim), 2 * e->kv_dim);
     rc |= alloc(e, &e->part, e->part_elems);
+    rc |= alloc(e, &e->lead_flags, (int64_t)c.n_dec_layers * 3 * 16);
+    rc |= alloc(e, &e->lead_tmo, 4);
+    rc |= alloc(e, &e->lead_epoch, 4);
+    rc |= alloc(e, &e->qslab, (int64_t)B * widest(e->qkv_dim, d));
     const int G = c.n_heads / c.n_kv_heads;
     const int nsplit_dec = (c.max_audio + 63) / 64;
     // cross-attention key splits: up to max(ceil(max_text / 64), 16) (T5G_XATTN_SPLIT cap)
@@ -229,6 +243,8 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
         e->attn_tickets = atv && atv[0] == '1';
         const char* guv = getenv("T5G_GU_GEMV");
         e->gu_gemv = !(guv && guv[0] == '0');
+        const char* lnv = getenv("T5G_LEAD_NORM");
+        if (lnv) e->lead_sites = atoi(lnv) & 7;
         const char* xsv = getenv("T5G_XATTN_SPLIT");
         e->xsplit = xsv ? atoi(xsv) : 1;
         const int xmax = (c.max_text + 63) / 64 > 16 ? (c.max_text + 63) / 64 : 16;
@@ -420,11 +436,36 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
     // one cos/sin table per step: every layer's q/k rotation uses the same positions
     const float* tab = nullptr;
     if (decode) {
-        RC(rope_table(pos, e->w.inv_freq, M, D, e->rope_tab, st));
+        RC(rope_table(pos, e->w.inv_freq, M, D, e->rope_tab, st, e->lead_epoch));
         tab = e->rope_tab;
     }
+    // PRO_LEAD chain (sdpa decode, M <= 16): the norm after o, cross-o and down (but the
+    // last layer's) runs in the first M blocks of the GEMV that consumes it
+    const bool lead = decode && e->lead_sites && M <= 16 && !(c.softcap > 0.f) && s_qkv > 1 && s_cq > 1 &&
+                      d % 32 == 0 && d <= 4096;
+    auto lead_gemv = [&](const void* W, int N, void* Y, int ldy, int nsplit, const void* post_w, const void* pre_w,
+                         int site, int epi) -> int {
+        DecGemmArgs g = dec_args(M, W, N, d, Y, ldy, 8);
+        g.un = 8;
+        g.X = xn;
+        g.ldx = d;
+        g.part = e->part;
+        g.nsplit_p = nsplit;
+        g.ldp = d;
+        g.h_in = h;
+        g.h_out = h;
+        g.post_w = (const bf16_t*)post_w;
+        g.pre_w = (const bf16_t*)pre_w;
+        g.eps = c.rms_eps;
+        g.flags = e->lead_flags + site * 16;
+        g.tmo = e->lead_tmo;
+        g.epoch = e->lead_epoch;
+        return gemv_dec(g, epi, PRO_LEAD, st);
+    };
     for (int l = 0; l < c.n_dec_layers; ++l) {
         const t5g_layer_weights& L = e->dec[l];
+        const bool lead_qkv = lead && (e->lead_sites & 1) && l > 0;   // layer 0: embedding norm
+        const bool lead_cq = lead && (e->lead_sites & 2), lead_gu = lead && (e->lead_sites & 4);
         if (l == 0) {
             NormArgs n = norm_args(M, d, c.rms_eps);
             n.ids = ids;
@@ -438,7 +479,12 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         // --- self attention
         RopeArgs r;
         memset(&r, 0, sizeof(r));
-        if (s_qkv > 1) {
+        if (lead_qkv) {
+            RC(lead_gemv(L.qkv, e->qkv_dim, e->qslab, e->qkv_dim, s_down, e->dec[l - 1].norms[5], L.norms[0],
+                         3 * l, EPI_F32));
+            r.Xpart = e->qslab;
+            r.nsplit = 1;
+        } else if (s_qkv > 1) {
             RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, s_qkv, nullptr, e->part, e->qkv_dim, EPI_F32, st, !decode));
             r.Xpart = e->part;
             r.nsplit = s_qkv;
@@ -500,8 +546,8 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
                 a.part = e->apart;
                 a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
                 if (s_qkv > 1) {
-                    a.Qpart = e->part;
-                    a.q_nsplit = s_qkv;
+                    a.Qpart = lead_qkv ? e->qslab : e->part;
+                    a.q_nsplit = lead_qkv ? 1 : s_qkv;
                     a.ldqp = e->qkv_dim;
                     a.pos = pos;
                     a.inv_freq = e->w.inv_freq;
@@ -528,7 +574,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         }
         RC(gemm(att, e->q_dim, M, L.o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
                 s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode));
-        {
+        if (!lead_cq) {
             NormArgs n = norm_args(M, d, c.rms_eps);
             if (s_o > 1) {
                 n.part = e->part;
@@ -546,7 +592,11 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         }
         // --- PM cross attention
         memset(&r, 0, sizeof(r));
-        if (s_cq > 1) {
+        if (lead_cq) {
+            RC(lead_gemv(L.cross_q, e->q_dim, e->qslab, e->q_dim, s_o, L.norms[1], L.norms[2], 3 * l + 1, EPI_F32));
+            r.Xpart = e->qslab;
+            r.nsplit = 1;
+        } else if (s_cq > 1) {
             RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, s_cq, nullptr, e->part, e->q_dim, EPI_F32, st, !decode));
             r.Xpart = e->part;
             r.nsplit = s_cq;
@@ -596,8 +646,8 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
                 a.kv_cap = c.max_text;
                 a.part = e->apart;
                 a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
-                a.Qpart = e->part;
-                a.q_nsplit = s_cq;
+                a.Qpart = lead_cq ? e->qslab : e->part;
+                a.q_nsplit = lead_cq ? 1 : s_cq;
                 a.ldqp = e->q_dim;
                 a.pos = pos;
                 a.inv_freq = e->w.inv_freq;
@@ -611,7 +661,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         }
         RC(gemm(att, e->q_dim, M, L.cross_o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
                 s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode));
-        {
+        if (!lead_gu) {
             NormArgs n = norm_args(M, d, c.rms_eps);
             if (s_o > 1) {
                 n.part = e->part;
@@ -628,7 +678,9 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             RC(resid_norm(n, st));
         }
         // --- GeGLU MLP (decode: the one-block-per-CU GEMV unless T5G_GU_GEMV=0)
-        if (decode && e->gu_gemv && M <= 16) {
+        if (lead_gu) {
+            RC(lead_gemv(L.gate_up, 2 * f, act, f, s_o, L.norms[3], L.norms[4], 3 * l + 2, EPI_GEGLU));
+        } else if (decode && e->gu_gemv && M <= 16) {
             DecGemmArgs g = dec_args(M, L.gate_up, 2 * f, d, act, f, 8);
             g.X = xn;
             g.ldx = d;
@@ -639,7 +691,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         }
         RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, s_down > 1 ? (void*)e->part : (void*)tmp, d,
                 s_down > 1 ? EPI_F32 : EPI_BF16, st, !decode));
-        {
+        if (!(lead && (e->lead_sites & 1)) || l == c.n_dec_layers - 1) {
             NormArgs n = norm_args(M, d, c.rms_eps);
             if (s_down > 1) {
                 n.part = e->part;
@@ -1014,8 +1066,10 @@ extern "C" int t5g_read_tokens(t5g_engine* e, int32_t* out, int32_t B, void* str
     if (!e || !out || B <= 0 || B > e->c.max_batch) return T5G_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipMemcpyAsync(out, e->out_tokens, (size_t)B * e->c.max_gen * sizeof(int), hipMemcpyDeviceToHost, st));
+    unsigned tmo = 0;
+    HIPCHK(hipMemcpyAsync(&tmo, e->lead_tmo, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    return T5G_OK;
+    return tmo ? T5G_ESYNC : T5G_OK;
 }
 
 extern "C" int t5g_write_state(t5g_engine* e, const t5g_sampler_state* s, int32_t row, int32_t slot, int32_t token,

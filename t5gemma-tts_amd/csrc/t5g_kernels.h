@@ -31,7 +31,11 @@ int gemm_p16(const GemmArgs& a, int epi, hipStream_t st);
 // sub-block's bf16 output: residual add + the two RMSNorms of PMDecoderLayer
 // (PRO_NORM), or the audio embedding gather (PRO_EMBED). Outputs are whole (no
 // split-K), so the next consumer can run the same prologue on them.
-enum { PRO_LOAD = 0, PRO_NORM = 1, PRO_EMBED = 2, PRO_DIRECT = 3 };
+// PRO_LEAD: blocks 0..M-1 each finish ONE row of the previous sub-block (sum of its
+// fp32 split-K slabs, post-norm, residual add, pre-norm: exactly resid_norm_kernel),
+// publish it (sc1 stores + a per-row flag), and every block stages the rows after
+// polling the M flags -- the separate norm launch disappears from the chain.
+enum { PRO_LOAD = 0, PRO_NORM = 1, PRO_EMBED = 2, PRO_DIRECT = 3, PRO_LEAD = 4 };
 struct DecGemmArgs {
     int M, K;                 // rows (<= 16), reduction length (= X row width)
     const bf16_t* W;          // packed P16
@@ -55,6 +59,13 @@ struct DecGemmArgs {
     int un;                   // fragments in flight per wave (8 / 16), 0 = default
     int max_grid;             // blocks per launch cap, 0 = one per CU
     int splits;               // split-K over blockIdx.y (EPI_F32 slabs [splits][M][ldy]; PRO_LOAD/DIRECT)
+    // PRO_LEAD: the row producer's operands (X above is the normed output it publishes;
+    // h_in/h_out the residual stream, post_w/pre_w the two norms)
+    const float* part;        // fp32 split-K slabs [nsplit_p][M][ldp] of the previous Linear
+    int nsplit_p, ldp;
+    unsigned* flags;          // [M] per-row publish words (hold the last step's epoch)
+    unsigned* tmo;            // set to 1 when a bounded flag poll gives up (never expected)
+    const unsigned* epoch;    // this step's epoch (advanced by rope_table_kernel, never 0)
 };
 int gemv_dec(const DecGemmArgs& a, int epi, int pro, hipStream_t st);
 size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int pro, int rg);
@@ -104,7 +115,9 @@ struct RopeArgs {
 };
 int rope_store(const RopeArgs& a, hipStream_t st);
 // tab[r][i] = bf16(cos(inv_freq[i] * pos[r])), tab[r][D/2 + i] = bf16(sin(...)), r < rows
-int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st);
+// epoch (optional): advanced once per call (the decode step's PRO_LEAD epoch)
+int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st,
+               unsigned* epoch = nullptr);
 
 // ---- attention ----------------------------------------------------------------
 struct AttnArgs {
