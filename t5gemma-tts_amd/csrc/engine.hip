@@ -89,6 +89,7 @@ struct t5g_engine {
     // decode gate/up on gemv_dec (one block per CU, 1152 single-group units dealt
     // round-robin: 18.3 us vs 19.7 us for the 576-block P16 GEMM); T5G_GU_GEMV=0 reverts
     bool gu_gemv = true;
+    bool down_gemv = false;   // T5G_DOWN_GEMV=1: decode down projection on gemv_dec split-K (probe)
     // decode norms folded into the consuming GEMV (PRO_LEAD: blocks 0..M-1 finish and
     // publish the rows, the others poll per-row flags): one launch fewer per site.
     // T5G_LEAD_NORM = site mask (1 next-layer qkv, 2 cross-q, 4 gate/up). Off by default:
@@ -243,6 +244,8 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
         e->attn_tickets = atv && atv[0] == '1';
         const char* guv = getenv("T5G_GU_GEMV");
         e->gu_gemv = !(guv && guv[0] == '0');
+        const char* dgv = getenv("T5G_DOWN_GEMV");
+        e->down_gemv = dgv && dgv[0] == '1';
         const char* lnv = getenv("T5G_LEAD_NORM");
         if (lnv) e->lead_sites = atoi(lnv) & 7;
         const char* xsv = getenv("T5G_XATTN_SPLIT");
@@ -689,8 +692,17 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         } else {
             RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st, !decode));
         }
-        RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, s_down > 1 ? (void*)e->part : (void*)tmp, d,
-                s_down > 1 ? EPI_F32 : EPI_BF16, st, !decode));
+        if (decode && e->down_gemv && M <= 16 && s_down > 1) {
+            DecGemmArgs g = dec_args(M, L.down, d, f, e->part, d, 8);
+            g.X = act;
+            g.ldx = f;
+            g.un = 8;
+            g.splits = s_down;
+            RC(gemv_dec(g, EPI_F32, PRO_LOAD, st));
+        } else {
+            RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, s_down > 1 ? (void*)e->part : (void*)tmp, d,
+                    s_down > 1 ? EPI_F32 : EPI_BF16, st, !decode));
+        }
         if (!(lead && (e->lead_sites & 1)) || l == c.n_dec_layers - 1) {
             NormArgs n = norm_args(M, d, c.rms_eps);
             if (s_down > 1) {
