@@ -89,8 +89,9 @@ struct t5g_engine {
     // decode gate/up on gemv_dec (one block per CU, 1152 single-group units dealt
     // round-robin: 18.3 us vs 19.7 us for the 576-block P16 GEMM); T5G_GU_GEMV=0 reverts
     bool gu_gemv = true;
-    bool down_gemv = false;
-    int s_down = 8;           // decode down-projection k-slices (T5G_S_DOWN, 2..8; probe)   // T5G_DOWN_GEMV=1: decode down projection on gemv_dec split-K (probe)
+    bool down_gemv = false;   // T5G_DOWN_GEMV=1: decode down projection on gemv_dec split-K (probe)
+    int s_down = 8;           // decode down-projection k-slices (T5G_S_DOWN, 2..8; probe)
+    int s_qkv = 2, s_o = 4;   // decode qkv / (o, cross-q, cross-o) k-slices (T5G_S_QKV, T5G_S_O, 2..4 = QSMAX; probe)
     // decode norms folded into the consuming GEMV (PRO_LEAD: blocks 0..M-1 finish and
     // publish the rows, the others poll per-row flags): one launch fewer per site.
     // T5G_LEAD_NORM = site mask (1 next-layer qkv, 2 cross-q, 4 gate/up). Off by default:
@@ -249,6 +250,10 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
         e->down_gemv = dgv && dgv[0] == '1';
         const char* sdv = getenv("T5G_S_DOWN");
         if (sdv && atoi(sdv) >= 2 && atoi(sdv) <= 8) e->s_down = atoi(sdv);
+        const char* sqv = getenv("T5G_S_QKV");
+        if (sqv && atoi(sqv) >= 2 && atoi(sqv) <= 4) e->s_qkv = atoi(sqv);
+        const char* sov = getenv("T5G_S_O");
+        if (sov && atoi(sov) >= 2 && atoi(sov) <= 4) e->s_o = atoi(sov);
         const char* lnv = getenv("T5G_LEAD_NORM");
         if (lnv) e->lead_sites = atoi(lnv) & 7;
         const char* xsv = getenv("T5G_XATTN_SPLIT");
@@ -438,7 +443,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
     bf16_t* tmp = e->tmp;
     const int G = c.n_heads / c.n_kv_heads;
     // split-K factors (decode: spread weight streams over >= 512 blocks)
-    const int s_qkv = decode ? 2 : 1, s_o = decode ? 4 : 1, s_cq = decode ? 4 : 1, s_down = decode ? e->s_down : 1;
+    const int s_qkv = decode ? e->s_qkv : 1, s_o = decode ? e->s_o : 1, s_cq = decode ? e->s_o : 1, s_down = decode ? e->s_down : 1;
     // one cos/sin table per step: every layer's q/k rotation uses the same positions
     const float* tab = nullptr;
     if (decode) {
