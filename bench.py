@@ -1,6 +1,6 @@
 """Throughput benchmark: T5Gemma-TTS-2b-2b generate() on MI355X.
 
-Workload (BASELINE.json metric, configs[2]): bf16, batch 8 voice-cloning
+Default workload (BASELINE.json metric, configs[2], C3): bf16, batch 8 voice-cloning
 utterances per GPU -- T_x = 60 text tokens (28 transcript + x_sep + 31 target),
 T_p = 151 prompt frames (150 codes + y_sep), tgt_y_lens = T_p + 500 (10 s),
 top-k 30 / top-p 0.9 / T 0.8, throughput mode (EOS never accepted before the
@@ -9,10 +9,15 @@ A "step" = one full generate() (encoder + prefill + AR loop + on-device stop
 rules) over the batch. Weights: seeded random at the exact 2b-2b shapes (no
 checkpoint download); data: synthetic.
 
-Multi-GPU (torchrun): one process per GPU, rank 0 draws the global batch and
-broadcasts it (RCCL), every rank generates its shard (weak scaling, no per-step
-collective), token counts are all-reduced. value = tokens of all ranks / max
-rank time.
+``--e2e`` (configs[4], C5): batch 32 per GPU, 10 s target, generate() plus the batched
+XCodec2 decode of every row at 882 samples per token (Anime-XCodec2-44.1kHz-v2 rate)
+inside the timed region; reports the real-time factor.
+
+Multi-GPU: ``--gpus N`` launches N ranks itself (one process per GPU via
+torch.distributed.run, before any GPU call) unless it already runs under a launcher
+(WORLD_SIZE set, as the driver's torchrun). Rank 0 draws the global batch and broadcasts
+it (RCCL), every rank generates its shard (weak scaling, no per-step collective), ids are
+all-gathered. value = tokens of all ranks / max rank time.
 """
 from __future__ import annotations
 
@@ -26,10 +31,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
 
 T_X, T_P, DUR_FRAMES = 60, 151, 500
 B_PER_GPU = 8
+B_PER_GPU_E2E = 32
+CPU_SAMPLE_TOKENS = 160
 
 
 def make_batch(cfg, n: int, seed: int):
@@ -43,37 +49,29 @@ def make_batch(cfg, n: int, seed: int):
     return rows
 
 
-def cpu_baseline(cfg, sd_gpu, utt, steps: int = 24):
+def cpu_baseline(cfg, sd_gpu, utt, n_tokens: int = CPU_SAMPLE_TOKENS):
     """Time the CPU oracle (the reference's algorithm restated in PyTorch CPU ops, pinned
-    to the reference's golden vectors) on a bounded sample of the same workload."""
+    bitwise to the reference's golden vectors) over a complete, measured generate() of
+    one utterance of the same workload: encoder + prefill + ``n_tokens`` AR steps, batch 1
+    as the reference. Nothing is extrapolated; the rate is tokens / wall time like the
+    reference's own [Speed] line (inference_tts_utils.py:289, 308-321)."""
+    import torch
     from oracle.t5g_oracle import SamplerParams, T5GemmaTTSOracle
     threads = int(os.environ.get("OMP_NUM_THREADS", torch.get_num_threads()))
     torch.set_num_threads(threads)
     sd = {k: v.cpu() for k, v in sd_gpu.items()}
     orc = T5GemmaTTSOracle(cfg, sd)
     x, y, tgt = utt
-    t0 = time.perf_counter()
-    ctx = orc.prepare(x, y, tgt)
-    t_pre = time.perf_counter() - t0
     p = SamplerParams(top_k=30, top_p=0.9, temperature=0.8, eos_disabled=True)
-    from oracle.t5g_oracle import draw_noise, sample_helper
-    g = torch.Generator().manual_seed(1)
-    st = ctx["state"]
-    t1 = time.perf_counter()
-    for _ in range(steps):
-        lg = orc.step_logits(ctx)
-        tok, _ = sample_helper(lg, p, st, draw_noise(g, lg.shape[-1]), eos=cfg.eog_inference,
-                               encodec_sr=cfg.encodec_sr, extra_cutoff=cfg.extra_cutoff)
-        st.cur_num_gen += 1
-        st.current_length += 1
-        orc.advance(ctx, tok)
-    t_step = (time.perf_counter() - t1) / steps
-    n_tok = DUR_FRAMES + int(cfg.extra_budget) + 1
-    rate = n_tok / (t_pre + n_tok * t_step)
-    return {"value": round(rate, 3), "unit": "audio tokens/s", "cores": threads, "kind": "port",
-            "sample": f"1 utterance of this workload (T_x {T_X}, T_p {T_P}): encoder+prefill "
-                      f"{t_pre:.2f}s + {steps} AR steps ({t_step:.3f}s/step), extrapolated to "
-                      f"{n_tok} tokens/utterance at batch 1 (reference batch-1 semantics)"}
+    t0 = time.perf_counter()
+    out = orc.generate(x, y, tgt, p, seed=1, max_steps=n_tokens)
+    dt = time.perf_counter() - t0
+    n = int(out["gen"].numel())
+    return {"value": round(n / dt, 3), "unit": "audio tokens/s", "cores": threads, "kind": "port",
+            "sample": f"1 utterance of this workload (T_x {T_X}, T_p {T_P}), complete generate(): encoder + "
+                      f"prefill + {n} AR steps (self-attention keys {T_P + 1}..{T_P + n}) in {dt:.1f} s, "
+                      f"batch 1 (reference semantics); the reference itself measured 7.04 tok/s on 8 cores "
+                      f"(SURVEY 6)"}
 
 
 def main():
@@ -82,12 +80,20 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--batch", type=int, default=B_PER_GPU)
+    ap.add_argument("--batch", type=int, default=0, help="utterances per GPU (default 8, --e2e 32)")
+    ap.add_argument("--e2e", action="store_true", help="C5: generate + XCodec2 decode in the timed region")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo (CPU collectives; lets N ranks share one GPU "
                          "to rehearse the sharded path)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started before this process touches the GPU
+        from t5gemma_tts_amd.distributed import launch_local_ranks
+        sys.exit(launch_local_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus,
+                                    require_gpus=args.dist_backend == "nccl"))
+
+    import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -100,6 +106,10 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(args.dist_backend)
+        world = dist.get_world_size()
+        rank = dist.get_rank()
+    if args.dist_backend == "nccl" and torch.cuda.device_count() < world:
+        raise SystemExit(f"{world} ranks but only {torch.cuda.device_count()} GPU(s)")
     dev = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}")
     comm_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     torch.cuda.set_device(dev)
@@ -110,12 +120,18 @@ def main():
     from t5gemma_tts_amd.weights import synthetic_weights
 
     cfg = config_2b2b()
-    B = args.batch
+    B = args.batch or (B_PER_GPU_E2E if args.e2e else B_PER_GPU)
     torch.manual_seed(1234)
     sd = synthetic_weights(cfg, seed=1234, device=str(dev))
     n_tok_row = DUR_FRAMES + int(cfg.extra_budget) + 1
     eng = T5GemmaTTSEngine(cfg, sd, device=str(dev), max_batch=B, max_text=64,
                            max_audio=T_P + 1 + n_tok_row + 8, max_gen=n_tok_row + 4)
+    codec = None
+    if args.e2e:
+        from t5gemma_tts_amd.codec import XCodec2Decoder, codec_44k, synthetic_codec_weights
+        ccfg = codec_44k()
+        codec = XCodec2Decoder(ccfg, synthetic_codec_weights(ccfg, 1), device=str(dev), max_batch=B,
+                               max_frames=n_tok_row)
 
     # global batch drawn on rank 0; each step broadcasts it over RCCL, shards it (LPT over
     # the token budget, B per rank), generates, and all-gathers the ids (8(e))
@@ -127,11 +143,21 @@ def main():
         costs = [r[1] for r in rows]
     params = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3, eos_disabled=True)
     gen_tokens = [0]
+    audio_frames = [0]
 
     def generate(shard, i):
         utts = [Utterance(x=r[2:2 + r[0]], y=r[2 + r[0]:], tgt_y_len=r[1]) for r in shard]
         out = eng.generate(utts, params, seeds=[1000 * i + rank * B + b for b in range(len(utts))], chunk=64)
         gen_tokens[0] += sum(len(g) for g in out["gen"])
+        if codec is not None:
+            # strip EOS (inference_tts_utils.py:323-354) and decode every row in one launch
+            frames = [g[g != cfg.eog_inference] for g in out["gen"]]
+            lens = [max(1, int(f.numel())) for f in frames]
+            codes = torch.zeros(len(frames), max(lens), dtype=torch.long)
+            for b, f in enumerate(frames):
+                codes[b, :f.numel()] = f
+            codec.decode(codes, lens=lens)
+            audio_frames[0] += sum(lens)
         return [g.tolist() for g in out["gen"]]
 
     def step(i):
@@ -146,6 +172,7 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    audio_frames[0] = 0
     t0 = time.perf_counter()
     tokens = 0
     for i in range(args.steps):
@@ -154,20 +181,20 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    tot = torch.tensor([float(tokens), dt], dtype=torch.float64, device=comm_dev)
+    tot = torch.tensor([float(tokens), dt, float(audio_frames[0])], dtype=torch.float64, device=comm_dev)
     if dist is not None:
-        t_tok = tot[:1].clone()
-        dist.all_reduce(t_tok, op=dist.ReduceOp.SUM)
-        t_dt = tot[1:].clone()
+        t_sum = tot[[0, 2]].clone()
+        dist.all_reduce(t_sum, op=dist.ReduceOp.SUM)
+        t_dt = tot[1:2].clone()
         dist.all_reduce(t_dt, op=dist.ReduceOp.MAX)
-        tokens_all, dt_max = float(t_tok.item()), float(t_dt.item())
+        tokens_all, frames_all, dt_max = float(t_sum[0].item()), float(t_sum[1].item()), float(t_dt.item())
     else:
-        tokens_all, dt_max = float(tokens), dt
+        tokens_all, frames_all, dt_max = float(tokens), float(audio_frames[0]), dt
     value = tokens_all / dt_max
 
-    # ---- roofline of the dominant kernel: decode GeGLU gate/up GEMM (largest weight stream)
+    # ---- roofline of the dominant kernel: decode GeGLU gate/up GEMV (largest weight stream)
     roof = None
-    if rank == 0:
+    if rank == 0 and not args.e2e:
         import ctypes as C
         from t5gemma_tts_amd import _lib
         L = _lib.lib()
@@ -195,25 +222,43 @@ def main():
         roof["decode_step_GBps"] = round(decode_weight_bytes(cfg) / (step_us.value * 1e-6) / 1e9, 1)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.e2e:
         r0 = rows[0]
         cpu = cpu_baseline(cfg, sd, (r0[2:2 + r0[0]], r0[2 + r0[0]:], r0[1]))
 
     if rank == 0:
         ms = dt_max / args.steps * 1e3
-        line = {
-            "metric": "XCodec2 audio tokens/sec (whole node) + RTF, T5Gemma-TTS-2b-2b bs=8",
-            "value": round(value, 2), "unit": "audio tokens/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic (seeded random 2b-2b weights, random text/prompt codes)",
-            "config": {"workload": "C3 voice-clone: 2b-2b bf16, 8 utterances/GPU, T_x 60, T_p 151, "
-                                   "10 s target (751 tokens/utterance), top-k 30/top-p 0.9/T 0.8",
-                       "global_batch": B * world, "seq_len": T_P + 1 + n_tok_row,
-                       "parallelism": f"dp{world} (utterance shards)"},
-            "rtf_audio_s_per_wall_s": round(value / 50.0, 3),
-            "roofline": roof, "cpu_baseline": cpu,
-        }
+        if args.e2e:
+            hop = codec.cfg.hop_length
+            audio_s = frames_all / 50.0
+            line = {
+                "metric": "end-to-end text->waveform RTF, T5Gemma-TTS-2b-2b + XCodec2 decode (882 samples/token)",
+                "value": round(audio_s / dt_max, 3), "unit": "audio seconds per wall second", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "bf16 (voice model) + fp32 (codec)",
+                "data": "synthetic (seeded random 2b-2b + codec weights, random text/prompt codes)",
+                "config": {"workload": f"C5 end-to-end: 2b-2b bf16, {B} utterances/GPU, T_x 60, T_p 151, 10 s "
+                                       f"target (751 tokens/utterance), generate + XCodec2 decode at {hop} "
+                                       f"samples/token in the timed region",
+                           "global_batch": B * world, "seq_len": T_P + 1 + n_tok_row,
+                           "parallelism": f"dp{world} (utterance shards)"},
+                "audio_tokens_per_s": round(value, 2), "wall_s_per_audio_s": round(dt_max / audio_s, 5),
+                "samples_per_s": round(frames_all * hop / dt_max, 1),
+            }
+        else:
+            line = {
+                "metric": "XCodec2 audio tokens/sec (whole node) + RTF, T5Gemma-TTS-2b-2b bs=8",
+                "value": round(value, 2), "unit": "audio tokens/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "bf16",
+                "data": "synthetic (seeded random 2b-2b weights, random text/prompt codes)",
+                "config": {"workload": f"C3 voice-clone: 2b-2b bf16, {B} utterances/GPU, T_x 60, T_p 151, "
+                                       "10 s target (751 tokens/utterance), top-k 30/top-p 0.9/T 0.8",
+                           "global_batch": B * world, "seq_len": T_P + 1 + n_tok_row,
+                           "parallelism": f"dp{world} (utterance shards)"},
+                "rtf_audio_s_per_wall_s": round(value / 50.0, 3),
+                "roofline": roof, "cpu_baseline": cpu,
+            }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -187,11 +187,13 @@ int t5g_write_state(t5g_engine* e, const t5g_sampler_state* state, int32_t row, 
 int t5g_step_only(t5g_engine* e, void* stream);
 int t5g_read_flags(t5g_engine* e, int32_t* flags_out, int32_t B, void* stream);
 /* Host re-run of one sampler step with torch.sort's exact std::sort tie order
- * (resolves ambiguous steps; see csrc/host_sampler.cpp). Pure host function. */
+ * (resolves ambiguous steps; see csrc/host_sampler.cpp). Pure host function.
+ * max_gen / max_len: the engine's generated-token and self-attention cache capacity
+ * (EOS is forced at the last generated slot or when the cache has no room left). */
 int t5g_host_sample(const uint16_t* logits_bf16, int32_t V, const t5g_sampler_row* row,
                     const int32_t* top_k_list, const int32_t* silence, const t5g_sampler_state* state_in,
                     const uint16_t* noise_bf16, int32_t eos, int32_t eos_guard, float budget_extra,
-                    int32_t text_guard, float progress_scale, int32_t max_gen,
+                    int32_t text_guard, float progress_scale, int32_t max_gen, int32_t max_len,
                     t5g_sampler_state* state_out, int32_t* token_out);
 
 /* Device pointer of the logits buffer bf16 [max_batch][logits_ld] (debug / parity). */
@@ -252,6 +254,28 @@ int t5g_gemv(const t5g_gemv_args* args, void* stream);
  * (see t5g_time_gemm); average microseconds per launch in *avg_us. */
 int t5g_time_gemv(const t5g_gemv_args* args, const void* const* Wp_list, int32_t n_w, int32_t iters, void* stream,
                   float* avg_us);
+
+/* Decode attention on caller buffers (single-query rows, sdpa numerics): the kernels the
+ * engine's decode step runs for self / cross attention ([tf] T5GemmaSelfAttention
+ * :264-304 with the KV cache of cache_utils.py:127-144; PMCrossAttention :167-253) --
+ * keys split in chunks of <= 64 over workgroups, exp values rounded to bf16 before P.V
+ * like torch's CPU SDPA, partials merged by the combine kernel. For parity tests. */
+typedef struct {
+    int32_t B, n_heads, n_kv_heads, head_dim;
+    const void* q;            /* bf16 [B][n_heads * head_dim], PM-RoPE already applied */
+    const void* k_cache;      /* bf16 [B][n_kv_heads][cap][head_dim] */
+    const void* v_cache;
+    int32_t cap;              /* key slots per (row, kv head) */
+    const int32_t* kv_len;    /* device [B]: keys of each row (query = key kv_len - 1) */
+    int32_t causal;           /* 1: self attention (keys <= query), 0: cross attention */
+    int32_t window;           /* sliding window (0: none) */
+    float scale;
+    void* out;                /* bf16 [B][n_heads * head_dim] */
+    void* work;               /* fp32 partials, t5g_attention_decode_work_bytes() */
+} t5g_attn_decode_args;
+int64_t t5g_attention_decode_work_bytes(int32_t B, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
+                                        int32_t cap);
+int t5g_attention_decode(const t5g_attn_decode_args* args, void* stream);
 
 #ifdef __cplusplus
 }

@@ -83,6 +83,13 @@ class GemvArgs(C.Structure):
                 ("splits", C.c_int32), ("layout", C.c_int32)]
 
 
+class AttnDecodeArgs(C.Structure):
+    _fields_ = [("B", C.c_int32), ("n_heads", C.c_int32), ("n_kv_heads", C.c_int32), ("head_dim", C.c_int32),
+                ("q", C.c_void_p), ("k_cache", C.c_void_p), ("v_cache", C.c_void_p), ("cap", C.c_int32),
+                ("kv_len", C.c_void_p), ("causal", C.c_int32), ("window", C.c_int32), ("scale", C.c_float),
+                ("out", C.c_void_p), ("work", C.c_void_p)]
+
+
 # name -> (restype, argtypes); exactly the functions include/t5gtts.h declares
 _P, _I, _L, _F = C.c_void_p, C.c_int32, C.c_int64, C.c_float
 SIGNATURES = {
@@ -102,7 +109,7 @@ SIGNATURES = {
     "t5g_step_only": (C.c_int, [_P, _P]),
     "t5g_read_flags": (C.c_int, [_P, _P, _I, _P]),
     "t5g_host_sample": (C.c_int, [_P, _I, C.POINTER(SamplerRow), _P, _P, C.POINTER(SamplerState), _P, _I, _I,
-                                  _F, _I, _F, _I, C.POINTER(SamplerState), C.POINTER(_I)]),
+                                  _F, _I, _F, _I, _I, C.POINTER(SamplerState), C.POINTER(_I)]),
     "t5g_logits_ptr": (_P, [_P, C.POINTER(_I)]),
     "t5g_copy_logits": (C.c_int, [_P, _P, _I, _P]),
     "t5g_sample_only": (C.c_int, [_P, _I, _P, _I, _P]),
@@ -111,6 +118,8 @@ SIGNATURES = {
     "t5g_time_decode_step": (C.c_int, [_P, _I, _P, C.POINTER(_F)]),
     "t5g_gemv": (C.c_int, [C.POINTER(GemvArgs), _P]),
     "t5g_time_gemv": (C.c_int, [C.POINTER(GemvArgs), C.POINTER(_P), _I, _I, _P, C.POINTER(_F)]),
+    "t5g_attention_decode_work_bytes": (_L, [_I, _I, _I, _I, _I]),
+    "t5g_attention_decode": (C.c_int, [C.POINTER(AttnDecodeArgs), _P]),
 }
 
 _lib = None

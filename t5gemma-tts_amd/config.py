@@ -163,9 +163,10 @@ class VoiceConfig:
 # ----------------------------------------------------------------------
 # Named configurations used by tests / bench
 # ----------------------------------------------------------------------
-def config_2b2b(attn_implementation: str = "sdpa") -> VoiceConfig:
-    """T5Gemma-TTS-2b-2b as released (examples/training/t5gemma_2b-2b.sh)."""
-    return VoiceConfig(backbone=BackboneDims(attn_implementation=attn_implementation))
+def config_2b2b(attn_implementation: str = "sdpa", **voice_kw) -> VoiceConfig:
+    """T5Gemma-TTS-2b-2b as released (examples/training/t5gemma_2b-2b.sh). ``voice_kw``
+    overrides VoiceConfig fields (e.g. a short ``extra_cutoff`` for bounded golden runs)."""
+    return VoiceConfig(backbone=BackboneDims(attn_implementation=attn_implementation), **voice_kw)
 
 
 def config_mid(attn_implementation: str = "sdpa", layers: int = 2) -> VoiceConfig:

@@ -4,6 +4,15 @@
 // rounds (see DESIGN.md "numerics contract").
 #pragma once
 #include <hip/hip_runtime.h>
+
+// The in-launch cross-workgroup hand-offs (sampler slice candidates, attention split
+// tickets) use the gfx950 form measured valid in the MI355X guide (sc1 write-through
+// stores, every storing wave's vmcnt(0) drain, one relaxed agent-scope atomic, sc1
+// loads by the last arriver) rather than release/acquire fences. That is a property of
+// this ISA's cache policy bits, not of the HIP memory model: refuse any other target.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "libt5gtts device code is written for gfx950 (MI355X) only"
+#endif
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 

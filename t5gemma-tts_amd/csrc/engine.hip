@@ -1021,6 +1021,7 @@ static SamplerArgs sampler_args(t5g_engine* e, const bf16_t* logits, int ld, int
     s.progress_scale = e->c.progress_scale;
     s.out_tokens = e->out_tokens;
     s.max_gen = e->c.max_gen;
+    s.max_len = e->c.max_audio;
     s.kv_len = e->kv_len;
     s.next_pos = e->next_pos;
     s.next_token = e->next_token;
@@ -1198,6 +1199,42 @@ extern "C" int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, 
     *avg_us = ms * 1000.f / iters;
     hipEventDestroy(e0);
     hipEventDestroy(e1);
+    return T5G_OK;
+}
+
+extern "C" int64_t t5g_attention_decode_work_bytes(int32_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t cap) {
+    if (B <= 0 || Hkv <= 0 || Hq % Hkv || D <= 0 || cap <= 0) return -1;
+    const int64_t nsplit = (cap + 63) / 64;
+    return (int64_t)B * Hkv * nsplit * (Hq / Hkv) * (D + 2) * 4;
+}
+
+extern "C" int t5g_attention_decode(const t5g_attn_decode_args* g, void* stream) {
+    if (!g || !g->q || !g->k_cache || !g->v_cache || !g->kv_len || !g->out || !g->work) return T5G_EINVAL;
+    if (g->B <= 0 || g->n_kv_heads <= 0 || g->n_heads % g->n_kv_heads || g->cap <= 0 || g->cap > 4096)
+        return T5G_EINVAL;
+    AttnArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Q = (const bf16_t*)g->q;
+    a.ldq = g->n_heads * g->head_dim;
+    a.Mq = g->B;
+    a.K = (const bf16_t*)g->k_cache;
+    a.V = (const bf16_t*)g->v_cache;
+    a.kv_hstride = (long)g->cap * g->head_dim;
+    a.kv_bstride = a.kv_hstride * g->n_kv_heads;
+    a.kv_len = g->kv_len;
+    a.Hkv = g->n_kv_heads;
+    a.D = g->head_dim;
+    a.G = g->n_heads / g->n_kv_heads;
+    a.causal = g->causal;
+    a.window = g->window;
+    a.scale = g->scale;
+    a.O = (bf16_t*)g->out;
+    a.ldo = a.ldq;
+    a.chunk = 64;
+    a.nsplit = (g->cap + 63) / 64;
+    a.kv_cap = g->cap;
+    a.part = (float*)g->work;
+    RC(attention_decode(a, (hipStream_t)stream));
     return T5G_OK;
 }
 

@@ -8,7 +8,7 @@
 //
 // This is part of libt5gtts.so (product library, C++), not of the oracle: it is
 // the production fallback for exact-parity mode and is cross-checked against the
-// oracle in tests/test_host_sampler.py.
+// reference's sampler goldens in tests/test_lib_cpu.py.
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
@@ -54,7 +54,7 @@ void softmax_bf16(const std::vector<float>& x, std::vector<float>& p) {
 extern "C" int t5g_host_sample(const uint16_t* logits, int32_t V, const t5g_sampler_row* row,
                                const int32_t* top_k_list, const int32_t* silence, const t5g_sampler_state* st_in,
                                const uint16_t* noise, int32_t eos, int32_t eos_guard, float budget_extra,
-                               int32_t text_guard, float progress_scale, int32_t max_gen,
+                               int32_t text_guard, float progress_scale, int32_t max_gen, int32_t max_len,
                                t5g_sampler_state* st_out, int32_t* token_out) {
     if (!logits || !row || !st_in || !noise || !st_out || !token_out || V <= 0) return T5G_EINVAL;
     t5g_sampler_state st = *st_in;
@@ -143,7 +143,8 @@ extern "C" int t5g_host_sample(const uint16_t* logits, int32_t V, const t5g_samp
     if (text_guard > 0) force = force || eff_len > std::max(1, st.first_input_len) * text_guard;
     const bool budget = st.target_total >= 0 &&
                         (double)st.cur_num_gen > (double)(st.target_total - st.prompt_offset) + (double)budget_extra;
-    if (force || budget) token = eos;
+    const bool cap = st.cur_num_gen + 1 >= max_gen || st.current_length >= max_len;   // as sampler.hip
+    if (force || budget || cap) token = eos;
     bool in_sil = false;
     for (int s = 0; s < row->n_silence; ++s) in_sil |= silence[row->silence_off + s] == token;
     st.consec_silence = (in_sil && token == st.prev_token) ? st.consec_silence + 1 : 0;
@@ -151,7 +152,7 @@ extern "C" int t5g_host_sample(const uint16_t* logits, int32_t V, const t5g_samp
     st.cur_num_gen += 1;
     st.current_length += 1;
     st.last_token = token;
-    if (token == eos || st.cur_num_gen >= max_gen) {
+    if (token == eos) {
         st.done = 1;
     } else {
         double v = (double)(st.current_length - 1) / (double)std::max(1, st.est_total - 1) * (double)progress_scale;

@@ -158,11 +158,15 @@ __device__ __forceinline__ uint32_t philox(uint32_t c0, uint32_t c1, uint32_t c2
 }
 
 // The exponential draw q of torch.multinomial for element i: parity mode reads the
-// uploaded reference stream, production draws Philox4x32-10(i, step, row; seed).
+// uploaded reference stream, production draws Philox4x32-10(i, step; seed): the
+// counter holds no batch slot, so an utterance samples the same tokens whatever
+// its slot in the batch or the rank it is sharded to (rows needing different
+// streams get different seeds from the host).
 __device__ __forceinline__ float draw_q(const SamplerArgs& a, const SamplerRow& pr, const SamplerState& st, int b,
                                         int i) {
     if (a.noise) return bf2f(a.noise[((long)b * a.noise_steps + st.cur_num_gen) * a.V + i]);
-    const uint32_t u = philox((uint32_t)i, (uint32_t)st.cur_num_gen, (uint32_t)b, pr.seed_lo, pr.seed_hi);
+    (void)b;
+    const uint32_t u = philox((uint32_t)i, (uint32_t)st.cur_num_gen, 0u, pr.seed_lo, pr.seed_hi);
     const float uf = ((float)(u >> 8) + 1.0f) * (1.0f / 16777216.0f);
     float q = rbf(-logf(uf));
     if (q <= 0.f) q = 5.9604645e-08f;
@@ -176,7 +180,10 @@ __device__ void finish_row(const SamplerArgs& a, const SamplerRow& pr, SamplerSt
     if (a.text_guard > 0) force = force || (eff_len > max(1, st.first_input_len) * a.text_guard);
     bool budget = st.target_total >= 0 &&
                   (double)st.cur_num_gen > (double)(st.target_total - st.prompt_offset) + (double)a.budget_extra;
-    if (force || budget) token = a.eos;
+    // capacity: the last generated-token slot, or a self-attention cache with no room
+    // for the next key, ends the row with EOS (only reachable without tgt_y_lens)
+    const bool cap = st.cur_num_gen + 1 >= a.max_gen || st.current_length >= a.max_len;
+    if (force || budget || cap) token = a.eos;
     bool in_sil = false;
     for (int s = 0; s < pr.n_silence; ++s) in_sil |= (a.silence[pr.silence_off + s] == token);
     if (in_sil && token == st.prev_token)
@@ -189,7 +196,7 @@ __device__ void finish_row(const SamplerArgs& a, const SamplerRow& pr, SamplerSt
     st.current_length += 1;
     st.last_token = token;
     st.ambiguous_steps += ambiguous;
-    if (token == a.eos || st.cur_num_gen >= a.max_gen) {
+    if (token == a.eos) {
         st.done = 1;
     } else {
         double v = (double)(st.current_length - 1) / (double)max(1, st.est_total - 1) * (double)a.progress_scale;

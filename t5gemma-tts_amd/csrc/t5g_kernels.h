@@ -196,6 +196,7 @@ struct SamplerArgs {
     float progress_scale;
     int* out_tokens;          // [B][max_gen]
     int max_gen;
+    int max_len;              // self-attention cache slots per row (engine max_audio)
     int* kv_len;              // [B] self-attention keys (advanced with current_length)
     float* next_pos;          // [B] float PM position for the next step
     int* next_token;          // [B] token fed to the next decoder step

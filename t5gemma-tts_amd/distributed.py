@@ -13,10 +13,34 @@ DistributedDynamicBatchSampler (steps/trainer_utils.py:210-660).
 """
 from __future__ import annotations
 
+import os
+import subprocess
+import sys
 from typing import Callable, List, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
+
+
+def launch_local_ranks(script: str, argv: Sequence[str], n: int, require_gpus: bool = True,
+                       master_port: int = 0) -> int:
+    """Run ``script argv`` as ``n`` ranks of one node under torch.distributed.run (one
+    process per GPU) and return the launcher's exit code. Called by a process that has
+    not touched the GPU; the ranks are children (never an exec). ``require_gpus``: fail
+    before launching when fewer than n GPUs are visible (``device_count`` does not
+    initialise the GPU on this image)."""
+    if n < 1:
+        raise ValueError("n must be >= 1")
+    if require_gpus:
+        have = torch.cuda.device_count()
+        if have < n:
+            raise SystemExit(f"{os.path.basename(script)}: {n} ranks requested but only {have} GPU(s) visible")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this driver
+    port = master_port or int(env.get("BENCH_MASTER_PORT", "29512"))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), script] + list(argv)
+    return subprocess.call(cmd, env=env)
 
 
 def assign_shards(costs: Sequence[float], world: int, max_per_rank: int = 0) -> List[List[int]]:

@@ -51,14 +51,28 @@ class Utterance:
     prompt_frames: Optional[int] = None
 
 
-def reference_noise(seed: int, steps: int, V: int) -> torch.Tensor:
+def reference_noise(seed, steps: int, V: int) -> torch.Tensor:
     """The exponential draws torch.multinomial(p, 1) makes on CPU for ``steps``
-    consecutive calls after ``torch.manual_seed(seed)`` (parity mode, SURVEY a14' 6)."""
-    g = torch.Generator().manual_seed(int(seed))
+    consecutive calls (parity mode, SURVEY a14' 6): after ``torch.manual_seed(seed)``
+    for an int ``seed``, or continuing a ``torch.Generator`` (its state is not
+    consumed: the draws come from a copy, see ``consume_noise``)."""
+    if isinstance(seed, torch.Generator):
+        g = torch.Generator()
+        g.set_state(seed.get_state())
+    else:
+        g = torch.Generator().manual_seed(int(seed))
     out = torch.empty(steps, V, dtype=BF16)
     for s in range(steps):
         out[s] = torch.empty(V, dtype=BF16).exponential_(1, generator=g)
     return out
+
+
+def consume_noise(gen: torch.Generator, steps: int, V: int) -> None:
+    """Advance ``gen`` past ``steps`` multinomial calls over V probabilities, exactly as
+    the reference's AR loop leaves torch's global generator (:744-751, one
+    ``exponential_`` of V bf16 draws per step, EOS step included)."""
+    for _ in range(steps):
+        torch.empty(V, dtype=BF16).exponential_(1, generator=gen)
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -247,19 +261,29 @@ class T5GemmaTTSEngine:
     # ------------------------------------------------------------------
     def generate(self, utts: Sequence[Utterance], params: Union[SamplingParams, Sequence[SamplingParams]],
                  seeds: Optional[Sequence[int]] = None, parity: bool = False, use_graph: bool = True,
-                 chunk: int = 32, record_logits: bool = False):
+                 chunk: int = 32, record_logits: bool = False,
+                 generators: Optional[Sequence[torch.Generator]] = None):
         """Run inference_tts on a batch. ``parity=True`` uses the reference's CPU RNG
-        stream (seed per row, reseeded before the loop) and resolves tie-ambiguous
-        top-p steps on the host -- token-exact reproduction mode (slow: one host
-        sync per step). Returns dict(res=[...], gen=[...], steps, ambiguous)."""
+        stream and resolves tie-ambiguous top-p steps on the host -- token-exact
+        reproduction mode (slow: one host sync per step). The stream of row i is
+        ``torch.manual_seed(seeds[i])`` or, with ``generators``, the continuation of
+        ``generators[i]`` (e.g. ``torch.default_generator`` after ``seed_everything``),
+        which is then advanced by exactly the draws the reference would have made.
+        Returns dict(res=[...], gen=[...], steps, ambiguous)."""
+        if generators is not None and not parity:
+            raise ValueError("generators= drives the reference RNG stream: parity=True only")
         stream = _stream(self.device)
-        ctx = self._prepare(utts, params, seeds, parity, stream)
+        ctx = self._prepare(utts, params, generators if generators is not None else seeds, parity, stream)
         if parity:
             self._run_parity(ctx, stream, record_logits)
         else:
             while not self._decode_chunk(ctx, chunk, use_graph, stream):
                 pass
-        return self._collect(ctx, stream)
+        out = self._collect(ctx, stream)
+        if generators is not None:
+            for g, row in zip(generators, out["gen"]):
+                consume_noise(g, len(row), self.V)
+        return out
 
     # -- phases ------------------------------------------------------------------
     def _prepare(self, utts, params, seeds, parity, stream):
@@ -272,6 +296,8 @@ class T5GemmaTTSEngine:
         if isinstance(params, SamplingParams):
             params = [params] * B
         seeds = list(seeds) if seeds is not None else list(range(1, B + 1))
+        if len(seeds) < B:
+            raise ValueError(f"{len(seeds)} seeds for {B} rows")
         # ---- host plumbing: packed text / audio tokens and float PM positions
         ids, trow, tt, tpos, tlen = [], [], [], [], []
         aid, arow, at, apos, alen, last = [], [], [], [], [], []
@@ -317,12 +343,15 @@ class T5GemmaTTSEngine:
             st.est_total, st.prev_token, st.consec_silence = est, -1, 0
             st.first_input_len, st.done, st.ambiguous_steps, st.last_token, st.next_pos = len(x), 0, 0, -1, 0.0
             if tgt is not None:
-                budget = int(math.floor(tgt - (pf + 1) + cfg.extra_budget)) + 2
+                budget = min(int(math.floor(tgt - (pf + 1) + cfg.extra_budget)) + 2, self.max_gen)
+                if cur_len + budget > self.max_audio:
+                    raise ValueError(f"row {b}: prompt {cur_len} + budget {budget} > max_audio {self.max_audio}")
             else:
-                budget = self.max_gen
-            budget = min(budget, self.max_gen)
-            if cur_len + budget > self.max_audio:
-                raise ValueError(f"row {b}: prompt {cur_len} + budget {budget} > max_audio {self.max_audio}")
+                # no tgt_y_lens (:624): the reference has no time budget, only EOS; the
+                # engine's cache capacity bounds the row (EOS forced at the last slot)
+                budget = min(self.max_gen, self.max_audio - cur_len)
+                if budget < 1:
+                    raise ValueError(f"row {b}: prompt {cur_len} leaves no room in max_audio {self.max_audio}")
             max_steps = max(max_steps, budget)
             p = params[b]
             r = rows[b]
@@ -336,7 +365,8 @@ class T5GemmaTTSEngine:
             r.n_silence, r.silence_off = len(p.silence_tokens), len(silence)
             silence += [int(s) for s in p.silence_tokens]
             r.eos_disabled = int(bool(p.eos_disabled))
-            r.seed_lo, r.seed_hi = int(seeds[b]) & 0xFFFFFFFF, (int(seeds[b]) >> 32) & 0xFFFFFFFF
+            sd = int(seeds[b].initial_seed()) if isinstance(seeds[b], torch.Generator) else int(seeds[b])
+            r.seed_lo, r.seed_hi = sd & 0xFFFFFFFF, (sd >> 32) & 0xFFFFFFFF
         i32 = dict(dtype=torch.int32, device=dev)
         d_ids, d_trow, d_tt = (torch.tensor(v, **i32) for v in (ids, trow, tt))
         d_tpos = torch.cat(tpos).to(dev)
@@ -405,7 +435,8 @@ class T5GemmaTTSEngine:
                 _lib.check(L.t5g_host_sample(
                     _ptr(lg), self.V, C.byref(rows[b]), tk, sl, C.byref(pre[b]), _ptr(nz), eos,
                     self._cfg.eos_guard, self._cfg.budget_extra, self._cfg.text_guard,
-                    self._cfg.progress_scale, self.max_gen, C.byref(out_st), C.byref(tok)), "host_sample")
+                    self._cfg.progress_scale, self.max_gen, self.max_audio, C.byref(out_st), C.byref(tok)),
+                    "host_sample")
                 out_st.ambiguous_steps = pre[b].ambiguous_steps + 1
                 _lib.check(L.t5g_write_state(self.h, C.byref(out_st), b, pre[b].cur_num_gen, tok.value,
                                              stream), "write_state")
@@ -450,7 +481,6 @@ class T5GemmaVoiceForConditionalGeneration:
         self.config = cfg
         self.args = cfg
         self.engine = T5GemmaTTSEngine(cfg, state_dict, device=device, **engine_kw)
-        self.seed = 1
 
     @classmethod
     def from_pretrained(cls, model_dir: str, device="cuda:0", **engine_kw):
@@ -466,9 +496,20 @@ class T5GemmaVoiceForConditionalGeneration:
 
     @torch.inference_mode()
     def inference_tts(self, x, x_lens, y, tgt_y_lens, top_k=-100, top_p=1.0, min_p=0.0, temperature=1.0,
-                      stop_repetition=3, silence_tokens=None, multi_trial=None, parity=False, seeds=None,
+                      stop_repetition=3, silence_tokens=None, multi_trial=None, parity=True, seeds=None,
                       **kwargs):
+        """Reference signature and RNG contract (:565-862). With the defaults the noise of
+        every step is drawn from torch's global CPU generator exactly as the reference's
+        ``torch.multinomial`` draws it (:137), so ``seed_everything(s)`` followed by this
+        call returns the reference's tokens and leaves the global generator where the
+        reference leaves it. ``parity=False`` is the fast path (on-device Philox noise,
+        graph-replayed loop); its per-row seeds are drawn from the global generator
+        unless ``seeds`` is given. Batch > 1 (not allowed by the reference, :594) gives
+        row i its own stream: ``seeds[i]``, or a seed drawn from the global generator."""
         cfg = self.config
+        if multi_trial:
+            import warnings
+            warnings.warn("multi_trial is not supported and will be ignored")   # :585-586
         if int(getattr(cfg, "n_codebooks", 1)) != 1:
             raise ValueError("XCodec2 inference expects n_codebooks=1.")
         B = x.shape[0]
@@ -483,9 +524,13 @@ class T5GemmaVoiceForConditionalGeneration:
                                   prompt_frames=pf))
         params = SamplingParams(top_k=top_k, top_p=top_p, min_p=min_p, temperature=temperature,
                                 stop_repetition=stop_repetition, silence_tokens=tuple(silence_tokens or ()))
+        generators = None
         if seeds is None:
-            seeds = [self.seed + b for b in range(B)]
-        out = self.engine.generate(utts, params, seeds=seeds, parity=parity)
+            if parity and B == 1:
+                generators = [torch.default_generator]
+            else:
+                seeds = [int(s) for s in torch.randint(0, 2 ** 62, (B,), dtype=torch.int64).tolist()]
+        out = self.engine.generate(utts, params, seeds=seeds, parity=parity, generators=generators)
         n = max(len(g) for g in out["gen"])
         if B == 1:
             return out["res"][0].view(1, 1, -1), out["gen"][0].view(1, 1, -1)

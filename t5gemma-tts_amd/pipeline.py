@@ -118,6 +118,24 @@ def strip_sep_and_eos(frames: torch.Tensor, sep_token: Optional[int], eos_token:
     return frames[mask].view(frames.size(0), frames.size(1), n)
 
 
+CODEC_INPUT_SR = 16000     # XCodec2 encodes 16 kHz audio (data/tokenizer.py:125-143)
+CODEC_INPUT_HOP = 320      # input samples per code at 16 kHz
+
+
+def prompt_frames_for_samples(n_samples: int, sample_rate: int) -> int:
+    """Codes XCodec2's encoder emits for the first ``n_samples`` of a ``sample_rate`` file.
+
+    The reference truncates the reference audio to ``prompt_end_frame`` samples at the
+    file's own rate (``torchaudio.load(num_frames=...)``, data/tokenizer.py:127-128, with
+    ``prompt_end_frame = int(cut_off_sec * sr)``, inference_commandline_hf.py:181),
+    resamples to 16 kHz (torchaudio: ceil(n * 16000 / sr) samples) and encodes; the
+    encoder pads one sample and then up to a multiple of the 320-sample hop
+    ([tf] feature_extraction_xcodec2.py "acoustic encoder padding"), i.e. n16 // 320 + 1
+    codes."""
+    n16 = -(-int(n_samples) * CODEC_INPUT_SR // int(sample_rate))
+    return n16 // CODEC_INPUT_HOP + 1
+
+
 def _eos_token(model_args):
     return getattr(model_args, "eos", getattr(model_args, "eog", None))
 
@@ -126,12 +144,16 @@ def _eos_token(model_args):
 def inference_one_sample(model, model_args, text_tokenizer, audio_tokenizer, prompt_codes, target_text, lang,
                          device, decode_config, prompt_end_frame, target_generation_length, prefix_transcript=None,
                          quiet=False, repeat_prompt=0, multi_trial=None, return_frames=False, seed=None,
-                         parity=False):
+                         parity=True, prompt_sample_rate=CODEC_INPUT_SR):
     """Same arguments and returns as the reference (inference_tts_utils.py:140-378),
     except that ``prompt_codes`` (codec ids of the reference audio, or None) replaces
-    ``audio_fn`` because the codec encoder is out of scope; ``prompt_end_frame`` > 0
-    truncates them like the reference's ``num_frames``. ``lang``/``device`` are accepted
-    for signature compatibility (normalisation is out of scope; the engine's device wins)."""
+    ``audio_fn``. ``prompt_end_frame`` keeps the reference's units -- a count of audio
+    SAMPLES of the reference file at ``prompt_sample_rate`` (its own rate, e.g.
+    ``int(cut_off_sec * sr)``) -- and keeps the codes those samples encode to
+    (``prompt_frames_for_samples``). ``parity=True`` (default) draws the sampling noise
+    from torch's global generator like the reference; ``seed`` gives the row its own
+    ``manual_seed`` stream instead. ``lang``/``device`` are accepted for signature
+    compatibility (the engine's device wins)."""
     multi_trial = multi_trial or []
     if int(getattr(model_args, "n_codebooks", 1)) != 1:
         raise ValueError("XCodec2 backend supports only n_codebooks=1.")
@@ -145,7 +167,7 @@ def inference_one_sample(model, model_args, text_tokenizer, audio_tokenizer, pro
         silence = [int(v) for v in silence.strip("[]() ").split(",") if v.strip()]
     if prompt_codes is not None and prompt_end_frame and prompt_end_frame > 0:
         pc = torch.as_tensor(prompt_codes).reshape(-1)
-        prompt_codes = pc[:int(prompt_end_frame)]
+        prompt_codes = pc[:prompt_frames_for_samples(int(prompt_end_frame), int(prompt_sample_rate))]
     original_audio = build_prompt(prompt_codes, getattr(model_args, "y_sep_token", None), codec_sr,
                                   target_generation_length, repeat_prompt,
                                   float(getattr(model_args, "audio_max_length", 40.0)))

@@ -63,7 +63,9 @@ class _Args:
     pass
 
 
-def build_reference_model(RT, cfg, seed, workdir):
+def build_reference_model(RT, cfg, seed, workdir, lowmem=False):
+    """``lowmem``: construct the throw-away backbone directly in bf16 (2b-2b: the fp32
+    init alone would take 24 GB); every parameter is overwritten by load_state_dict."""
     from transformers import T5GemmaConfig, T5GemmaForConditionalGeneration
 
     bb = cfg.backbone
@@ -76,7 +78,15 @@ def build_reference_model(RT, cfg, seed, workdir):
                          decoder=dict(side, num_hidden_layers=bb.num_decoder_layers),
                          vocab_size=bb.text_vocab_size)
     bdir = os.path.join(workdir, "backbone")
-    T5GemmaForConditionalGeneration(tcfg).to(torch.bfloat16).save_pretrained(bdir)
+    prev = torch.get_default_dtype()
+    if lowmem:
+        torch.set_default_dtype(torch.bfloat16)
+    try:
+        bb_model = T5GemmaForConditionalGeneration(tcfg).to(torch.bfloat16)
+    finally:
+        torch.set_default_dtype(prev)
+    bb_model.save_pretrained(bdir)
+    del bb_model
 
     a = _Args()
     a.t5gemma_model_name = bdir
@@ -212,6 +222,50 @@ def gen_model_golden(RT, name, cfg_kw, seed, n_cases, out, store_logits="full", 
     np.savez_compressed(os.path.join(HERE, f"{out}.npz"), **arrays)
 
 
+def full_cases(cfg, seed, n_cases, steps):
+    """C3-shaped utterances (bench.py make_batch): T_x 60 (28 transcript ids + x_sep + 31
+    target ids), T_p 151 (150 codes + y_sep), tgt_y_lens = T_p + 1 so that the time budget
+    (:773-777) stops the row after ``steps`` tokens (extra_cutoff = (steps - 2) / 50)."""
+    rng = np.random.default_rng(seed)
+    cases = []
+    for i in range(n_cases):
+        x = rng.integers(3, cfg.backbone.text_vocab_size - 1, size=60)
+        x[28] = cfg.x_sep_token
+        y = rng.integers(0, cfg.audio_vocab_size, size=150).tolist() + [cfg.y_sep_token]
+        cases.append(dict(x=[int(v) for v in x], y=[int(v) for v in y], tgt=len(y) + 1, seed=int(2000 + i),
+                          top_k=30, top_p=0.9, min_p=0.0, temperature=0.8, stop_repetition=3,
+                          silence_tokens=[]))
+    return cases
+
+
+def gen_full_golden(RT, out="golden_full", seed=13, n_cases=2, steps=16):
+    """Full-depth 2b-2b (26 + 26 layers, d 2304, V 65541) at the C3 shapes: the
+    reference's own inference_tts, top-64 logits + per-step sha of the full row."""
+    import hashlib
+    kw = {"extra_cutoff": (steps - 2) / 50.0}
+    cfg = named_config("2b2b", **kw)
+    with tempfile.TemporaryDirectory(dir=os.environ.get("GOLDEN_TMP", "/tmp")) as td:
+        m, sd = build_reference_model(RT, cfg, seed, td, lowmem=True)
+        cases = full_cases(cfg, seed, n_cases, steps)
+        arrays = {}
+        for ci, c in enumerate(cases):
+            res, gen, logs, dt = run_case(RT, m, cfg, c)
+            c["res"], c["gen"] = res, gen
+            c["ref_seconds"] = round(dt, 4)
+            c["n_steps"] = int(logs.shape[0])
+            top = torch.topk(logs.float(), 64, dim=-1)
+            arrays[f"top_vals_{ci}"] = bf16_bits(top.values.to(torch.bfloat16))
+            arrays[f"top_idx_{ci}"] = top.indices.numpy().astype(np.int32)
+            c["logit_sha"] = [hashlib.sha256(bf16_bits(r).tobytes()).hexdigest()[:16] for r in logs]
+            print(f"[full] case {ci}: T_x={len(c['x'])} T_p={len(c['y'])} gen={len(gen)} ({dt:.2f}s)", flush=True)
+        digest = state_dict_digest(sd)
+    meta = {"config": "2b2b", "config_kw": kw, "weight_seed": seed, "weight_sha256": digest,
+            "torch": torch.__version__, "threads": torch.get_num_threads(), "cases": cases}
+    with open(os.path.join(HERE, f"{out}.json"), "w") as f:
+        json.dump(meta, f)
+    np.savez_compressed(os.path.join(HERE, f"{out}.npz"), **arrays)
+
+
 def gen_sampler_golden(RU, out="golden_sampler", V=65541, n=48):
     """Per-step sampler cases at the real vocab: reference topk_sampling +
     torch.multinomial under torch.manual_seed(seed). Logits regenerable from
@@ -266,6 +320,8 @@ if __name__ == "__main__":
                          out="golden_tiny_eager")
     if "tiny_window" in todo:
         gen_model_golden(RT, "tiny", {"sliding_window": 8}, seed=9, n_cases=4, out="golden_tiny_window")
+    if "full" in todo:
+        gen_full_golden(RT)
     if "mid" in todo:
         gen_model_golden(RT, "mid", {}, seed=11, n_cases=2, out="golden_mid", store_logits="top",
                          max_tx=40, tgt_frames=(4, 8))

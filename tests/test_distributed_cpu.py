@@ -75,3 +75,24 @@ def test_run_sharded_gloo(world):
         assert out == expect
         mines += mine
     assert sorted(mines) == list(range(7))
+
+
+def test_launch_local_ranks_gloo(tmp_path):
+    """bench.py --gpus N's launcher: N ranks under torch.distributed.run, each seeing
+    WORLD_SIZE = N and its own rank through a gloo process group (the bench's N > 1 path
+    reports n_gpus = dist.get_world_size())."""
+    from t5gemma_tts_amd.distributed import launch_local_ranks
+    script = tmp_path / "probe.py"
+    script.write_text(
+        "import os, sys, torch.distributed as dist\n"
+        "dist.init_process_group('gloo')\n"
+        "t = __import__('torch').tensor([dist.get_rank() + 1])\n"
+        "dist.all_reduce(t)\n"
+        "open(os.path.join(sys.argv[1], f'rank{dist.get_rank()}'), 'w').write(f'{dist.get_world_size()} {int(t)}')\n"
+        "dist.destroy_process_group()\n")
+    rc = launch_local_ranks(str(script), [str(tmp_path)], 2, require_gpus=False, master_port=_free_port())
+    assert rc == 0
+    assert sorted(p.name for p in tmp_path.glob("rank*")) == ["rank0", "rank1"]
+    assert all(p.read_text() == "2 3" for p in tmp_path.glob("rank*"))
+    with pytest.raises(SystemExit):      # more ranks than GPUs: refused before launching
+        launch_local_ranks(str(script), [str(tmp_path)], 4, require_gpus=True)

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN
+from conftest import GOLDEN, REPO
 
 pytestmark = pytest.mark.gpu
 
@@ -190,10 +190,69 @@ def _oparams(c):
                          stop_repetition=c["stop_repetition"], silence_tokens=tuple(c["silence_tokens"]))
 
 
+# free-running token-exact cases each golden set must keep (measured on MI355X, see
+# profiles/r02_parity_rates.json); every other case must diverge only at an explained
+# sampling-boundary flip (see _explain_divergence)
+MIN_EXACT = {"golden_tiny": 6, "golden_tiny_eager": 4, "golden_tiny_window": 4}
+
+
+def _topk_agree(g, r, k, tol):
+    gv, gi = torch.topk(g.float(), k)
+    rv, ri = torch.topk(r.float(), k)
+    cut = min(gv[-1].item(), rv[-1].item())
+    sg = {int(i) for i, v in zip(gi, gv) if v.item() > cut + tol}
+    sr = {int(i) for i, v in zip(ri, rv) if v.item() > cut + tol}
+    return sg <= set(ri.tolist()) and sr <= set(gi.tolist())
+
+
+def _explain_divergence(cfg, c, gpu_logits, ref_logits, t, gpu_tok, oparams):
+    """First divergent step t of a free-running run (identical histories before t): the
+    GPU and reference logits agree within tolerance, the reference sampler returns the
+    reference token on the reference logits and the GPU token on the GPU logits (same
+    noise), and both tokens survive the top-k/top-p filter of BOTH logit rows -- i.e. the
+    divergence is a draw landing on a bf16 rounding difference, not a different model."""
+    import copy
+    from oracle.t5g_oracle import RowState, draw_noise, sample_helper, top_k_top_p_filtering
+    gen = torch.Generator().manual_seed(int(c["seed"]))
+    V = ref_logits.shape[-1]
+    for _ in range(t + 1):
+        noise = draw_noise(gen, V)
+    y = c["y"]
+    st = RowState(current_length=len(y) + 1 + t, prompt_offset=len(y) + 1, target_total=c["tgt"],
+                  first_input_len=len(c["x"]), cur_num_gen=t)
+    st.est_total = c["tgt"] + 1
+    hist = c["gen"][:t]
+    for i in range(len(hist)):   # silence-run state of the shared history
+        st.consec_silence = st.consec_silence + 1 if (hist[i] in c["silence_tokens"] and i > 0
+                                                      and hist[i] == hist[i - 1]) else 0
+    st.prev_token = hist[-1] if hist else -1
+    kw = dict(eos=cfg.eog_inference, encodec_sr=cfg.encodec_sr, extra_cutoff=cfg.extra_cutoff)
+    tg, _ = sample_helper(gpu_logits.clone(), oparams, copy.deepcopy(st), noise, **kw)
+    tr, _ = sample_helper(ref_logits.clone(), oparams, copy.deepcopy(st), noise, **kw)
+    scale = ref_logits.float().abs().max().item()
+    err = (gpu_logits.float() - ref_logits.float()).abs().max().item() / scale
+    surv = []
+    for lg in (gpu_logits, ref_logits):
+        x = lg.clone()
+        kk = oparams.top_k[min(len(oparams.top_k) - 1, t)] if isinstance(oparams.top_k, list) else oparams.top_k
+        if oparams.temperature != 1.0:
+            x = x / oparams.temperature
+        f = top_k_top_p_filtering(x, top_k=kk, top_p=oparams.top_p, min_p=oparams.min_p)
+        surv.append(set(torch.nonzero(torch.isfinite(f)).view(-1).tolist()))
+    ok = (tg == gpu_tok and tr == c["gen"][t] and err <= 0.02
+          and (gpu_tok == cfg.eog_inference or all(gpu_tok in s for s in surv))
+          and (c["gen"][t] == cfg.eog_inference or all(c["gen"][t] in s for s in surv)))
+    return ok, {"step": t, "gpu_token": gpu_tok, "ref_token": c["gen"][t], "rel_err": err}
+
+
 @pytest.mark.parametrize("name", ["golden_tiny", "golden_tiny_eager", "golden_tiny_window"])
 def test_tiny_engine_vs_reference_golden(name):
-    """Parity mode on the reference's golden cases: teacher-forced sampler exactness and
-    logit tolerance at every step; free-running token-exact rate reported."""
+    """Parity mode on the reference's golden cases (SURVEY §7 acceptance criteria):
+    (a) teacher-forced, the reference sampler on the GPU's logits returns the GPU's token
+        at every step, and the logits stay within 2 % of max |logit| of the oracle's;
+    (b) per-step top-k candidate sets agree with the reference's (ties within tolerance);
+    (c) free-running token equality with the reference on >= MIN_EXACT[name] cases, and
+        every other case diverges only at an explained sampling-boundary flip."""
     _need_gpu()
     from t5gemma_tts_amd.config import named_config
     from t5gemma_tts_amd.engine import Utterance
@@ -204,7 +263,8 @@ def test_tiny_engine_vs_reference_golden(name):
     cfg = named_config(meta["config"], **meta["config_kw"])
     sd = synthetic_weights(cfg, meta["weight_seed"])
     eng = _engine(cfg, sd, max_batch=8, max_text=64, max_audio=256, max_gen=200)
-    exact_tokens, worst, rows_exact, rows = 0, 0.0, 0, 0
+    exact_tokens, worst, rows_exact, rows, topk_ok, topk_n = 0, 0.0, 0, 0, 0, 0
+    divergences = []
     for ci, c in enumerate(meta["cases"]):
         u = Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"])
         out = eng.generate([u], _params(c), seeds=[c["seed"]], parity=True, record_logits=True)
@@ -213,13 +273,32 @@ def test_tiny_engine_vs_reference_golden(name):
         rows_exact += ex
         rows += len(out["gen"][0])
         g = out["gen"][0].tolist()
-        if g == c["gen"]:
+        ref = _bf16_from_bits(arrs[f"logits_{ci}"])
+        got = [l[0].cpu() for l in out["logits"]]
+        t_div = next((t for t in range(min(len(g), len(c["gen"]))) if g[t] != c["gen"][t]), None)
+        if t_div is None and len(g) != len(c["gen"]):
+            t_div = min(len(g), len(c["gen"]))
+        n_cmp = len(g) if t_div is None else t_div + 1
+        for t in range(min(n_cmp, ref.shape[0], len(got))):
+            topk_n += 1
+            topk_ok += int(_topk_agree(got[t], ref[t], 30, 0.02 * ref[t].float().abs().max().item()))
+        if t_div is None:
             exact_tokens += 1
-            ref = _bf16_from_bits(arrs[f"logits_{ci}"])
-            got = torch.stack([l[0].cpu() for l in out["logits"]])
-            assert got.shape == ref.shape
-    print(f"{name}: free-running token-exact {exact_tokens}/{len(meta['cases'])}; teacher-forced: "
-          f"max rel logit err {worst:.3g}, bit-identical logit rows {rows_exact}/{rows}")
+            assert len(got) == ref.shape[0]
+        else:
+            ok, info = _explain_divergence(cfg, c, got[t_div], ref[t_div], t_div, g[t_div], _oparams(c))
+            info["case"] = ci
+            divergences.append(info)
+            assert ok, info
+    rates = {"cases": len(meta["cases"]), "free_running_token_exact": exact_tokens,
+             "teacher_forced_max_rel_logit_err": worst, "bit_identical_logit_rows": rows_exact, "rows": rows,
+             "topk30_set_agree_steps": topk_ok, "topk_steps": topk_n, "divergences": divergences}
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", f"parity_{name}.json"), "w") as f:
+        json.dump(rates, f, indent=1)
+    print(name, json.dumps(rates))
+    assert topk_ok == topk_n, rates
+    assert exact_tokens >= MIN_EXACT[name], rates
 
 
 def test_batched_rows_equal_single_rows():
@@ -342,7 +421,7 @@ def test_sampler_kernel_vs_reference_golden():
             lg_h = logits.contiguous()
             nz_h = noise[0, 100].cpu().contiguous()
             assert L.t5g_host_sample(C.c_void_p(lg_h.data_ptr()), V, C.byref(row), tk, tk, C.byref(state),
-                                     C.c_void_p(nz_h.data_ptr()), cfg.eos, 10, 250.0, 0, 2000.0, 128,
+                                     C.c_void_p(nz_h.data_ptr()), cfg.eos, 10, 250.0, 0, 2000.0, 128, 4096,
                                      C.byref(hs), C.byref(ht)) == 0
             tok = ht.value
         if tok == c["token"]:

@@ -1,0 +1,192 @@
+"""Full-depth parity at the headline workload (BASELINE configs[2], C3): T5Gemma-TTS-2b-2b
+(26 + 26 layers, d 2304, 8 x 256 heads, FFN 9216, V 65 541), a batch of 8 voice-clone rows
+(T_x 60, T_p 151) on the GPU engine, against
+
+* ``golden_full``: the reference's own ``inference_tts`` (models/t5gemma.py, identical to
+  hf_export/modeling_t5gemma_voice.py:565-862) run in the build container on the same
+  seeded weights (tests/golden/make_golden.py ``gen_full_golden``): tokens, top-64 logits
+  and the sha of every full logit row, for 2 utterances x 16 steps;
+* the CPU oracle (oracle/t5g_oracle.py, pinned bitwise to those goldens) teacher-forced on
+  the GPU's token history: for the golden rows, and for one long row over its whole
+  generation (L = 152 .. 667 self-attention keys, up to 11 decode key chunks).
+
+Asserted at every step: the reference sampler fed the GPU logits (and the same noise)
+returns the GPU's token; GPU logits within ``RTOL`` of max |logit| of the oracle's; the
+top-30 candidate sets agree up to values tied within that tolerance. Match rates are
+written to gpurun_out/parity_full.json (copied to profiles/)."""
+import copy
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, REPO
+
+pytestmark = pytest.mark.gpu
+BF16 = torch.bfloat16
+RTOL = 0.03        # teacher-forced max |gpu - ref| / max |ref| per step (26+26 bf16 layers)
+TOPK = 30
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _load():
+    with open(os.path.join(GOLDEN, "golden_full.json")) as f:
+        meta = json.load(f)
+    return meta, dict(np.load(os.path.join(GOLDEN, "golden_full.npz")))
+
+
+def _long_rows(cfg, n, seed):
+    rng = np.random.default_rng(seed)
+    rows = []
+    for _ in range(n):
+        x = rng.integers(3, cfg.backbone.text_vocab_size - 1, size=60)
+        x[28] = cfg.x_sep_token
+        y = rng.integers(0, cfg.audio_vocab_size, size=150).tolist() + [cfg.y_sep_token]
+        rows.append(dict(x=[int(v) for v in x], y=[int(v) for v in y], tgt=len(y) + 500))
+    return rows
+
+
+def topk_agree(g, r, k, tol):
+    """Top-k index sets of g and r equal, except members whose value is within ``tol`` of
+    the k-th value (ties at the cut may legitimately swap)."""
+    gv, gi = torch.topk(g.float(), k)
+    rv, ri = torch.topk(r.float(), k)
+    cut = min(gv[-1].item(), rv[-1].item())
+    sg = {int(i) for i, v in zip(gi, gv) if v.item() > cut + tol}
+    sr = {int(i) for i, v in zip(ri, rv) if v.item() > cut + tol}
+    return sg <= set(ri.tolist()) and sr <= set(gi.tolist())
+
+
+def _write(name, payload):
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", name), "w") as f:
+        json.dump(payload, f, indent=1)
+
+
+@pytest.mark.timeout(1200)
+def test_c3_full_depth_batch8_vs_reference():
+    _need_gpu()
+    from oracle.t5g_oracle import SamplerParams as OP
+    from oracle.t5g_oracle import T5GemmaTTSOracle, draw_noise, sample_helper
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import SamplingParams, T5GemmaTTSEngine, Utterance
+    from t5gemma_tts_amd.weights import state_dict_digest, synthetic_weights
+
+    meta, arrs = _load()
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    assert state_dict_digest(sd) == meta["weight_sha256"], "weights differ from the golden run"
+    cases = meta["cases"]
+    golden_rows = {0: 0, 5: 1}             # batch row -> golden case
+    longs = _long_rows(cfg, 6, seed=20251226)
+    utts, seeds, ocases = [], [], []
+    li = 0
+    for b in range(8):
+        if b in golden_rows:
+            c = cases[golden_rows[b]]
+            utts.append(Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"]))
+            seeds.append(c["seed"])
+        else:
+            r = longs[li]
+            li += 1
+            utts.append(Utterance(x=r["x"], y=r["y"], tgt_y_len=r["tgt"]))
+            seeds.append(3000 + b)
+    p = dict(top_k=30, top_p=0.9, min_p=0.0, temperature=0.8, stop_repetition=3, silence_tokens=())
+    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=8, max_text=64, max_audio=151 + 1 + 520,
+                           max_gen=520)
+    out = eng.generate(utts, SamplingParams(**p), seeds=seeds, parity=True, record_logits=True)
+    logits = out["logits"]                 # per step: [8, V] on device
+    report = {"rtol": RTOL, "rows": {}}
+    orc = T5GemmaTTSOracle(cfg, sd)
+    op = OP(**p)
+
+    def teacher_forced(b, max_steps=None):
+        u = utts[b]
+        ctx = orc.prepare(u.x, u.y, u.tgt_y_len)
+        st = ctx["state"]
+        gen = torch.Generator().manual_seed(int(seeds[b]))
+        toks = out["gen"][b].tolist()
+        worst, exact_rows, topk_ok, ref_tok_same, n = 0.0, 0, 0, 0, 0
+        for t, tok in enumerate(toks):
+            if max_steps is not None and t >= max_steps:
+                break
+            lo = orc.step_logits(ctx)
+            lg = logits[t][b].cpu()
+            noise = draw_noise(gen, lo.shape[-1])
+            scale = lo.float().abs().max().item()
+            err = (lg.float() - lo.float()).abs().max().item() / max(scale, 1e-6)
+            worst = max(worst, err)
+            exact_rows += int(torch.equal(lg, lo))
+            topk_ok += int(topk_agree(lg, lo, TOPK, RTOL * scale))
+            st_g, st_r = copy.deepcopy(st), copy.deepcopy(st)
+            tok_g, _ = sample_helper(lg.clone(), op, st_g, noise, eos=cfg.eog_inference, encodec_sr=cfg.encodec_sr,
+                                     extra_cutoff=cfg.extra_cutoff)
+            tok_r, _ = sample_helper(lo.clone(), op, st_r, noise, eos=cfg.eog_inference, encodec_sr=cfg.encodec_sr,
+                                     extra_cutoff=cfg.extra_cutoff)
+            assert tok_g == tok, f"row {b} step {t}: reference sampler on GPU logits -> {tok_g}, GPU {tok}"
+            ref_tok_same += int(tok_r == tok)
+            n += 1
+            ctx["state"] = st = st_g
+            st.cur_num_gen += 1
+            st.current_length += 1
+            if tok == cfg.eog_inference:
+                break
+            orc.advance(ctx, tok)
+        return dict(steps=n, max_rel_err=worst, bit_identical_rows=exact_rows, topk_agree=topk_ok,
+                    ref_sampler_same_token=ref_tok_same, kv_len_max=len(utts[b].y) + 1 + n)
+
+    # golden rows: free-running vs the reference's tokens + teacher-forced vs the oracle
+    for b, ci in golden_rows.items():
+        c = cases[ci]
+        g = out["gen"][b].tolist()
+        prefix = 0
+        while prefix < min(len(g), len(c["gen"])) and g[prefix] == c["gen"][prefix]:
+            prefix += 1
+        top_idx, top_val = arrs[f"top_idx_{ci}"], torch.from_numpy(arrs[f"top_vals_{ci}"].astype(np.int16)).view(BF16)
+        gold_ok = 0
+        for t in range(min(prefix + 1, len(g), top_idx.shape[0])):   # same history up to step t
+            lg = logits[t][b].cpu()
+            ref_v = top_val[t].float()
+            got_v = lg[torch.from_numpy(top_idx[t]).long()].float()
+            scale = ref_v.abs().max().item()
+            assert (got_v - ref_v).abs().max().item() <= RTOL * scale, (b, t)
+            gv, gi = torch.topk(lg.float(), TOPK)
+            gset = set(gi.tolist())
+            rset = {int(i) for i, v in zip(top_idx[t][:TOPK], ref_v[:TOPK]) if v.item() > ref_v[TOPK - 1].item()
+                    + RTOL * scale}
+            gold_ok += int(rset <= gset)
+        tf = teacher_forced(b)
+        tf.update(golden_tokens_exact=g == c["gen"], golden_prefix_match=prefix, golden_steps=len(c["gen"]),
+                  golden_topk_agree=gold_ok)
+        report["rows"][f"golden_{ci}"] = tf
+        assert tf["max_rel_err"] <= RTOL and tf["topk_agree"] == tf["steps"], tf
+    # one long row, every step teacher-forced (attention over 152 .. 667 keys)
+    tf = teacher_forced(1)
+    report["rows"]["long_row1"] = tf
+    assert tf["steps"] > 400 and tf["max_rel_err"] <= RTOL, tf
+    assert tf["topk_agree"] >= tf["steps"] - 2, tf
+    # the other long rows: the reference sampler on the GPU's logits reproduces every token
+    from oracle.t5g_oracle import RowState
+    for b in (2, 3, 4, 6, 7):
+        u = utts[b]
+        st = RowState(current_length=len(u.y) + 1, prompt_offset=len(u.y) + 1, target_total=u.tgt_y_len,
+                      first_input_len=len(u.x))
+        st.est_total = u.tgt_y_len + 1
+        gen = torch.Generator().manual_seed(int(seeds[b]))
+        toks = out["gen"][b].tolist()
+        for t, tok in enumerate(toks):
+            noise = draw_noise(gen, cfg.n_audio_tokens)
+            tok_g, _ = sample_helper(logits[t][b].cpu().clone(), op, st, noise, eos=cfg.eog_inference,
+                                     encodec_sr=cfg.encodec_sr, extra_cutoff=cfg.extra_cutoff)
+            assert tok_g == tok, (b, t)
+            st.cur_num_gen += 1
+            st.current_length += 1
+        report["rows"][f"long_row{b}"] = {"steps": len(toks), "sampler_exact": True}
+    _write("parity_full.json", report)
+    print(json.dumps(report))

@@ -82,3 +82,30 @@ def test_inference_batch_rows_match_single_runs():
         if f.numel():
             assert _rms(w, xc2_oracle.decode(csd, f.view(1, -1), ccfg)[0]) <= 1e-4
     assert stats["tokens"] > 0 and stats["t_codec"] > 0
+
+
+def test_drop_in_inference_tts_global_rng_contract():
+    """The reference seeds torch's global generator (seed_everything,
+    inference_commandline_hf.py:62-69, 95) and every AR step's torch.multinomial draws
+    from it (hf_export/modeling_t5gemma_voice.py:137). The drop-in inference_tts with
+    its default arguments must do the same: the tokens equal the engine's run on the
+    stream torch.manual_seed(s) starts (the reference's, pinned by the tiny goldens), and
+    the global generator ends where the reference leaves it (one V-draw per step)."""
+    from t5gemma_tts_amd.engine import SamplingParams, Utterance, consume_noise
+    cfg, sd, model, *_ = _setup()
+    V = cfg.n_audio_tokens
+    for seed, x, y, tgt in [(5, [5, 17, 301, 44, 9], [3, 60, cfg.y_sep_token], 24),
+                            (77, [8, 9, 10, 11, 12, 13, 14], [], 18)]:
+        kw = dict(top_k=30, top_p=0.9, min_p=0.0, temperature=0.8, stop_repetition=3, silence_tokens=[])
+        torch.manual_seed(seed)
+        res, gen = model.inference_tts(torch.tensor([x]), torch.tensor([len(x)]),
+                                       torch.tensor(y, dtype=torch.long).view(1, -1, 1),
+                                       tgt_y_lens=torch.tensor([tgt]), prompt_frames=len(y), **kw)
+        after = torch.rand(3)
+        ref = model.engine.generate([Utterance(x=x, y=y, tgt_y_len=tgt)], SamplingParams(**kw), seeds=[seed],
+                                    parity=True)
+        assert gen.view(-1).tolist() == ref["gen"][0].tolist()
+        assert res.view(-1).tolist() == y + ref["gen"][0].tolist()
+        torch.manual_seed(seed)
+        consume_noise(torch.default_generator, gen.shape[-1], V)
+        assert torch.equal(torch.rand(3), after)

@@ -98,7 +98,7 @@ def test_device_sampler_equals_host_reference(mode):
             nh = noise[b, 100].contiguous()
             _lib.check(eng.L.t5g_host_sample(C.c_void_p(lh.data_ptr()), V, C.byref(rows[b]), tk, tk,
                                              C.byref(sts[b]), C.c_void_p(nh.data_ptr()), EOS, 10, 250.0, 0, 2000.0,
-                                             128, C.byref(hs), C.byref(ht)), "host")
+                                             128, 4096, C.byref(hs), C.byref(ht)), "host")
             if flags[b] & 1:
                 amb += 1
                 continue

@@ -63,7 +63,7 @@ def test_host_sampler_matches_reference_golden():
         tok = C.c_int32()
         tk = (C.c_int32 * 1)()
         rc = L.t5g_host_sample(C.c_void_p(logits.data_ptr()), V, C.byref(row), tk, tk, C.byref(st),
-                               C.c_void_p(noise.data_ptr()), 65539, 10, 250.0, 0, 2000.0, 4096,
+                               C.c_void_p(noise.data_ptr()), 65539, 10, 250.0, 0, 2000.0, 4096, 4096,
                                C.byref(out), C.byref(tok))
         assert rc == 0
         assert tok.value == c["token"], c

@@ -92,11 +92,13 @@ def test_inference_one_sample_call_sequence():
     dc = {"top_k": 30, "top_p": 0.9, "min_p": 0.0, "temperature": 0.8, "stop_repetition": 3, "codec_sr": 50,
           "silence_tokens": "[1, 2]", "sample_batch_size": 1}
     cs, gs, cf, gf = inference_one_sample(model, cfg, None, codec, [3, 4, 5, 6], [20, 21], None, "cpu", dc,
-                                          prompt_end_frame=3, target_generation_length=2.0, prefix_transcript=[9],
+                                          prompt_end_frame=800, target_generation_length=2.0, prefix_transcript=[9],
                                           quiet=True, return_frames=True)
     x, xl, y, tgt, kw = model.calls[0]
     assert x.tolist() == [[9, cfg.x_sep_token, 20, 21]] and xl.tolist() == [4]
-    assert y[0, :, 0].tolist() == [3, 4, 5, cfg.y_sep_token]           # truncated to prompt_end_frame
+    # prompt_end_frame counts audio SAMPLES (inference_commandline_hf.py:181): 800 samples at
+    # 16 kHz encode to 800 // 320 + 1 = 3 codes
+    assert y[0, :, 0].tolist() == [3, 4, 5, cfg.y_sep_token]
     assert tgt.tolist() == [4 + 100]
     assert kw["prompt_frames"] == 4 and kw["silence_tokens"] == [1, 2] and kw["top_k"] == 30
     assert cf.tolist() == [[[3, 4, 5, 7, 8, 9]]] and gf.tolist() == [[[7, 8, 9]]]
@@ -109,3 +111,24 @@ def test_inference_one_sample_call_sequence():
     with pytest.raises(AssertionError):
         inference_one_sample(model2, cfg, None, codec2, None, [20], None, "cpu", dict(dc, sample_batch_size=2), 0,
                              1.0, quiet=True)
+
+
+def test_prompt_end_frame_is_a_sample_count():
+    """0.05 s of a 44.1 kHz file (2205 samples) -> 800 samples at 16 kHz -> 3 codes; the
+    reference's default cut_off_sec = 100 keeps every code of a short prompt."""
+    from t5gemma_tts_amd.pipeline import prompt_frames_for_samples
+    assert prompt_frames_for_samples(2205, 44100) == 3
+    assert prompt_frames_for_samples(800, 16000) == 3
+    assert prompt_frames_for_samples(639, 16000) == 2
+    assert prompt_frames_for_samples(0, 16000) == 1
+    cfg = config_tiny()
+    model, codec = FakeModel(cfg), FakeCodec()
+    dc = {"top_k": 30, "top_p": 0.9, "temperature": 0.8, "codec_sr": 50}
+    inference_one_sample(model, cfg, None, codec, list(range(10)), [20], None, "cpu", dc,
+                         prompt_end_frame=2205, target_generation_length=1.0, quiet=True, prompt_sample_rate=44100)
+    assert model.calls[0][2][0, :, 0].tolist() == [0, 1, 2, cfg.y_sep_token]
+    model, codec = FakeModel(cfg), FakeCodec()
+    inference_one_sample(model, cfg, None, codec, list(range(10)), [20], None, "cpu", dc,
+                         prompt_end_frame=int(100 * 44100), target_generation_length=1.0, quiet=True,
+                         prompt_sample_rate=44100)
+    assert model.calls[0][2][0, :, 0].tolist() == list(range(10)) + [cfg.y_sep_token]
