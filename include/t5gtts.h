@@ -30,7 +30,6 @@ extern "C" {
 #define T5G_EUNSUPPORTED (-3)
 #define T5G_ENOMEM (-4)
 #define T5G_ECAPACITY (-5)   /* exceeds engine capacity (max_batch / max_text / max_audio) */
-#define T5G_ESYNC (-6)       /* an in-launch row hand-off poll gave up (decode results invalid) */
 
 #define T5G_MAX_LAYERS 64
 
@@ -72,14 +71,6 @@ typedef struct {
     const void* cross_kv;  /* decoder only: packed [2 kv_dim][hidden]: k_proj | v_proj */
     const void* cross_o;   /* decoder only: packed [hidden][q_dim] */
     const void* norms[6];  /* bf16 [hidden]: pre_self, post_self, pre_cross, post_cross, pre_ff, post_ff */
-    /* decoder only, optional (NULL: unused): plain row-major bf16 copies read by the
-     * decode-step VALU GEMVs (csrc/gemv.hip gemv_rm_kernel) */
-    const void* rm_qkv;      /* [q_dim + 2 kv_dim][hidden] */
-    const void* rm_o;        /* [hidden][q_dim] */
-    const void* rm_gate_up;  /* [2 inter][hidden]: gate rows, then up rows */
-    const void* rm_down;     /* [hidden][inter] */
-    const void* rm_cross_q;  /* [q_dim][hidden] */
-    const void* rm_cross_o;  /* [hidden][q_dim] */
 } t5g_layer_weights;
 
 typedef struct {
@@ -94,7 +85,6 @@ typedef struct {
     const float* inv_freq;       /* fp32 [head_dim/2] RoPE inverse frequencies */
     const t5g_layer_weights* enc_layers;  /* host array [n_enc_layers] */
     const t5g_layer_weights* dec_layers;  /* host array [n_dec_layers] */
-    const void* rm_head1;        /* optional row-major [hidden][hidden] copy of head1 */
 } t5g_weights;
 
 /* Per-utterance sampler parameters (topk_sampling args, :744-750). */
@@ -173,8 +163,7 @@ int t5g_sampler_setup(t5g_engine* e, int32_t B, const t5g_sampler_row* rows, con
  * one iteration. Asynchronous. */
 int t5g_decode(t5g_engine* e, int32_t n_steps, int32_t use_graph, void* stream);
 
-/* Synchronous readback: state[B] and tokens [B][max_gen] (host buffers).
- * t5g_read_tokens returns T5G_ESYNC if a decode launch's bounded row-flag poll gave up. */
+/* Synchronous readback: state[B] and tokens [B][max_gen] (host buffers). */
 int t5g_read_state(t5g_engine* e, t5g_sampler_state* state_out, int32_t B, void* stream);
 int t5g_read_tokens(t5g_engine* e, int32_t* tokens_out, int32_t B, void* stream);
 /* Host write of one row's state (parity-mode correction of an ambiguous step). */
@@ -217,37 +206,32 @@ int t5g_time_gemm(const void* X_dev, int32_t ldx, int32_t M, const void* const* 
                   float* avg_us);
 int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, float* avg_us);
 
-/* Decode-step GEMV with the row prologue fused in (csrc/gemv.hip; M <= 16 rows).
- * Replaces, per decoder sub-block, the reference's F.linear plus the RMSNorm /
- * residual wiring in front of it (PMDecoderLayer.forward :285-323,
- * [tf] T5GemmaRMSNorm :61-78):
- *   pro 0 (rows):  X = X                                     (staged through LDS)
- *   pro 1 (norm):  h' = bf16(h_in + RMSNorm_post(v)), X = RMSNorm_pre(h')
- *   pro 2 (embed): h' = bf16(table[ids] * scale),     X = RMSNorm_pre(h')
- *   pro 3 (direct): X = X read straight from L2 beside the weight stream
- * then Y = X . W^T (packed W) with epilogue epi (as t5g_gemm, no split-K).
- * Block 0 writes h' to h_out and X to x_out when those are non-NULL. */
+/* Decode-step GEMV (csrc/gemv.hip; M <= 16 rows): Y = X . W^T on a packed W with
+ * epilogue epi (as t5g_gemm: 0 bf16, 1 +bias bf16, 3 GeGLU(tanh), 4 fp32 split-K slabs),
+ * X rows staged through LDS, at most one workgroup per CU -- the kernel the decode step
+ * runs its gate/up projection on ([tf] T5GemmaMLP :81-97). Fields marked "reserved" must
+ * be 0 / NULL (the fused-prologue variants measured slower in round 1 were removed). */
 typedef struct {
     int32_t M, K, N;
-    int32_t epi, pro, nw;     /* nw: waves per block, 4 / 8 / 16 */
+    int32_t epi, pro, nw;     /* pro: reserved (0); nw: waves per block, 4 / 8 / 16 (GeGLU 4 / 8) */
     const void* W;            /* packed [N][K] */
-    const void* bias;         /* bf16 [N] (epi 1, 2) */
+    const void* bias;         /* bf16 [N] (epi 1) */
     void* Y;                  /* bf16 or fp32 [M][ldy] */
     int32_t ldy, ldx;
-    const void* X;            /* bf16 [M][ldx] (pro 0, 3) */
-    const void* v;            /* bf16 [M][K] (pro 1) */
-    const void* h_in;         /* bf16 [M][K] (pro 1) */
-    const int32_t* ids;       /* [M] (pro 2) */
-    const void* table;        /* bf16 [vocab][K] (pro 2) */
-    float scale, eps;
-    const void* post_w;       /* bf16 [K] (pro 1) */
-    const void* pre_w;        /* bf16 [K] (pro 1, 2) */
-    void* h_out;              /* bf16 [M][K] or NULL */
-    void* x_out;              /* bf16 [M][K] or NULL */
+    const void* X;            /* bf16 [M][ldx] */
+    const void* v;            /* reserved */
+    const void* h_in;         /* reserved */
+    const int32_t* ids;       /* reserved */
+    const void* table;        /* reserved */
+    float scale, eps;         /* reserved */
+    const void* post_w;       /* reserved */
+    const void* pre_w;        /* reserved */
+    void* h_out;              /* reserved */
+    void* x_out;              /* reserved */
     int32_t un;               /* tuning: fragments in flight per wave (8 / 16), 0 = default */
     int32_t max_grid;         /* tuning: blocks per launch cap, 0 = one per CU */
-    int32_t splits;           /* split-K (epi 4 with pro 0/3): fp32 slabs [splits][M][ldy]; 0/1 = none */
-    int32_t layout;           /* 0: W packed P16 (MFMA); 1: W plain row-major (VALU, M <= 8; GeGLU: gate then up rows) */
+    int32_t splits;           /* split-K (epi 4): fp32 slabs [splits][M][ldy]; 0/1 = none */
+    int32_t layout;           /* reserved (0: W packed P16) */
 } t5g_gemv_args;
 int t5g_gemv(const t5g_gemv_args* args, void* stream);
 /* hipEvent-timed `iters` launches rotating over packed weights Wp_list[i % n_w]

@@ -13,7 +13,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("T5G_LIB", os.path.join(_PKG, "lib", "libt5gtts.so"))
 MAX_LAYERS = 64
 
-T5G_ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "EUNSUPPORTED", -4: "ENOMEM", -5: "ECAPACITY", -6: "ESYNC"}
+T5G_ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "EUNSUPPORTED", -4: "ENOMEM", -5: "ECAPACITY"}
 
 
 class T5GError(RuntimeError):
@@ -46,17 +46,14 @@ class Config(C.Structure):
 class LayerWeights(C.Structure):
     _fields_ = [("qkv", C.c_void_p), ("o", C.c_void_p), ("gate_up", C.c_void_p), ("down", C.c_void_p),
                 ("cross_q", C.c_void_p), ("cross_kv", C.c_void_p), ("cross_o", C.c_void_p),
-                ("norms", C.c_void_p * 6), ("rm_qkv", C.c_void_p), ("rm_o", C.c_void_p),
-                ("rm_gate_up", C.c_void_p), ("rm_down", C.c_void_p), ("rm_cross_q", C.c_void_p),
-                ("rm_cross_o", C.c_void_p)]
+                ("norms", C.c_void_p * 6)]
 
 
 class Weights(C.Structure):
     _fields_ = [("enc_embed", C.c_void_p), ("audio_embed", C.c_void_p), ("enc_final_norm", C.c_void_p),
                 ("dec_final_norm", C.c_void_p), ("head1", C.c_void_p), ("head1_bias", C.c_void_p),
                 ("head2", C.c_void_p), ("head2_bias", C.c_void_p), ("inv_freq", C.c_void_p),
-                ("enc_layers", C.POINTER(LayerWeights)), ("dec_layers", C.POINTER(LayerWeights)),
-                ("rm_head1", C.c_void_p)]
+                ("enc_layers", C.POINTER(LayerWeights)), ("dec_layers", C.POINTER(LayerWeights))]
 
 
 class SamplerRow(C.Structure):

@@ -80,11 +80,8 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
     dst[i + H2] = f2bf(o2);
 }
 
-__global__ void rope_table_kernel(const float* pos, const float* inv_freq, int D, float* tab, unsigned* epoch) {
+__global__ void rope_table_kernel(const float* pos, const float* inv_freq, int D, float* tab) {
     const int r = blockIdx.x, H2 = D / 2;
-    // the decode step's first kernel also advances the step epoch that the PRO_LEAD row
-    // hand-offs of this step publish and poll (gemv.hip): no per-step flag reset
-    if (epoch && r == 0 && threadIdx.x == 0) *epoch = *epoch + 1u == 0u ? 1u : *epoch + 1u;
     for (int i = threadIdx.x; i < H2; i += blockDim.x) {
         const float ang = inv_freq[i] * pos[r];
         tab[(long)r * D + i] = rbf(cosf(ang));
@@ -92,10 +89,9 @@ __global__ void rope_table_kernel(const float* pos, const float* inv_freq, int D
     }
 }
 
-int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st,
-               unsigned* epoch) {
+int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st) {
     if (rows <= 0) return 0;
-    hipLaunchKernelGGL(rope_table_kernel, dim3((unsigned)rows), dim3(128), 0, st, pos, inv_freq, D, tab, epoch);
+    hipLaunchKernelGGL(rope_table_kernel, dim3((unsigned)rows), dim3(128), 0, st, pos, inv_freq, D, tab);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -111,16 +107,29 @@ int rope_store(const RopeArgs& a, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
+// Many-query attention (encoder self attention, decoder prefill self / cross attention,
+// eager decode): one block per (query, kv head) over all of the row's keys, the G query
+// heads of the GQA group sharing every K/V row read. ``sdpa`` numerics follow aten's CPU
+// flash attention (common.h sdpa_*): kv blocks of 512 keys with a running max, the fast
+// exp on each block's 16-multiple prefix, lane-ordered sums, bf16 P before P.V, output
+// scaled by 1/l; a causal row t sees its q-block's key range (sdpa_qsplit). ``eager``
+// mirrors eager_attention_forward (bf16 scores, tanh softcap, bf16 normalised probs).
+constexpr int SDPA_KV_BLOCK = 512;
+constexpr int SDPA_MAX_BLOCKS = 8;   // kv_cap <= 4096
+
 template <int D, int G, bool EAGER>
 __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     constexpr int LPK = D / 8;        // lanes per key row
     constexpr int KPW = 64 / LPK;     // keys per wave instruction
     constexpr int KPB = KPW * 4;      // keys per block iteration
+    static_assert(SDPA_KV_BLOCK % KPB == 0, "kv blocks must hold whole key groups");
     extern __shared__ __attribute__((aligned(16))) float sm[];  // [G][chunk] scores, then probs
     __shared__ float red[32];
     __shared__ f32x4 ored[4][G][64][2];
+    __shared__ float blk_et[G][SDPA_MAX_BLOCKS];
+    __shared__ float stat_l[G];
 
-    const int qi = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+    const int qi = blockIdx.x, kvh = blockIdx.y;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int kg = lane / LPK, dl = lane % LPK;
     const int row = a.q_row ? a.q_row[qi] : qi;
@@ -134,19 +143,14 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
         lo = max(0, t - a.window);
         hi = min(len, t + a.window + 1);
     }
-    const int c0 = lo + sp * a.chunk;
-    const int c1 = min(hi, c0 + a.chunk);
-    const int n = c1 - c0;
-
-    float* part = a.part ? a.part + (((long)qi * a.Hkv + kvh) * a.nsplit + sp) * (G * (D + 2)) : nullptr;
-    if (n <= 0) {
-        if (a.nsplit > 1 && threadIdx.x < G) {
-            part[threadIdx.x * (D + 2)] = -INFINITY;
-            part[threadIdx.x * (D + 2) + 1] = 0.f;
-        }
-        return;
+    const int n = hi - lo;
+    if (n <= 0) return;
+    // keys in aten's blocks for this row: a causal row sees its q-block's range
+    int nk = hi;
+    if (a.causal && a.window == 0) {
+        const int qs = sdpa_qsplit(len);
+        nk = min(t - t % qs + qs, len);
     }
-    // q fragment: 8 dims per lane per head
     float q[G][8];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -161,12 +165,12 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
 
     // ---- scores
-    for (int j0 = c0; j0 < c1; j0 += KPB) {
+    for (int j0 = lo; j0 < hi; j0 += KPB) {
         const int j = j0 + wave * KPW + kg;
         float s[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) s[g] = 0.f;
-        if (j < c1) {
+        if (j < hi) {
             u32x4 w = *(const u32x4*)(Kb + (long)j * D + 8 * dl);
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
@@ -180,7 +184,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 #pragma unroll
             for (int o = LPK / 2; o > 0; o >>= 1) s[g] += __shfl_xor(s[g], o, 64);
         }
-        if (dl == 0 && j < c1) {
+        if (dl == 0 && j < hi) {
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 float v;
@@ -188,32 +192,56 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
                     v = rbf(rbf(s[g]) * a.scale);
                     if (a.softcap > 0.f) v = rbf(rbf(tanhf(rbf(v / a.softcap))) * a.softcap);
                 } else {
-                    v = s[g] * a.scale;
+                    v = __fmul_rn(s[g], a.scale);
                 }
-                sm[g * a.chunk + (j - c0)] = v;
+                sm[g * a.chunk + (j - lo)] = v;
             }
         }
     }
     __syncthreads();
-    // ---- softmax statistics
-    float mx[G], sum[G];
+    // ---- softmax
+    if constexpr (EAGER) {
+        // softmax(fp32) over the row, normalised probabilities rounded to bf16
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        float lm = -INFINITY;
-        for (int i = threadIdx.x; i < n; i += 256) lm = fmaxf(lm, sm[g * a.chunk + i]);
-        mx[g] = block_max(lm, red);
-        float ls = 0.f;
-        for (int i = threadIdx.x; i < n; i += 256) ls += expf(sm[g * a.chunk + i] - mx[g]);
-        sum[g] = block_sum(ls, red);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const float inv = 1.0f / sum[g];
-        for (int i = threadIdx.x; i < n; i += 256) {
-            float e = expf(sm[g * a.chunk + i] - mx[g]);
-            sm[g * a.chunk + i] = EAGER ? rbf(e * inv) : rbf(e);
+        for (int g = 0; g < G; ++g) {
+            float lm = -INFINITY;
+            for (int i = threadIdx.x; i < n; i += 256) lm = fmaxf(lm, sm[g * a.chunk + i]);
+            const float mx = block_max(lm, red);
+            float ls = 0.f;
+            for (int i = threadIdx.x; i < n; i += 256) ls += expf(sm[g * a.chunk + i] - mx);
+            const float inv = 1.0f / block_sum(ls, red);
+            __syncthreads();
+            for (int i = threadIdx.x; i < n; i += 256) sm[g * a.chunk + i] = rbf(expf(sm[g * a.chunk + i] - mx) * inv);
         }
+    } else if (wave < G) {
+        // one wave per query head, block by block (running max, lane-ordered sums)
+        const int g = wave;
+        float* sg = sm + g * a.chunk;
+        float m = -INFINITY, l = 0.f;
+        int b = 0;
+        for (int bs = lo; bs < nk; bs += SDPA_KV_BLOCK, ++b) {
+            const int blen = min(SDPA_KV_BLOCK, nk - bs);
+            const int bhi = min(bs + blen, hi);   // keys past hi are masked (p = 0)
+            float lm = -INFINITY;
+            for (int i = bs + lane; i < bhi; i += 64) lm = fmaxf(lm, sg[i - lo]);
+            const float mn = fmaxf(m, wave_max(lm));
+            auto pf = [&](int pos) -> float {
+                return bs + pos < bhi ? sdpa_p(__fsub_rn(sg[bs + pos - lo], mn), pos, blen) : 0.f;
+            };
+            const float ts = sdpa_block_sum(blen, lane, pf);
+            const float et = sdpa_block_rescale(m, mn);
+            l = fmaf(et, l, ts);
+            // this wave's lanes all finished reading the block's scores before any writes
+            float pw[SDPA_KV_BLOCK / 64];
+#pragma unroll
+            for (int k = 0; k < SDPA_KV_BLOCK / 64; ++k) pw[k] = pf(lane + 64 * k);
+#pragma unroll
+            for (int k = 0; k < SDPA_KV_BLOCK / 64; ++k)
+                if (bs + lane + 64 * k < bhi) sg[bs + lane + 64 * k - lo] = rbf(pw[k]);
+            if (lane == 0) blk_et[g][b] = et;
+            m = mn;
+        }
+        if (lane == 0) stat_l[g] = l;
     }
     __syncthreads();
     // ---- P.V: lane owns dims [8*dl, 8*dl+8) of key group kg
@@ -222,13 +250,22 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
-    for (int j0 = c0; j0 < c1; j0 += KPB) {
+    for (int j0 = lo; j0 < hi; j0 += KPB) {
+        if (!EAGER && j0 > lo && (j0 - lo) % SDPA_KV_BLOCK == 0) {
+            // a new kv block: dst *= expf(m_old - m_new) (aten rescales before adding P.V)
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float et = blk_et[g][(j0 - lo) / SDPA_KV_BLOCK];
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) o[g][jj] *= et;
+            }
+        }
         const int j = j0 + wave * KPW + kg;
-        if (j < c1) {
+        if (j < hi) {
             u32x4 w = *(const u32x4*)(Vb + (long)j * D + 8 * dl);
 #pragma unroll
             for (int g = 0; g < G; ++g) {
-                float p = sm[g * a.chunk + (j - c0)];
+                float p = sm[g * a.chunk + (j - lo)];
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     o[g][2 * jj] += p * bf_lo(w[jj]);
@@ -253,109 +290,43 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
         }
     }
     __syncthreads();
-    // final: thread t handles (g, dl) pairs
     for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
         const int g = idx / LPK, d8 = idx % LPK;
         f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
         f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
         float v[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-        if (a.nsplit > 1) {
-            float* pg = part + g * (D + 2);
-            if (d8 == 0) {
-                pg[0] = mx[g];
-                pg[1] = sum[g];
-            }
+        const float inv = EAGER ? 1.0f : __fdiv_rn(1.0f, stat_l[g]);
+        u32x4 w;
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) pg[2 + 8 * d8 + jj] = v[jj];
-        } else {
-            const float inv = EAGER ? 1.0f : 1.0f / sum[g];
-            u32x4 w;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) w[jj] = pack2(v[2 * jj] * inv, v[2 * jj + 1] * inv);
-            *(u32x4*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 8 * d8) = w;
-        }
+        for (int jj = 0; jj < 4; ++jj) w[jj] = pack2(__fmul_rn(v[2 * jj], inv), __fmul_rn(v[2 * jj + 1], inv));
+        *(u32x4*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 8 * d8) = w;
     }
 }
 
-// Decode-shaped attention (one query row per (row, kv head)): 64 keys per block,
-// every K and V row of the block is requested before the first use (16 B per lane,
-// NIT loads of each in flight), softmax statistics by one wave per head.
-// Fusions: (1) q may come straight from the q-projection's fp32 split-K slabs; the
-// block sums them, rounds to bf16 and applies the float-position PM-RoPE with a
-// lane shuffle (rotate_half partner = lane ^ LPK/2), bit-identical to
-// rope_store_kernel; (2) the key-split partials are merged in the same launch by
-// the last-arriving block of each (row, kv head) (agent-scope release/acquire
-// ticket, CDNA guide G16), so no combine launch.
-template <int D, int G>
-__device__ __forceinline__ void merge_splits(const AttnArgs& a, const float* base, int qi, int kvh, float* wz,
-                                             float* Linv, int q0 = 0, int nq = G * D / 4) {
-    constexpr int ZMAX = 16;  // splits held in registers; more are streamed
-    const int S = a.nsplit;
-    // Slabs are read with sc1 loads (L1 bypass): in the in-launch merge they were
-    // written moments ago by other workgroups with sc1 (write-through) stores, the
-    // CDNA guide G16 row-1 hand-off (no acquire fence needed).
-    const __amdgpu_buffer_rsrc_t rs = frag_rsrc(base, (uint32_t)S * G * (D + 2) * 4u);
-    auto ld4 = [&](int off) __attribute__((always_inline)) {
-        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off * 4, 0, 16));
-    };
-    auto ld1 = [&](int off) __attribute__((always_inline)) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off * 4, 0, 16));
-    };
-    // thread idx owns (g, d4) quad q0 + idx of this block's nq quads (all G*D/4 of them in
-    // the in-launch merge; a slice of them per combine block)
-    const int idx = threadIdx.x;
-    const bool own = idx < nq;
-    const int quad = q0 + (own ? idx : 0);
-    const int g = quad / (D / 4), d4 = quad % (D / 4);
-    f32x4 pv[ZMAX];
-#pragma unroll
-    for (int z = 0; z < ZMAX; ++z)
-        if (own && z < S) pv[z] = ld4(z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
-    if (threadIdx.x < 64 * G) {
-        const int gg = threadIdx.x / 64, z = threadIdx.x % 64;
-        const float m = z < S ? ld1(z * G * (D + 2) + gg * (D + 2)) : -INFINITY;
-        const float l = z < S ? ld1(z * G * (D + 2) + gg * (D + 2) + 1) : 0.f;
-        const float M = wave_max(m);
-        const float w = (m == -INFINITY) ? 0.f : expf(m - M);
-        const float L = wave_sum(w * l);
-        wz[gg * 64 + z] = w;
-        if (z == 0) Linv[gg] = 1.0f / L;
-    }
-    __syncthreads();
-    if (!own) return;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int z = 0; z < ZMAX; ++z)
-        if (z < S) {
-            const float w = wz[g * 64 + z];
-            if (w != 0.f) acc += w * pv[z];
-        }
-    for (int z = ZMAX; z < S; ++z) {
-        const float w = wz[g * 64 + z];
-        if (w != 0.f) acc += w * ld4(z * G * (D + 2) + g * (D + 2) + 2 + 4 * d4);
-    }
-    const float inv = Linv[g];
-    uint2 o;
-    o.x = pack2(acc[0] * inv, acc[1] * inv);
-    o.y = pack2(acc[2] * inv, acc[3] * inv);
-    *(uint2*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 4 * d4) = o;
-}
-
+// ---------------------------------------------------------------------------
+// Decode attention (one query row per (row, kv head), sdpa numerics): the row's keys
+// [lo, hi) are cut into 64-key chunks from lo, one workgroup each, so aten's 512-key
+// blocks are whole chunk groups.
+//  * attn_decode_kernel: q straight from the projection's fp32 split-K slabs (summed,
+//    rounded, PM-RoPE'd in-kernel), the step's own k/v appended to the cache by the
+//    chunk holding t, scores of the chunk. A row of <= 64 keys is finished here (softmax,
+//    P.V, output). Longer rows publish scores + chunk maxima for:
+//  * attn_pv_kernel: the chunk's p against its block's running max (known only once
+//    every chunk of the block has its scores), bf16 P, partial P.V;
+//  * attn_combine_kernel: l with aten's lane-ordered block sums, the partial P.V summed
+//    per block, rescaled across blocks, scaled by 1/l.
 constexpr int QSMAX = 4;   // q / appended-k/v projection slabs read by the decode kernel
+constexpr int DCH = 64;    // keys per decode chunk
 
 template <int D, int G>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
-    constexpr int CH = 64;
     constexpr int LPK = D / 8;
     constexpr int KPW = 64 / LPK;
     constexpr int KPB = KPW * 4;
-    constexpr int NIT = CH / KPB;
-    __shared__ float sm[G][CH];
-    __shared__ float stat[G][2];
+    constexpr int NIT = DCH / KPB;
+    __shared__ float sm[G][DCH];
+    __shared__ float stat_l[G];
     __shared__ f32x4 ored[4][G][LPK][2];
-    __shared__ float wz[G * 64];
-    __shared__ float Linv[G];
-    __shared__ int last_flag;
     __shared__ float qs[G][D];
     __shared__ float kvnew[2][D];   // appended key (pre-RoPE) / value of position t
 
@@ -376,28 +347,20 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         lo = max(0, t - a.window);
         hi = min(len, t + a.window + 1);
     }
-    // The row's keys [lo, hi) are split into nsplit equal chunks (<= CH keys each, since
-    // nsplit * CH >= kv_cap): every block streams the same share whatever the row length,
-    // and no block loads keys past it (the old fixed 64-key chunks streamed whole chunks
-    // for blocks past the length: 31 MB instead of 17 MB per layer at L = 527). A row of
-    // <= CH keys stays one chunk (one softmax pass, no merge: closest to the reference's
-    // single-pass sdpa on short rows).
     const int span = max(hi - lo, 0);
-    const int chunk = span <= CH ? span : (span + a.nsplit - 1) / a.nsplit;
-    const int c0 = lo + sp * chunk;
-    const int c1 = min(hi, c0 + chunk);
+    const bool single = span <= DCH;     // the whole row is chunk 0: finished in this kernel
+    const int c0 = lo + sp * DCH;
+    const int c1 = min(hi, c0 + DCH);
     const int n = c1 - c0;
     // the block whose keys include t appends the step's own key/value (a.append)
     const bool has_t = a.append && a.Qpart && t >= c0 && t < c1;
     const bf16_t* Kb = a.K + row * a.kv_bstride + kvh * a.kv_hstride;
     const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
     // Issue order = wait order (vmcnt is in-order): first what the q path needs (the
-    // projection's split-K slabs, the PM-RoPE table), then the K/V stream, so q can be
-    // summed, staged and rotated while K/V are still in flight. All loads are
-    // unconditional (clamped addresses): a load under a branch makes the compiler
-    // wait for everything in flight at the join.
-    // Thread roles in the slab stage: quads [0, G*D/4) are q, the next 2*D/4 the
-    // appended k and v (block holding key t only); the rest re-read quad 0.
+    // projection's split-K slabs, the PM-RoPE table), then the K (and, for a single-chunk
+    // row, V) stream, so q can be summed, staged and rotated while they are in flight.
+    // All loads are unconditional (clamped addresses): a load under a branch makes the
+    // compiler wait for everything in flight at the join.
     f32x4 u[QSMAX];
     int role = -1, c4 = 0, g_own = 0;
     if (a.Qpart) {
@@ -418,8 +381,6 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         for (int s = 0; s < QSMAX; ++s)
             u[s] = *(const f32x4*)(a.Qpart + ((long)min(s, a.q_nsplit - 1) * a.Mq + qi) * a.ldqp + col);
     }
-    // this lane's 8 cos / 8 sin of the row's PM-RoPE table (dims 8*dl .. 8*dl+7 never wrap
-    // D/2): four 16-B loads
     float c8[8], s8[8];
     if (a.rope_tab) {
         const float* tr = a.rope_tab + (long)row * D + (8 * dl) % (D / 2);
@@ -433,9 +394,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             s8[4 + jj] = sb[jj];
         }
     }
-    // K/V of the block's keys, requested right behind the q slabs: buffer loads, keys
-    // past c1 fall outside the descriptor (zeros, no traffic) -- no branch, so the
-    // compiler keeps one in-order wait per use
+    // buffer loads: keys past c1 (and V of multi-chunk rows) fall outside the descriptor
+    // (zeros, no traffic) -- no branch
     const __amdgpu_buffer_rsrc_t krs = frag_rsrc(Kb, (uint32_t)a.kv_cap * D * 2u);
     const __amdgpu_buffer_rsrc_t vrs = frag_rsrc(Vb, (uint32_t)a.kv_cap * D * 2u);
     u32x4 kr[NIT], vr[NIT];
@@ -444,7 +404,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         const int j = c0 + i * KPB + wave * KPW + kg;
         const int off = j < c1 ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
         kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
-        vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
+        vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, single ? off : (int)0x7ffffff0,
+                                                                              0, 0));
     }
     float q[G][8];
     if (a.Qpart) {
@@ -492,178 +453,297 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             }
         }
     }
-    const long pstride = (long)G * (D + 2);
-    float* pbase = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * pstride;
-    const __amdgpu_buffer_rsrc_t prs = frag_rsrc(pbase, (uint32_t)(a.nsplit * pstride * 4));
-    if (n > 0) {
+    if (n <= 0) return;
 #pragma unroll
-        for (int i = 0; i < NIT; ++i) {
-            const int j = c0 + i * KPB + wave * KPW + kg;
-            if (j >= c1) {
-                kr[i] = (u32x4){0u, 0u, 0u, 0u};
-                vr[i] = (u32x4){0u, 0u, 0u, 0u};
-            }
-            if (has_t && j == t) {
-                // key t: PM-RoPE of the new key (rope_store_kernel's arithmetic), then append
-                const float sg = dl < LPK / 2 ? -1.0f : 1.0f;
-                const int pbase = (8 * dl + D / 2) % D;
-                u32x4 kw, vw;
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    float ko[2], vo[2];
-#pragma unroll
-                    for (int e = 0; e < 2; ++e) {
-                        const int dd = 8 * dl + 2 * jj + e;
-                        const float c = c8[2 * jj + e], sn = s8[2 * jj + e];
-                        const float x = kvnew[0][dd], pr = kvnew[0][pbase + 2 * jj + e];
-                        ko[e] = rbf(rbf(x * c) + rbf((sg * pr) * sn));
-                        vo[e] = kvnew[1][dd];
-                    }
-                    kw[jj] = pack2(ko[0], ko[1]);
-                    vw[jj] = pack2(vo[0], vo[1]);
-                }
-                kr[i] = kw;
-                vr[i] = vw;
-                *(u32x4*)(const_cast<bf16_t*>(Kb) + (long)t * D + 8 * dl) = kw;
-                *(u32x4*)(const_cast<bf16_t*>(Vb) + (long)t * D + 8 * dl) = vw;
-            }
+    for (int i = 0; i < NIT; ++i) {
+        const int j = c0 + i * KPB + wave * KPW + kg;
+        if (j >= c1) {
+            kr[i] = (u32x4){0u, 0u, 0u, 0u};
+            vr[i] = (u32x4){0u, 0u, 0u, 0u};
         }
-#pragma unroll
-        for (int i = 0; i < NIT; ++i) {
-            float s[G];
-#pragma unroll
-            for (int g = 0; g < G; ++g) s[g] = 0.f;
+        if (has_t && j == t) {
+            // key t: PM-RoPE of the new key (rope_store_kernel's arithmetic), then append
+            const float sg = dl < LPK / 2 ? -1.0f : 1.0f;
+            const int pbase = (8 * dl + D / 2) % D;
+            u32x4 kw, vw;
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
-                const float k0 = bf_lo(kr[i][jj]), k1 = bf_hi(kr[i][jj]);
+                float ko[2], vo[2];
 #pragma unroll
-                for (int g = 0; g < G; ++g) s[g] += q[g][2 * jj] * k0 + q[g][2 * jj + 1] * k1;
+                for (int e = 0; e < 2; ++e) {
+                    const int dd = 8 * dl + 2 * jj + e;
+                    const float c = c8[2 * jj + e], sn = s8[2 * jj + e];
+                    const float x = kvnew[0][dd], pr = kvnew[0][pbase + 2 * jj + e];
+                    ko[e] = rbf(rbf(x * c) + rbf((sg * pr) * sn));
+                    vo[e] = kvnew[1][dd];
+                }
+                kw[jj] = pack2(ko[0], ko[1]);
+                vw[jj] = pack2(vo[0], vo[1]);
             }
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int o = LPK / 2; o > 0; o >>= 1) s[g] += __shfl_xor(s[g], o, 64);
-            const int jl = i * KPB + wave * KPW + kg;
-            if (dl == 0) {
-#pragma unroll
-                for (int g = 0; g < G; ++g) sm[g][jl] = s[g] * a.scale;
-            }
+            kr[i] = kw;
+            if (single) vr[i] = vw;
+            *(u32x4*)(const_cast<bf16_t*>(Kb) + (long)t * D + 8 * dl) = kw;
+            *(u32x4*)(const_cast<bf16_t*>(Vb) + (long)t * D + 8 * dl) = vw;
         }
-        __syncthreads();
-        T5G_TS(2);
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        float s[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) s[g] = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const float k0 = bf_lo(kr[i][jj]), k1 = bf_hi(kr[i][jj]);
+#pragma unroll
+            for (int g = 0; g < G; ++g) s[g] += q[g][2 * jj] * k0 + q[g][2 * jj + 1] * k1;
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int o = LPK / 2; o > 0; o >>= 1) s[g] += __shfl_xor(s[g], o, 64);
+        const int jl = i * KPB + wave * KPW + kg;
+        if (dl == 0) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) sm[g][jl] = __fmul_rn(s[g], a.scale);
+        }
+    }
+    __syncthreads();
+    T5G_TS(2);
+    if (!single) {
+        // publish the chunk's scores and maxima (read by the next two launches)
         if (wave < G) {
             const int g = wave;
             const float s = lane < n ? sm[g][lane] : -INFINITY;
+            if (lane < n) a.sbuf[((long)qi * a.Hkv * G + kvh * G + g) * a.kv_cap + c0 + lane] = s;
             const float mx = wave_max(s);
-            const float e = lane < n ? expf(s - mx) : 0.f;
-            const float l = wave_sum(e);
-            sm[g][lane] = rbf(e);
-            if (lane == 0) {
-                stat[g][0] = mx;
-                stat[g][1] = l;
+            if (lane == 0) a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + sp) * G + g] = mx;
+        }
+        T5G_TS(5);
+        return;
+    }
+    // single-chunk row: one aten kv block of `span` keys
+    if (wave < G) {
+        const int g = wave;
+        const float s = lane < n ? sm[g][lane] : -INFINITY;
+        const float mx = wave_max(s);
+        auto pf = [&](int pos) -> float { return pos < n ? sdpa_p(__fsub_rn(sm[g][pos], mx), pos, span) : 0.f; };
+        const float l = sdpa_block_sum(span, lane, pf);
+        const float p = pf(lane);
+        sm[g][lane] = rbf(p);
+        if (lane == 0) stat_l[g] = l;
+    }
+    __syncthreads();
+    float o[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        const int jl = i * KPB + wave * KPW + kg;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float p = sm[g][jl];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                o[g][2 * jj] += p * bf_lo(vr[i][jj]);
+                o[g][2 * jj + 1] += p * bf_hi(vr[i][jj]);
             }
         }
-        __syncthreads();
-        float o[G][8];
+    }
 #pragma unroll
-        for (int g = 0; g < G; ++g)
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
+        for (int jj = 0; jj < 8; ++jj)
 #pragma unroll
-        for (int i = 0; i < NIT; ++i) {
-            const int jl = i * KPB + wave * KPW + kg;
+            for (int off = LPK; off < 64; off <<= 1) o[g][jj] += __shfl_xor(o[g][jj], off, 64);
+    if (kg == 0) {
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const float p = sm[g][jl];
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    o[g][2 * jj] += p * bf_lo(vr[i][jj]);
-                    o[g][2 * jj + 1] += p * bf_hi(vr[i][jj]);
-                }
-            }
+        for (int g = 0; g < G; ++g) {
+            ored[wave][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
+            ored[wave][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
         }
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj)
-#pragma unroll
-                for (int off = LPK; off < 64; off <<= 1) o[g][jj] += __shfl_xor(o[g][jj], off, 64);
-        if (kg == 0) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                ored[wave][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
-                ored[wave][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
-            }
-        }
-        __syncthreads();
-        T5G_TS(4);
-        for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
-            const int g = idx / LPK, d8 = idx % LPK;
-            const f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
-            const f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
-            if (a.nsplit > 1) {
-                // sc1 (write-through) slab stores: the merging block may sit on another XCD
-                const int pg = sp * (int)pstride + g * (D + 2);
-                if (d8 == 0) {
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(stat[g][0]), prs, pg * 4, 0, 16);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(stat[g][1]), prs, (pg + 1) * 4, 0, 16);
-                }
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo4), prs, (pg + 2 + 8 * d8) * 4, 0, 16);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi4), prs, (pg + 6 + 8 * d8) * 4, 0, 16);
-            } else {
-                const float inv = 1.0f / stat[g][1];
-                u32x4 w;
-                w[0] = pack2(lo4[0] * inv, lo4[1] * inv);
-                w[1] = pack2(lo4[2] * inv, lo4[3] * inv);
-                w[2] = pack2(hi4[0] * inv, hi4[1] * inv);
-                w[3] = pack2(hi4[2] * inv, hi4[3] * inv);
-                *(u32x4*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 8 * d8) = w;
-            }
-        }
-    } else if (a.nsplit > 1 && threadIdx.x < G) {
-        const int pg = sp * (int)pstride + threadIdx.x * (D + 2);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(-INFINITY), prs, pg * 4, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b32(0u, prs, (pg + 1) * 4, 0, 16);
+    }
+    __syncthreads();
+    T5G_TS(4);
+    for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
+        const int g = idx / LPK, d8 = idx % LPK;
+        const f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
+        const f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
+        const float inv = __fdiv_rn(1.0f, stat_l[g]);
+        u32x4 w;
+        w[0] = pack2(__fmul_rn(lo4[0], inv), __fmul_rn(lo4[1], inv));
+        w[1] = pack2(__fmul_rn(lo4[2], inv), __fmul_rn(lo4[3], inv));
+        w[2] = pack2(__fmul_rn(hi4[0], inv), __fmul_rn(hi4[1], inv));
+        w[3] = pack2(__fmul_rn(hi4[2], inv), __fmul_rn(hi4[3], inv));
+        *(u32x4*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 8 * d8) = w;
     }
     T5G_TS(5);
-    if (a.nsplit == 1 || !a.counters) return;
-    // ---- in-launch merge (CDNA guide G16, valid form row 1): every storing wave drains
-    // its sc1 slab stores, then one lane adds to the (row, kv head) ticket; the block
-    // whose add returns nsplit-1 merges, reading the slabs with sc1 loads. No fences.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int* ctr = a.counters + qi * a.Hkv + kvh;
-        const int ticket = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = ticket == a.nsplit - 1;
-        if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-        last_flag = last;
-    }
-    __syncthreads();
-    if (!last_flag) return;
-    T5G_TS(3);
-    merge_splits<D, G>(a, pbase, qi, kvh, wz, Linv);
-    T5G_TS(6);
 }
 
-// merge of the key-split partials (used when no ticket counters are supplied):
-// O = sum_z e^(m_z - M) o_z / sum_z e^(m_z - M) l_z
-// Each (row, kv head) is merged by CZ blocks of 64*G threads, one slice of 32 (g, d4) quads
-// each: a block reads 1/CZ of the slabs, so the merge is spread over 4x the CUs (a single
-// block per (row, kv head) was per-CU-bandwidth bound: 31 KB of slabs at 15 splits).
+// row geometry shared by the pv / combine kernels (same rules as attn_decode_kernel)
+struct DecRow {
+    int lo, hi, span;
+};
+__device__ __forceinline__ DecRow dec_row(const AttnArgs& a, int qi) {
+    const int row = a.q_row ? a.q_row[qi] : qi;
+    const int len = a.kv_len[row];
+    const int t = a.q_pos ? a.q_pos[qi] : len - 1;
+    int lo = 0, hi = len;
+    if (a.causal) {
+        hi = min(t + 1, len);
+        if (a.window > 0) lo = max(0, t - a.window + 1);
+    } else if (a.window > 0) {
+        lo = max(0, t - a.window);
+        hi = min(len, t + a.window + 1);
+    }
+    return {lo, hi, max(hi - lo, 0)};
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256, 2) void attn_pv_kernel(AttnArgs a) {
+    constexpr int LPK = D / 8;
+    constexpr int KPW = 64 / LPK;
+    constexpr int KPB = KPW * 4;
+    constexpr int NIT = DCH / KPB;
+    constexpr int CPB = SDPA_KV_BLOCK / DCH;   // chunks per aten kv block
+    __shared__ float sp_p[G][DCH];
+    __shared__ float mrun[G];
+    __shared__ f32x4 ored[4][G][LPK][2];
+    const int qi = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int kg = lane / LPK, dl = lane % LPK;
+    const int row = a.q_row ? a.q_row[qi] : qi;
+    const DecRow r = dec_row(a, qi);
+    if (r.span <= DCH) return;                  // finished by attn_decode_kernel
+    const int c0 = r.lo + sp * DCH;
+    if (c0 >= r.hi) return;
+    const int c1 = min(r.hi, c0 + DCH);
+    const int n = c1 - c0;
+    // V rows of the chunk first (in flight while the maxima and scores are read)
+    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
+    const __amdgpu_buffer_rsrc_t vrs = frag_rsrc(Vb, (uint32_t)a.kv_cap * D * 2u);
+    u32x4 vr[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        const int j = c0 + i * KPB + wave * KPW + kg;
+        const int off = j < c1 ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
+        vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
+    }
+    const int bi = sp / CPB;                                  // aten kv block of this chunk
+    const int nch = (r.span + DCH - 1) / DCH;
+    const int blen = min(SDPA_KV_BLOCK, r.span - bi * SDPA_KV_BLOCK);
+    if (wave < G) {
+        const int g = wave;
+        // running max through the end of this chunk's block
+        const int cend = min(nch, (bi + 1) * CPB);
+        const float m = lane < cend ? a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + lane) * G + g] : -INFINITY;
+        const float mx = wave_max(m);
+        if (lane == 0) mrun[g] = mx;
+        const float s = lane < n ? a.sbuf[((long)qi * a.Hkv * G + kvh * G + g) * a.kv_cap + c0 + lane] : 0.f;
+        const int pos = c0 + lane - r.lo - bi * SDPA_KV_BLOCK;
+        sp_p[g][lane] = lane < n ? rbf(sdpa_p(__fsub_rn(s, mx), pos, blen)) : 0.f;
+    }
+    __syncthreads();
+    float o[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        const int jl = i * KPB + wave * KPW + kg;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float p = sp_p[g][jl];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                o[g][2 * jj] += p * bf_lo(vr[i][jj]);
+                o[g][2 * jj + 1] += p * bf_hi(vr[i][jj]);
+            }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+            for (int off = LPK; off < 64; off <<= 1) o[g][jj] += __shfl_xor(o[g][jj], off, 64);
+    if (kg == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            ored[wave][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
+            ored[wave][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
+        }
+    }
+    __syncthreads();
+    float* pbase = a.part + (((long)qi * a.Hkv + kvh) * a.nsplit + sp) * (G * (D + 2));
+    for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
+        const int g = idx / LPK, d8 = idx % LPK;
+        const f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
+        const f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
+        float* pg = pbase + g * (D + 2);
+        if (d8 == 0) pg[0] = mrun[g];
+        *(f32x4*)(pg + 2 + 8 * d8) = lo4;
+        *(f32x4*)(pg + 6 + 8 * d8) = hi4;
+    }
+}
+
+// Each (row, kv head) is combined by CZ blocks of 64*G threads, one slice of the (g, d4)
+// quads each (a single block per (row, kv head) was per-CU-bandwidth bound).
 template <int D, int G>
 constexpr int combine_cz() { return (G * D / 4 + 31) / 32; }
 
 template <int D, int G>
 __global__ __launch_bounds__(64 * G) void attn_combine_kernel(AttnArgs a) {
-    __shared__ float wz[G * 64];
-    __shared__ float Linv[G];
+    constexpr int CPB = SDPA_KV_BLOCK / DCH;
+    __shared__ float blk_et[G][SDPA_MAX_BLOCKS];
+    __shared__ float stat_l[G];
     const int qi = blockIdx.x, kvh = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     T5G_TS(3);
-    const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2));
+    const DecRow r = dec_row(a, qi);
+    if (r.span <= DCH) return;
+    const int nch = (r.span + DCH - 1) / DCH;
+    const int nblk = (r.span + SDPA_KV_BLOCK - 1) / SDPA_KV_BLOCK;
+    {   // wave g: l of head g with aten's lane-ordered block sums
+        const int g = wave;
+        const float* mb = a.mbuf + ((long)qi * a.Hkv + kvh) * a.nsplit * G + g;
+        const float* sb = a.sbuf + ((long)qi * a.Hkv * G + kvh * G + g) * a.kv_cap + r.lo;
+        float m = -INFINITY, l = 0.f;
+        for (int b = 0; b < nblk; ++b) {
+            const int ce = min(nch, (b + 1) * CPB), cs = b * CPB;
+            const float cm = (cs + lane < ce) ? mb[(cs + lane) * G] : -INFINITY;
+            const float mn = fmaxf(m, wave_max(cm));
+            const int bs = b * SDPA_KV_BLOCK;
+            const int blen = min(SDPA_KV_BLOCK, r.span - bs);
+            auto pf = [&](int pos) -> float { return sdpa_p(__fsub_rn(sb[bs + pos], mn), pos, blen); };
+            const float ts = sdpa_block_sum(blen, lane, pf);
+            const float et = sdpa_block_rescale(m, mn);
+            l = fmaf(et, l, ts);
+            if (lane == 0) blk_et[g][b] = et;
+            m = mn;
+        }
+        if (lane == 0) stat_l[g] = l;
+    }
+    __syncthreads();
     constexpr int QPB = (G * D / 4 + combine_cz<D, G>() - 1) / combine_cz<D, G>();
-    const int q0 = (int)blockIdx.z * QPB;
-    merge_splits<D, G>(a, base, qi, kvh, wz, Linv, q0, min(QPB, G * D / 4 - q0));
+    const int quad = (int)blockIdx.z * QPB + (int)threadIdx.x;
+    if ((int)threadIdx.x >= QPB || quad >= G * D / 4) return;
+    const int g = quad / (D / 4), d4 = quad % (D / 4);
+    const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2)) + g * (D + 2) + 2 + 4 * d4;
+    f32x4 dst = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < nblk; ++b) {
+        f32x4 blk = {0.f, 0.f, 0.f, 0.f};
+        const int ce = min(nch, (b + 1) * CPB);
+        for (int c = b * CPB; c < ce; ++c) blk += *(const f32x4*)(base + (long)c * G * (D + 2));
+        dst = dst * blk_et[g][b] + blk;
+    }
+    const float inv = __fdiv_rn(1.0f, stat_l[g]);
+    uint2 o;
+    o.x = pack2(__fmul_rn(dst[0], inv), __fmul_rn(dst[1], inv));
+    o.y = pack2(__fmul_rn(dst[2], inv), __fmul_rn(dst[3], inv));
+    *(uint2*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 4 * d4) = o;
     T5G_TS(6);
 }
 
@@ -671,17 +751,19 @@ template <int D, int G>
 static int launch_decode(const AttnArgs& a, hipStream_t st) {
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
     hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, a);
-    if (a.nsplit > 1 && !a.counters)
+    if (a.nsplit > 1) {
+        hipLaunchKernelGGL((attn_pv_kernel<D, G>), grid, dim3(256), 0, st, a);
         hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, combine_cz<D, G>()),
-                           dim3(64 * G), 0,
-                           st, a);
+                           dim3(64 * G), 0, st, a);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int attention_decode(const AttnArgs& a, hipStream_t st) {
     if (a.Mq <= 0) return 0;
-    if (a.nsplit < 1 || a.nsplit > 64 || !a.part || a.eager) return -1;
-    if ((long)a.nsplit * 64 < a.kv_cap || a.kv_cap <= 0) return -1;   // chunks of <= 64 keys
+    if (a.eager || !a.part || a.kv_cap <= 0 || a.kv_cap > SDPA_KV_BLOCK * SDPA_MAX_BLOCKS) return -1;
+    if (a.nsplit != (a.kv_cap + DCH - 1) / DCH) return -1;   // 64-key chunks from the row start
+    if (a.nsplit > 1 && (!a.sbuf || !a.mbuf || a.nsplit > 64)) return -1;
     if (a.append && (!a.Qpart || !a.rope_tab || (a.G + 2) * a.D / 4 > 256)) return -1;
     if (a.Qpart && (a.q_nsplit < 1 || a.q_nsplit > QSMAX)) return -1;
     if (a.D == 256 && a.G == 2) return launch_decode<256, 2>(a, st);
@@ -693,24 +775,18 @@ int attention_decode(const AttnArgs& a, hipStream_t st) {
 
 template <int D, int G>
 static int launch_attn(const AttnArgs& a, hipStream_t st) {
-    dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
+    dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, 1u);
     size_t shm = (size_t)G * a.chunk * sizeof(float);
     if (a.eager)
         hipLaunchKernelGGL((attn_kernel<D, G, true>), grid, dim3(256), shm, st, a);
     else
         hipLaunchKernelGGL((attn_kernel<D, G, false>), grid, dim3(256), shm, st, a);
-    if (a.nsplit > 1)
-        hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, combine_cz<D, G>()),
-                           dim3(64 * G), 0,
-                           st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int attention(const AttnArgs& a, hipStream_t st) {
     if (a.Mq <= 0) return 0;
-    if (a.nsplit < 1 || a.chunk < 1) return -1;
-    if (a.eager && a.nsplit != 1) return -1;       // eager normalises over the full row
-    if (a.nsplit > 1 && !a.part) return -1;
+    if (a.nsplit != 1 || a.chunk < 1 || a.chunk > SDPA_KV_BLOCK * SDPA_MAX_BLOCKS) return -1;
     if ((size_t)a.G * a.chunk * sizeof(float) > 96 * 1024) return -1;
     if (a.D == 256 && a.G == 2) return launch_attn<256, 2>(a, st);
     if (a.D == 64 && a.G == 2) return launch_attn<64, 2>(a, st);

@@ -98,11 +98,64 @@ __device__ __forceinline__ float block_max(float v, float* red) {
     return s;
 }
 
+// ---- torch CPU SDPA softmax numerics (bf16 inputs), restated bit-exactly -----------
+// The reference's attention is F.scaled_dot_product_attention on CPU bf16 tensors
+// ([tf] integrations/sdpa_attention.py -> aten cpu_flash_attention, AVX-512 build).
+// Per query row and per kv block of <= 512 keys (running max m over the blocks):
+//   p_j = exp(s_j - m): the first blen & ~15 keys of the block through at::vec's fast exp
+//         (sdpa_fexp, the constants of the shipped kernel), the remaining tail through
+//         double-precision exp;
+//   tmp_sum = 16 lane accumulators (key % 16, in key order) -> xor 8/4/2/1 tree -> + tail
+//         in order (sdpa_block_sum); l = fma(expf(m_old - m), l_old, tmp_sum);
+//   out   = bf16(sum_j bf16(p_j) v_j (scaled by expf(m_old - m) per block) * (1 / l)).
+// Verified bit-exact against torch 2.10 CPU SDPA in the build container.
+__device__ __forceinline__ float sdpa_fexp(float x) {
+    if (!(x >= -87.3365478515625f)) return 0.f;           // below ln(FLT_MIN) / masked (-inf)
+    const float t = __fmul_rn(x, 1.44269502162933349609375f);   // x * log2(e), fp32 product
+    const float n = floorf(t);
+    const float f = __fsub_rn(t, n);
+    float p = fmaf(f, -0.07920423895120621f, -0.2243383675813675f);
+    p = fmaf(f, p, 0.3035426139831543f);
+    const float q = fmaf(p, f, 0.00010703434963943437f);
+    const float y = fmaf(__fsub_rn(t, q), 8388608.0f, 1065353216.0f);
+    return __int_as_float((int)y);                          // cvttps2dq: truncate
+}
+__device__ __forceinline__ float sdpa_exp_tail(float x) { return (float)exp((double)x); }
+// p of block position `pos` of a block with `blen` keys
+__device__ __forceinline__ float sdpa_p(float x, int pos, int blen) {
+    return pos < (blen & ~15) ? sdpa_fexp(x) : sdpa_exp_tail(x);
+}
+// tmp_sum of one kv block (one wave; every lane returns it). p(pos) -> fp32 p of the
+// block's key `pos`, 0 <= pos < blen.
+template <typename P>
+__device__ __forceinline__ float sdpa_block_sum(int blen, int lane, P p) {
+    const int n16 = blen & ~15;
+    float acc = 0.f;
+    if (lane < 16)
+        for (int i = lane; i < n16; i += 16) acc = __fadd_rn(acc, p(i));
+    acc = __fadd_rn(acc, __shfl_xor(acc, 8, 64));
+    acc = __fadd_rn(acc, __shfl_xor(acc, 4, 64));
+    acc = __fadd_rn(acc, __shfl_xor(acc, 2, 64));
+    acc = __fadd_rn(acc, __shfl_xor(acc, 1, 64));
+    float s = __shfl(acc, 0, 64);
+    for (int i = n16; i < blen; ++i) s = __fadd_rn(s, p(i));
+    return s;
+}
+// rescale of the previous blocks' sums when the running max grows (std::expf in aten)
+__device__ __forceinline__ float sdpa_block_rescale(float m_old, float m_new) {
+    return m_old == -INFINITY ? 0.f : (float)exp((double)__fsub_rn(m_old, m_new));
+}
+// q-block split of aten's CPU flash attention: a causal query row t of a Tq-query call
+// sees keys [0, min(q0 + qsplit, Tk)) in its blocks (keys > t masked), q0 = t - t % qsplit
+__device__ __forceinline__ int sdpa_qsplit(int Tq) { return Tq >= 768 ? 256 : (Tq >= 192 ? 64 : 32); }
+
 __device__ __forceinline__ float gelu_tanh(float x) {
-    // torch gelu(approximate='tanh'): 0.5*x*(1+tanh(sqrt(2/pi)*(x+0.044715*x^3)))
+    // torch gelu(approximate='tanh') in aten's CPU vector order (no fused multiply-adds):
+    // x3 = (x*x)*x; inner = kBeta*(x + kKappa*x3); (0.5*x)*(1 + tanh(inner)); tanh in fp64
     const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-    float inner = k0 * (x + k1 * x * x * x);
-    return 0.5f * x * (1.f + tanhf(inner));
+    const float x3 = __fmul_rn(__fmul_rn(x, x), x);
+    const float inner = __fmul_rn(k0, __fadd_rn(x, __fmul_rn(k1, x3)));
+    return __fmul_rn(__fmul_rn(0.5f, x), __fadd_rn(1.f, (float)tanh((double)inner)));
 }
 __device__ __forceinline__ float gelu_erf(float x) {
     return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));

@@ -44,20 +44,13 @@ struct t5g_engine {
     // packed-token activations (encode / prefill)
     bf16_t *h, *xn, *qkv, *q, *att, *act, *tmp, *mem;
     float* part;          // split-K slabs (max over uses)
-    float* apart;         // attention partials
+    float* apart;         // decode attention partial P.V slabs
     int64_t part_elems, apart_elems;
     bf16_t *enc_k, *enc_v;                 // encoder self K/V [B][Hkv][max_text][D]
     std::vector<bf16_t*> ck, cv, sk, sv;   // per decoder layer cross / self caches
     int* enc_len;                          // [B] text lengths
     // decode (rows = max_batch)
     bf16_t *dh, *dxn, *dq, *datt, *dact, *dhh, *logits;
-    bf16_t *dh2, *dv;     // fused decode: second residual buffer, sub-block output rows
-    // Decode-step GEMV variant, chosen at creation by T5G_FUSED_DECODE (measured on MI355X,
-    // tools/micro_gemv.py): unset/0 = split-K MFMA GEMVs + separate norm
-    // kernels (fastest); 1 = norm prologues fused into row-major VALU GEMVs; 2 = fused
-    // prologues on the P16 MFMA GEMVs.
-    bool fused_decode = false;
-    bool fused_p16 = false;
     int logits_ld;
     // sampler
     SamplerRow* rows;
@@ -70,7 +63,6 @@ struct t5g_engine {
     int* next_token;
     int* flags;
     int* last_rows;
-    int* attn_tickets_buf;  // [max_batch][Hkv] in-launch split-merge counters (self-re-arming)
     float* rope_tab;    // [max_batch][D] per-row cos|sin of the decode step's PM position
     // multi-block sampler scratch (sampler.hip fast path)
     float* fs_val;
@@ -81,28 +73,11 @@ struct t5g_engine {
     unsigned* fs_ticket;
     int* fs_slow;
     bool fast_sampler = true;   // T5G_SAMPLER_FAST=0 at creation: single-block sampler only
-    // decode attention: key-split partials merged in-launch by the last block of each
-    // (row, kv head) (T5G_ATTN_TICKETS=1) instead of a combine launch; cross attention
-    // keys split over T5G_XATTN_SPLIT blocks per (row, kv head). Both off by default:
-    // measured on MI355X (tools/micro_timeline.cpp) neither beats the combine launch.
-    bool attn_tickets = false;
-    // decode gate/up on gemv_dec (one block per CU, 1152 single-group units dealt
-    // round-robin: 18.3 us vs 19.7 us for the 576-block P16 GEMM); T5G_GU_GEMV=0 reverts
-    bool gu_gemv = true;
-    bool down_gemv = false;   // T5G_DOWN_GEMV=1: decode down projection on gemv_dec split-K (probe)
-    int s_down = 8;           // decode down-projection k-slices (T5G_S_DOWN, 2..8; probe)
-    int s_qkv = 2, s_o = 4;   // decode qkv / (o, cross-q, cross-o) k-slices (T5G_S_QKV, T5G_S_O, 2..4 = QSMAX; probe)
-    // decode norms folded into the consuming GEMV (PRO_LEAD: blocks 0..M-1 finish and
-    // publish the rows, the others poll per-row flags): one launch fewer per site.
-    // T5G_LEAD_NORM = site mask (1 next-layer qkv, 2 cross-q, 4 gate/up). Off by default:
-    // measured on MI355X the in-launch hand-off costs what the launch boundary did
-    // (gate/up 23.2 us vs 18.0 + 4.9 norm; all sites 3019 vs 3411 tok/s).
-    int lead_sites = 0;
-    unsigned* lead_flags = nullptr;   // [n_dec_layers][3 sites][16 rows]: last published epoch
-    unsigned* lead_epoch = nullptr;   // step epoch, advanced by the step's rope_table launch
-    unsigned* lead_tmo = nullptr;     // poll give-up word (t5g_engine_status)
-    float* qslab = nullptr;           // [max_batch][qkv_dim] fp32 q|k|v of the lead GEMVs
-    int xsplit = 1;
+    // decode split-K factors (measured on MI355X): qkv 2, o / cross-q /
+    // cross-o 4, down 8 k-slices; gate/up on the one-block-per-CU GEMV
+    static constexpr int s_qkv = 2, s_o = 4, s_down = 8;
+    float* asbuf = nullptr;   // decode attention scores of rows > 64 keys [B][Hq][max(max_audio, max_text)]
+    float* ambuf = nullptr;   // decode attention chunk maxima [B][Hkv][nsplit][G]
     int B = 0;            // rows of the current call
     const bf16_t* noise = nullptr;
     int noise_steps = 0;
@@ -182,16 +157,14 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     // split-K slabs: decode uses up to 8 splits of [B][max(d, qkv)]
     e->part_elems = (int64_t)8 * B * widest(widest(d, e->qkv_dim), 2 * e->kv_dim);
     rc |= alloc(e, &e->part, e->part_elems);
-    rc |= alloc(e, &e->lead_flags, (int64_t)c.n_dec_layers * 3 * 16);
-    rc |= alloc(e, &e->lead_tmo, 4);
-    rc |= alloc(e, &e->lead_epoch, 4);
-    rc |= alloc(e, &e->qslab, (int64_t)B * widest(e->qkv_dim, d));
     const int G = c.n_heads / c.n_kv_heads;
-    const int nsplit_dec = (c.max_audio + 63) / 64;
-    // cross-attention key splits: up to max(ceil(max_text / 64), 16) (T5G_XATTN_SPLIT cap)
-    const int nsplit_x = (c.max_text + 63) / 64 > 16 ? (c.max_text + 63) / 64 : 16;
-    e->apart_elems = (int64_t)B * Hkv * (nsplit_dec > nsplit_x ? nsplit_dec : nsplit_x) * G * (D + 2);
+    const int nsplit_dec = (c.max_audio + 63) / 64, nsplit_x = (c.max_text + 63) / 64;
+    const int nsplit_max = nsplit_dec > nsplit_x ? nsplit_dec : nsplit_x;
+    const int cap_max = c.max_audio > c.max_text ? c.max_audio : c.max_text;
+    e->apart_elems = (int64_t)B * Hkv * nsplit_max * G * (D + 2);
     rc |= alloc(e, &e->apart, e->apart_elems);
+    rc |= alloc(e, &e->asbuf, (int64_t)B * c.n_heads * cap_max);
+    rc |= alloc(e, &e->ambuf, (int64_t)B * Hkv * nsplit_max * G);
     const int64_t enc_cache = (int64_t)B * Hkv * c.max_text * D;
     rc |= alloc(e, &e->enc_k, enc_cache);
     rc |= alloc(e, &e->enc_v, enc_cache);
@@ -213,8 +186,6 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->datt, (int64_t)B * e->q_dim);
     rc |= alloc(e, &e->dact, (int64_t)B * f);
     rc |= alloc(e, &e->dhh, (int64_t)B * d);
-    rc |= alloc(e, &e->dh2, (int64_t)B * d);
-    rc |= alloc(e, &e->dv, (int64_t)B * d);
     e->logits_ld = e->Vpad;
     rc |= alloc(e, &e->logits, (int64_t)B * e->logits_ld);
     rc |= alloc(e, &e->rows, B);
@@ -227,7 +198,6 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->next_token, B);
     rc |= alloc(e, &e->flags, B);
     rc |= alloc(e, &e->last_rows, B);
-    rc |= alloc(e, &e->attn_tickets_buf, (int64_t)B * Hkv);
     rc |= alloc(e, &e->rope_tab, (int64_t)B * D);
     rc |= alloc(e, &e->fs_val, (int64_t)B * FS_NB * FS_CAP);
     rc |= alloc(e, &e->fs_idx, (int64_t)B * FS_NB * FS_CAP);
@@ -239,28 +209,6 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     {
         const char* fsv = getenv("T5G_SAMPLER_FAST");
         e->fast_sampler = !(fsv && fsv[0] == '0');
-        const char* fdv = getenv("T5G_FUSED_DECODE");
-        e->fused_decode = fdv && (fdv[0] == '1' || fdv[0] == '2');
-        e->fused_p16 = fdv && fdv[0] == '2';
-        const char* atv = getenv("T5G_ATTN_TICKETS");
-        e->attn_tickets = atv && atv[0] == '1';
-        const char* guv = getenv("T5G_GU_GEMV");
-        e->gu_gemv = !(guv && guv[0] == '0');
-        const char* dgv = getenv("T5G_DOWN_GEMV");
-        e->down_gemv = dgv && dgv[0] == '1';
-        const char* sdv = getenv("T5G_S_DOWN");
-        if (sdv && atoi(sdv) >= 2 && atoi(sdv) <= 8) e->s_down = atoi(sdv);
-        const char* sqv = getenv("T5G_S_QKV");
-        if (sqv && atoi(sqv) >= 2 && atoi(sqv) <= 4) e->s_qkv = atoi(sqv);
-        const char* sov = getenv("T5G_S_O");
-        if (sov && atoi(sov) >= 2 && atoi(sov) <= 4) e->s_o = atoi(sov);
-        const char* lnv = getenv("T5G_LEAD_NORM");
-        if (lnv) e->lead_sites = atoi(lnv) & 7;
-        const char* xsv = getenv("T5G_XATTN_SPLIT");
-        e->xsplit = xsv ? atoi(xsv) : 1;
-        const int xmax = (c.max_text + 63) / 64 > 16 ? (c.max_text + 63) / 64 : 16;
-        if (e->xsplit < (c.max_text + 63) / 64) e->xsplit = (c.max_text + 63) / 64;
-        if (e->xsplit > xmax) e->xsplit = xmax;
     }
     if (rc) {
         t5g_engine_destroy(e);
@@ -431,6 +379,46 @@ extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t*
 // decode mode: M = B rows, positions/slots/tokens from the sampler buffers.
 static DecGemmArgs dec_args(int M, const void* W, int N, int K, void* Y, int ldy, int nw);
 
+// decode attention over a per-layer cache (self: the step's k/v appended in-kernel)
+static int decode_attention(t5g_engine* e, int M, const bf16_t* K, const bf16_t* Vc, int cap, const int* kv_len,
+                            int causal, int window, int q_col0, bool append, const float* pos, const float* tab,
+                            int q_nsplit, int ldqp, hipStream_t st) {
+    const t5g_config& c = e->c;
+    AttnArgs a;
+    memset(&a, 0, sizeof(a));
+    a.ldq = e->q_dim;
+    a.Mq = M;
+    a.K = K;
+    a.V = Vc;
+    a.kv_hstride = (long)cap * c.head_dim;
+    a.kv_bstride = a.kv_hstride * c.n_kv_heads;
+    a.kv_len = kv_len;
+    a.Hkv = c.n_kv_heads;
+    a.D = c.head_dim;
+    a.G = c.n_heads / c.n_kv_heads;
+    a.causal = causal;
+    a.window = window;
+    a.scale = c.attn_scale;
+    a.O = e->datt;
+    a.ldo = e->q_dim;
+    a.chunk = 64;
+    a.nsplit = (cap + 63) / 64;
+    a.kv_cap = cap;
+    a.part = e->apart;
+    a.sbuf = e->asbuf;
+    a.mbuf = e->ambuf;
+    a.Qpart = e->part + q_col0;   // q columns of the projection's fp32 split-K slabs
+    a.q_nsplit = q_nsplit;
+    a.ldqp = ldqp;
+    a.pos = pos;
+    a.inv_freq = e->w.inv_freq;
+    a.rope_tab = tab;
+    a.append = append ? 1 : 0;
+    a.k_col0 = e->q_dim - q_col0;
+    a.v_col0 = e->q_dim + e->kv_dim - q_col0;
+    return attention_decode(a, st);
+}
+
 static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row, const int* tok_t, const float* pos,
                         bool decode, hipStream_t st) {
     const t5g_config& c = e->c;
@@ -441,42 +429,49 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
     bf16_t* att = decode ? e->datt : e->att;
     bf16_t* act = decode ? e->dact : e->act;
     bf16_t* tmp = e->tmp;
-    const int G = c.n_heads / c.n_kv_heads;
-    // split-K factors (decode: spread weight streams over >= 512 blocks)
-    const int s_qkv = decode ? e->s_qkv : 1, s_o = decode ? e->s_o : 1, s_cq = decode ? e->s_o : 1, s_down = decode ? e->s_down : 1;
+    const bool eager = c.softcap > 0.f;
+    // split-K factors (decode: spread the weight streams over >= 512 blocks)
+    const int s_qkv = decode ? e->s_qkv : 1, s_o = decode ? e->s_o : 1, s_down = decode ? e->s_down : 1;
     // one cos/sin table per step: every layer's q/k rotation uses the same positions
     const float* tab = nullptr;
     if (decode) {
-        RC(rope_table(pos, e->w.inv_freq, M, D, e->rope_tab, st, e->lead_epoch));
+        RC(rope_table(pos, e->w.inv_freq, M, D, e->rope_tab, st));
         tab = e->rope_tab;
     }
-    // PRO_LEAD chain (sdpa decode, M <= 16): the norm after o, cross-o and down (but the
-    // last layer's) runs in the first M blocks of the GEMV that consumes it
-    const bool lead = decode && e->lead_sites && M <= 16 && !(c.softcap > 0.f) && s_qkv > 1 && s_cq > 1 &&
-                      d % 32 == 0 && d <= 4096;
-    auto lead_gemv = [&](const void* W, int N, void* Y, int ldy, int nsplit, const void* post_w, const void* pre_w,
-                         int site, int epi) -> int {
-        DecGemmArgs g = dec_args(M, W, N, d, Y, ldy, 8);
-        g.un = 8;
-        g.X = xn;
-        g.ldx = d;
-        g.part = e->part;
-        g.nsplit_p = nsplit;
-        g.ldp = d;
-        g.h_in = h;
-        g.h_out = h;
-        g.post_w = (const bf16_t*)post_w;
-        g.pre_w = (const bf16_t*)pre_w;
-        g.eps = c.rms_eps;
-        g.flags = e->lead_flags + site * 16;
-        g.tmo = e->lead_tmo;
-        g.epoch = e->lead_epoch;
-        return gemv_dec(g, epi, PRO_LEAD, st);
+    // norm after a Linear: h = h + RMSNorm_post(delta), xn = RMSNorm_pre(h)
+    auto resid = [&](int splits, const void* post_w, const void* pre_w) -> int {
+        NormArgs n = norm_args(M, d, c.rms_eps);
+        if (splits > 1) {
+            n.part = e->part;
+            n.nsplit = splits;
+            n.ldp = d;
+        } else {
+            n.delta = tmp;
+        }
+        n.post_w = (const bf16_t*)post_w;
+        n.resid = h;
+        n.pre_w = (const bf16_t*)pre_w;
+        n.resid_out = h;
+        n.normed_out = xn;
+        return resid_norm(n, st);
+    };
+    auto rope_args = [&]() {
+        RopeArgs r;
+        memset(&r, 0, sizeof(r));
+        r.M = M;
+        r.D = D;
+        r.pos = pos;
+        r.inv_freq = e->w.inv_freq;
+        r.tok_row = tok_row;
+        r.tok_t = tok_t;
+        r.kv_len = e->kv_len;
+        r.rope_tab = tab;
+        r.Qout = q;
+        r.ldq = e->q_dim;
+        return r;
     };
     for (int l = 0; l < c.n_dec_layers; ++l) {
         const t5g_layer_weights& L = e->dec[l];
-        const bool lead_qkv = lead && (e->lead_sites & 1) && l > 0;   // layer 0: embedding norm
-        const bool lead_cq = lead && (e->lead_sites & 2), lead_gu = lead && (e->lead_sites & 4);
         if (l == 0) {
             NormArgs n = norm_args(M, d, c.rms_eps);
             n.ids = ids;
@@ -488,274 +483,64 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             RC(resid_norm(n, st));
         }
         // --- self attention
-        RopeArgs r;
-        memset(&r, 0, sizeof(r));
-        if (lead_qkv) {
-            RC(lead_gemv(L.qkv, e->qkv_dim, e->qslab, e->qkv_dim, s_down, e->dec[l - 1].norms[5], L.norms[0],
-                         3 * l, EPI_F32));
-            r.Xpart = e->qslab;
-            r.nsplit = 1;
-        } else if (s_qkv > 1) {
-            RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, s_qkv, nullptr, e->part, e->qkv_dim, EPI_F32, st, !decode));
-            r.Xpart = e->part;
-            r.nsplit = s_qkv;
+        const int win = c.dec_sliding[l] ? c.sliding_window : 0;
+        if (decode && !eager) {
+            // q|k|v as fp32 split-K slabs; q rotated, k rotated + appended inside attention
+            RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, s_qkv, nullptr, e->part, e->qkv_dim, EPI_F32, st));
+            RC(decode_attention(e, M, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1, win, 0, true, pos, tab, s_qkv,
+                                e->qkv_dim, st));
         } else {
             RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, 1, nullptr, e->qkv, e->qkv_dim, EPI_BF16, st, !decode));
+            RopeArgs r = rope_args();
             r.X = e->qkv;
-        }
-        r.ldx = e->qkv_dim;
-        r.M = M;
-        r.D = D;
-        // decode: q is rotated inside the attention kernel; only k/v go to the cache here
-        r.nq = decode ? 0 : c.n_heads;
-        r.col0 = decode ? e->q_dim : 0;
-        r.nk = c.n_kv_heads;
-        r.nv = c.n_kv_heads;
-        r.rope_q = r.rope_k = 1;
-        r.pos = pos;
-        r.inv_freq = e->w.inv_freq;
-        r.tok_row = tok_row;
-        r.tok_t = tok_t;
-        r.kv_len = e->kv_len;
-        r.rope_tab = tab;
-        r.Qout = q;
-        r.ldq = e->q_dim;
-        r.Kc = e->sk[l];
-        r.Vc = e->sv[l];
-        r.c_hstride = (long)c.max_audio * D;
-        r.c_bstride = r.c_hstride * c.n_kv_heads;
-        // sdpa decode: the attention kernel appends k/v itself (AttnArgs::append)
-        const bool fused_append = decode && !(c.softcap > 0.f) && s_qkv > 1;
-        if (!fused_append) RC(rope_store(r, st));
-        {
-            AttnArgs a;
-            memset(&a, 0, sizeof(a));
-            a.Q = q;
-            a.ldq = e->q_dim;
-            a.Mq = M;
-            a.q_row = tok_row;
-            a.q_pos = tok_t;
-            a.K = e->sk[l];
-            a.V = e->sv[l];
-            a.kv_hstride = (long)c.max_audio * D;
-            a.kv_bstride = a.kv_hstride * c.n_kv_heads;
-            a.kv_len = e->kv_len;
-            a.Hkv = c.n_kv_heads;
-            a.D = D;
-            a.G = G;
-            a.causal = 1;
-            a.window = c.dec_sliding[l] ? c.sliding_window : 0;
-            a.scale = c.attn_scale;
-            a.softcap = c.softcap;
-            a.eager = c.softcap > 0.f;
-            a.O = att;
-            a.ldo = e->q_dim;
-            if (decode && !a.eager) {
-                a.chunk = 64;
-                a.nsplit = (c.max_audio + 63) / 64;
-                a.kv_cap = c.max_audio;
-                a.part = e->apart;
-                a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
-                if (s_qkv > 1) {
-                    a.Qpart = lead_qkv ? e->qslab : e->part;
-                    a.q_nsplit = lead_qkv ? 1 : s_qkv;
-                    a.ldqp = e->qkv_dim;
-                    a.pos = pos;
-                    a.inv_freq = e->w.inv_freq;
-                    a.rope_tab = tab;
-                    a.append = fused_append ? 1 : 0;
-                    a.k_col0 = e->q_dim;
-                    a.v_col0 = e->q_dim + e->kv_dim;
-                } else {
-                    return T5G_EINVAL;
-                }
-                RC(attention_decode(a, st));
-            } else {
-                if (decode) {  // eager decode: q rope via rope_store (q only)
-                    RopeArgs rq = r;
-                    rq.nq = c.n_heads;
-                    rq.nk = rq.nv = 0;
-                    rq.col0 = 0;
-                    RC(rope_store(rq, st));
-                }
-                a.nsplit = 1;
-                a.chunk = c.max_audio;
-                RC(attention(a, st));
-            }
+            r.ldx = e->qkv_dim;
+            r.nq = c.n_heads;
+            r.nk = r.nv = c.n_kv_heads;
+            r.rope_q = r.rope_k = 1;
+            r.Kc = e->sk[l];
+            r.Vc = e->sv[l];
+            r.c_hstride = (long)c.max_audio * D;
+            r.c_bstride = r.c_hstride * c.n_kv_heads;
+            RC(rope_store(r, st));
+            RC(attn_packed(e, M, q, tok_row, tok_t, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1, win, att, st));
         }
         RC(gemm(att, e->q_dim, M, L.o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
                 s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode));
-        if (!lead_cq) {
-            NormArgs n = norm_args(M, d, c.rms_eps);
-            if (s_o > 1) {
-                n.part = e->part;
-                n.nsplit = s_o;
-                n.ldp = d;
-            } else {
-                n.delta = tmp;
-            }
-            n.post_w = (const bf16_t*)L.norms[1];
-            n.resid = h;
-            n.pre_w = (const bf16_t*)L.norms[2];
-            n.resid_out = h;
-            n.normed_out = xn;
-            RC(resid_norm(n, st));
-        }
-        // --- PM cross attention
-        memset(&r, 0, sizeof(r));
-        if (lead_cq) {
-            RC(lead_gemv(L.cross_q, e->q_dim, e->qslab, e->q_dim, s_o, L.norms[1], L.norms[2], 3 * l + 1, EPI_F32));
-            r.Xpart = e->qslab;
-            r.nsplit = 1;
-        } else if (s_cq > 1) {
-            RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, s_cq, nullptr, e->part, e->q_dim, EPI_F32, st, !decode));
-            r.Xpart = e->part;
-            r.nsplit = s_cq;
+        RC(resid(s_o, L.norms[1], L.norms[2]));
+        // --- PM cross attention (q rotated by the decoder progress, :149-165)
+        if (decode && !eager) {
+            RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, s_o, nullptr, e->part, e->q_dim, EPI_F32, st));
+            RC(decode_attention(e, M, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, 0, false, pos, tab, s_o,
+                                e->q_dim, st));
         } else {
             RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, 1, nullptr, q, e->q_dim, EPI_BF16, st, !decode));
+            RopeArgs r = rope_args();
             r.X = q;
-        }
-        r.ldx = e->q_dim;
-        r.M = M;
-        r.D = D;
-        r.nq = c.n_heads;
-        r.rope_q = 1;
-        r.pos = pos;
-        r.inv_freq = e->w.inv_freq;
-        r.tok_row = tok_row;
-        r.rope_tab = tab;
-        r.Qout = q;
-        r.ldq = e->q_dim;
-        const bool fuse_q = decode && c.softcap <= 0.f && s_cq > 1;
-        if (!fuse_q) RC(rope_store(r, st));
-        {
-            AttnArgs a;
-            memset(&a, 0, sizeof(a));
-            a.Q = q;
-            a.ldq = e->q_dim;
-            a.Mq = M;
-            a.q_row = tok_row;
-            a.q_pos = tok_t;
-            a.K = e->ck[l];
-            a.V = e->cv[l];
-            a.kv_hstride = (long)c.max_text * D;
-            a.kv_bstride = a.kv_hstride * c.n_kv_heads;
-            a.kv_len = e->enc_len;
-            a.Hkv = c.n_kv_heads;
-            a.D = D;
-            a.G = G;
-            a.causal = 0;
-            a.window = 0;
-            a.scale = c.attn_scale;
-            a.softcap = c.softcap;
-            a.eager = c.softcap > 0.f;
-            a.O = att;
-            a.ldo = e->q_dim;
-            if (fuse_q) {
-                a.chunk = 64;
-                a.nsplit = e->xsplit;
-                a.kv_cap = c.max_text;
-                a.part = e->apart;
-                a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
-                a.Qpart = lead_cq ? e->qslab : e->part;
-                a.q_nsplit = lead_cq ? 1 : s_cq;
-                a.ldqp = e->q_dim;
-                a.pos = pos;
-                a.inv_freq = e->w.inv_freq;
-                a.rope_tab = tab;
-                RC(attention_decode(a, st));
-            } else {
-                a.nsplit = 1;
-                a.chunk = c.max_text;
-                RC(attention(a, st));
-            }
+            r.ldx = e->q_dim;
+            r.nq = c.n_heads;
+            r.rope_q = 1;
+            RC(rope_store(r, st));
+            RC(attn_packed(e, M, q, tok_row, tok_t, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, st));
         }
         RC(gemm(att, e->q_dim, M, L.cross_o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
                 s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode));
-        if (!lead_gu) {
-            NormArgs n = norm_args(M, d, c.rms_eps);
-            if (s_o > 1) {
-                n.part = e->part;
-                n.nsplit = s_o;
-                n.ldp = d;
-            } else {
-                n.delta = tmp;
-            }
-            n.post_w = (const bf16_t*)L.norms[3];
-            n.resid = h;
-            n.pre_w = (const bf16_t*)L.norms[4];
-            n.resid_out = h;
-            n.normed_out = xn;
-            RC(resid_norm(n, st));
-        }
-        // --- GeGLU MLP (decode: the one-block-per-CU GEMV unless T5G_GU_GEMV=0)
-        if (lead_gu) {
-            RC(lead_gemv(L.gate_up, 2 * f, act, f, s_o, L.norms[3], L.norms[4], 3 * l + 2, EPI_GEGLU));
-        } else if (decode && e->gu_gemv && M <= 16) {
+        RC(resid(s_o, L.norms[3], L.norms[4]));
+        // --- GeGLU MLP (decode: the one-block-per-CU GEMV)
+        if (decode && M <= 16) {
             DecGemmArgs g = dec_args(M, L.gate_up, 2 * f, d, act, f, 8);
             g.X = xn;
             g.ldx = d;
             g.un = 8;
-            RC(gemv_dec(g, EPI_GEGLU, PRO_LOAD, st));
+            RC(gemv_dec(g, EPI_GEGLU, st));
         } else {
             RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st, !decode));
         }
-        if (decode && e->down_gemv && M <= 16 && s_down > 1) {
-            DecGemmArgs g = dec_args(M, L.down, d, f, e->part, d, 8);
-            g.X = act;
-            g.ldx = f;
-            g.un = 8;
-            g.splits = s_down;
-            RC(gemv_dec(g, EPI_F32, PRO_LOAD, st));
-        } else {
-            RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, s_down > 1 ? (void*)e->part : (void*)tmp, d,
-                    s_down > 1 ? EPI_F32 : EPI_BF16, st, !decode));
-        }
-        if (!(lead && (e->lead_sites & 1)) || l == c.n_dec_layers - 1) {
-            NormArgs n = norm_args(M, d, c.rms_eps);
-            if (s_down > 1) {
-                n.part = e->part;
-                n.nsplit = s_down;
-                n.ldp = d;
-            } else {
-                n.delta = tmp;
-            }
-            n.post_w = (const bf16_t*)L.norms[5];
-            n.resid = h;
-            const bool last = l == c.n_dec_layers - 1;
-            n.pre_w = (const bf16_t*)(last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]);
-            n.resid_out = h;
-            n.normed_out = xn;
-            RC(resid_norm(n, st));
-        }
+        RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, s_down > 1 ? (void*)e->part : (void*)tmp, d,
+                s_down > 1 ? EPI_F32 : EPI_BF16, st, !decode));
+        const bool last = l == c.n_dec_layers - 1;
+        RC(resid(s_down, L.norms[5], last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]));
     }
     return T5G_OK;
-}
-
-// ---------------------------------------------------------------------------
-// Fused single-token decoder step (sdpa numerics, M <= 16 rows): 9 launches per layer.
-//   qkv   : [norm prologue: previous down output + residual, post_ff/pre_self] -> fp32 q|k|v
-//   attn  : self attention (PM-RoPE of q/k, k/v append) + split merge
-//   o     : att -> bf16 v
-//   cq    : [norm prologue: post_self/pre_cross] -> fp32 q
-//   cattn : cross attention over the cached encoder K/V
-//   co    : att -> bf16 v
-//   gu    : [norm prologue: post_cross/pre_ff] -> GeGLU -> act
-//   down  : act (direct from L2) -> bf16 v
-// then head1 with the final-norm prologue, head2 (PMDecoderLayer.forward :256-323,
-// decoder final norm [tf] :818, predict_layer :469-478).
-static bool fused_ok(const t5g_engine* e, int M) {
-    const t5g_config& c = e->c;
-    return e->fused_decode && !(c.softcap > 0.f) && M >= 1 && M <= 16 && c.hidden % 32 == 0 &&
-           c.hidden <= 4096 && (c.hidden <= 2560 || M <= 8) && c.intermediate % 32 == 0;
-}
-
-// row-major VALU GEMVs: every decoder projection has its plain copy, batch <= 8 rows
-static bool rm_ok(const t5g_engine* e, int M) {
-    if (!fused_ok(e, M) || e->fused_p16 || M > 8 || e->c.hidden > 2560 || !e->w.rm_head1) return false;
-    for (const t5g_layer_weights& L : e->dec)
-        if (!L.rm_qkv || !L.rm_o || !L.rm_gate_up || !L.rm_down || !L.rm_cross_q || !L.rm_cross_o) return false;
-    return true;
 }
 
 static DecGemmArgs dec_args(int M, const void* W, int N, int K, void* Y, int ldy, int nw) {
@@ -774,165 +559,9 @@ static DecGemmArgs dec_args(int M, const void* W, int N, int K, void* Y, int ldy
     return g;
 }
 
-static int decode_fused(t5g_engine* e, bool rm, hipStream_t st) {
-    const t5g_config& c = e->c;
-    // rm: plain row-major weights on the VALU GEMV (exact rows per CU); else P16 on MFMA
-    auto gv = [&](DecGemmArgs& g, const void* w_rm, int epi, int pro) -> int {
-        if (!rm) return gemv_dec(g, epi, pro, st);
-        g.W = (const bf16_t*)w_rm;
-        return gemv_rm(g, epi, pro, st);
-    };
-    const int M = e->B, d = c.hidden, f = c.intermediate, D = c.head_dim;
-    const int G = c.n_heads / c.n_kv_heads;
-    const int nw_norm = M <= 8 ? 4 : 8;       // prologue rows per wave <= 2
-    const int nw_wide = M <= 8 ? 8 : 8;
-    bf16_t* hb[2] = {e->dh, e->dh2};
-    int hc = 0;
-    RC(rope_table(e->next_pos, e->w.inv_freq, M, D, e->rope_tab, st));
-    auto norm_pro = [&](DecGemmArgs& g, const void* post_w, const void* pre_w, bool keep) {
-        g.v = e->dv;
-        g.h_in = hb[hc];
-        g.post_w = (const bf16_t*)post_w;
-        g.pre_w = (const bf16_t*)pre_w;
-        g.eps = c.rms_eps;
-        g.h_out = keep ? hb[hc ^ 1] : nullptr;
-        hc ^= 1;
-    };
-    for (int l = 0; l < c.n_dec_layers; ++l) {
-        const t5g_layer_weights& L = e->dec[l];
-        // --- self attention
-        {
-            DecGemmArgs g = dec_args(M, L.qkv, e->qkv_dim, d, e->part, e->qkv_dim, nw_wide);
-            int pro;
-            if (l == 0) {
-                pro = PRO_EMBED;
-                g.ids = e->next_token;
-                g.table = (const bf16_t*)e->w.audio_embed;
-                g.scale = c.normalizer;
-                g.pre_w = (const bf16_t*)L.norms[0];
-                g.eps = c.rms_eps;
-                g.h_out = hb[0];
-                hc = 0;
-            } else {
-                pro = PRO_NORM;
-                norm_pro(g, e->dec[l - 1].norms[5], L.norms[0], true);
-            }
-            RC(gv(g, L.rm_qkv, EPI_F32, pro));
-        }
-        {
-            AttnArgs a;
-            memset(&a, 0, sizeof(a));
-            a.Q = e->dq;
-            a.ldq = e->q_dim;
-            a.Mq = M;
-            a.K = e->sk[l];
-            a.V = e->sv[l];
-            a.kv_hstride = (long)c.max_audio * D;
-            a.kv_bstride = a.kv_hstride * c.n_kv_heads;
-            a.kv_len = e->kv_len;
-            a.Hkv = c.n_kv_heads;
-            a.D = D;
-            a.G = G;
-            a.causal = 1;
-            a.window = c.dec_sliding[l] ? c.sliding_window : 0;
-            a.scale = c.attn_scale;
-            a.O = e->datt;
-            a.ldo = e->q_dim;
-            a.chunk = 64;
-            a.nsplit = (c.max_audio + 63) / 64;
-            a.kv_cap = c.max_audio;
-            a.part = e->apart;
-            a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
-            a.Qpart = e->part;
-            a.q_nsplit = 1;
-            a.ldqp = e->qkv_dim;
-            a.pos = e->next_pos;
-            a.inv_freq = e->w.inv_freq;
-            a.rope_tab = e->rope_tab;
-            a.append = 1;
-            a.k_col0 = e->q_dim;
-            a.v_col0 = e->q_dim + e->kv_dim;
-            RC(attention_decode(a, st));
-        }
-        {
-            DecGemmArgs g = dec_args(M, L.o, d, e->q_dim, e->dv, d, nw_wide);
-            g.X = e->datt;
-            g.ldx = e->q_dim;
-            RC(gv(g, L.rm_o, EPI_BF16, rm ? PRO_DIRECT : PRO_LOAD));
-        }
-        // --- PM cross attention
-        {
-            DecGemmArgs g = dec_args(M, L.cross_q, e->q_dim, d, e->part, e->q_dim, nw_wide);
-            norm_pro(g, L.norms[1], L.norms[2], true);
-            RC(gv(g, L.rm_cross_q, EPI_F32, PRO_NORM));
-        }
-        {
-            AttnArgs a;
-            memset(&a, 0, sizeof(a));
-            a.Q = e->dq;
-            a.ldq = e->q_dim;
-            a.Mq = M;
-            a.K = e->ck[l];
-            a.V = e->cv[l];
-            a.kv_hstride = (long)c.max_text * D;
-            a.kv_bstride = a.kv_hstride * c.n_kv_heads;
-            a.kv_len = e->enc_len;
-            a.Hkv = c.n_kv_heads;
-            a.D = D;
-            a.G = G;
-            a.causal = 0;
-            a.scale = c.attn_scale;
-            a.O = e->datt;
-            a.ldo = e->q_dim;
-            a.chunk = 64;
-            a.nsplit = e->xsplit;
-            a.kv_cap = c.max_text;
-            a.part = e->apart;
-            a.counters = e->attn_tickets ? e->attn_tickets_buf : nullptr;
-            a.Qpart = e->part;
-            a.q_nsplit = 1;
-            a.ldqp = e->q_dim;
-            a.pos = e->next_pos;
-            a.inv_freq = e->w.inv_freq;
-            a.rope_tab = e->rope_tab;
-            RC(attention_decode(a, st));
-        }
-        {
-            DecGemmArgs g = dec_args(M, L.cross_o, d, e->q_dim, e->dv, d, nw_wide);
-            g.X = e->datt;
-            g.ldx = e->q_dim;
-            RC(gv(g, L.rm_cross_o, EPI_BF16, rm ? PRO_DIRECT : PRO_LOAD));
-        }
-        // --- GeGLU MLP
-        {
-            DecGemmArgs g = dec_args(M, L.gate_up, 2 * f, d, e->dact, f, nw_norm);
-            norm_pro(g, L.norms[3], L.norms[4], true);
-            RC(gv(g, L.rm_gate_up, EPI_GEGLU, PRO_NORM));
-        }
-        {
-            DecGemmArgs g = dec_args(M, L.down, d, f, e->dv, d, nw_wide);
-            g.X = e->dact;
-            g.ldx = f;
-            RC(gv(g, L.rm_down, EPI_BF16, PRO_DIRECT));
-        }
-    }
-    // predict head: final decoder norm fused into head1's prologue
-    {
-        DecGemmArgs g = dec_args(M, e->w.head1, d, d, e->dhh, d, nw_wide);
-        norm_pro(g, e->dec[c.n_dec_layers - 1].norms[5], e->w.dec_final_norm, false);
-        g.x_out = e->dxn;
-        g.bias = (const bf16_t*)e->w.head1_bias;
-        RC(gv(g, e->w.rm_head1, EPI_BIAS_GELU, PRO_NORM));
-    }
-    RC(gemm(e->dhh, d, M, e->w.head2, e->V, d, 1, e->w.head2_bias, e->logits, e->logits_ld, EPI_BIAS_BF16, st));
-    return T5G_OK;
-}
-
 // one decoder step + predict head for the e->B rows fed by the sampler buffers
 static int head(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st);
 static int decode_forward(t5g_engine* e, hipStream_t st) {
-    if (rm_ok(e, e->B)) return decode_fused(e, true, st);
-    if (fused_ok(e, e->B) && e->fused_p16) return decode_fused(e, false, st);
     int rc = decoder_pass(e, e->B, e->next_token, nullptr, nullptr, e->next_pos, true, st);
     if (rc) return rc;
     return head(e, e->dxn, e->B, st);
@@ -1087,10 +716,8 @@ extern "C" int t5g_read_tokens(t5g_engine* e, int32_t* out, int32_t B, void* str
     if (!e || !out || B <= 0 || B > e->c.max_batch) return T5G_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipMemcpyAsync(out, e->out_tokens, (size_t)B * e->c.max_gen * sizeof(int), hipMemcpyDeviceToHost, st));
-    unsigned tmo = 0;
-    HIPCHK(hipMemcpyAsync(&tmo, e->lead_tmo, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    return tmo ? T5G_ESYNC : T5G_OK;
+    return T5G_OK;
 }
 
 extern "C" int t5g_write_state(t5g_engine* e, const t5g_sampler_state* s, int32_t row, int32_t slot, int32_t token,
@@ -1202,10 +829,19 @@ extern "C" int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, 
     return T5G_OK;
 }
 
+// work = partial P.V slabs | scores | chunk maxima (fp32)
+static void attn_work_layout(int B, int Hq, int Hkv, int D, int cap, int64_t* part, int64_t* sc, int64_t* mx) {
+    const int64_t nsplit = (cap + 63) / 64;
+    *part = (int64_t)B * Hkv * nsplit * (Hq / Hkv) * (D + 2);
+    *sc = (int64_t)B * Hq * cap;
+    *mx = (int64_t)B * Hkv * nsplit * (Hq / Hkv);
+}
+
 extern "C" int64_t t5g_attention_decode_work_bytes(int32_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t cap) {
     if (B <= 0 || Hkv <= 0 || Hq % Hkv || D <= 0 || cap <= 0) return -1;
-    const int64_t nsplit = (cap + 63) / 64;
-    return (int64_t)B * Hkv * nsplit * (Hq / Hkv) * (D + 2) * 4;
+    int64_t p, s, m;
+    attn_work_layout(B, Hq, Hkv, D, cap, &p, &s, &m);
+    return (p + s + m) * 4;
 }
 
 extern "C" int t5g_attention_decode(const t5g_attn_decode_args* g, void* stream) {
@@ -1233,7 +869,11 @@ extern "C" int t5g_attention_decode(const t5g_attn_decode_args* g, void* stream)
     a.chunk = 64;
     a.nsplit = (g->cap + 63) / 64;
     a.kv_cap = g->cap;
+    int64_t np, ns, nm;
+    attn_work_layout(g->B, g->n_heads, g->n_kv_heads, g->head_dim, g->cap, &np, &ns, &nm);
     a.part = (float*)g->work;
+    a.sbuf = a.part + np;
+    a.mbuf = a.sbuf + ns;
     RC(attention_decode(a, (hipStream_t)stream));
     return T5G_OK;
 }
@@ -1242,20 +882,11 @@ static_assert(sizeof(t5g_gemv_args) == 152, "t5g_gemv_args layout");
 
 static int gemv_from_abi(const t5g_gemv_args* g, const void* W, DecGemmArgs* out) {
     if (!g || !W || !g->Y || g->M <= 0 || g->N <= 0 || g->K <= 0 || g->K % 32) return T5G_EINVAL;
+    if (g->pro != 0 || g->layout != 0) return T5G_EUNSUPPORTED;   // prologue variants were removed
     DecGemmArgs a = dec_args(g->M, W, g->N, g->K, g->Y, g->ldy, g->nw);
     a.X = (const bf16_t*)g->X;
     a.ldx = g->ldx;
-    a.v = (const bf16_t*)g->v;
-    a.h_in = (const bf16_t*)g->h_in;
-    a.ids = g->ids;
-    a.table = (const bf16_t*)g->table;
-    a.scale = g->scale;
-    a.eps = g->eps;
-    a.post_w = (const bf16_t*)g->post_w;
-    a.pre_w = (const bf16_t*)g->pre_w;
     a.bias = (const bf16_t*)g->bias;
-    a.h_out = (bf16_t*)g->h_out;
-    a.x_out = (bf16_t*)g->x_out;
     a.un = g->un;
     a.max_grid = g->max_grid;
     a.splits = g->splits > 1 ? g->splits : 1;
@@ -1263,15 +894,11 @@ static int gemv_from_abi(const t5g_gemv_args* g, const void* W, DecGemmArgs* out
     return T5G_OK;
 }
 
-static int gemv_any(const DecGemmArgs& a, const t5g_gemv_args* g, hipStream_t st) {
-    return g->layout == 1 ? gemv_rm(a, g->epi, g->pro, st) : gemv_dec(a, g->epi, g->pro, st);
-}
-
 extern "C" int t5g_gemv(const t5g_gemv_args* g, void* stream) {
     DecGemmArgs a;
     int rc = gemv_from_abi(g, g ? g->W : nullptr, &a);
     if (rc) return rc;
-    RC(gemv_any(a, g, (hipStream_t)stream));
+    RC(gemv_dec(a, g->epi, (hipStream_t)stream));
     return T5G_OK;
 }
 
@@ -1287,9 +914,9 @@ extern "C" int t5g_time_gemv(const t5g_gemv_args* g, const void* const* Wp_list,
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    RC(gemv_any(as[0], g, st));  // warm
+    RC(gemv_dec(as[0], g->epi, st));  // warm
     HIPCHK(hipEventRecord(e0, st));
-    for (int i = 0; i < iters; ++i) RC(gemv_any(as[i % n_w], g, st));
+    for (int i = 0; i < iters; ++i) RC(gemv_dec(as[i % n_w], g->epi, st));
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;

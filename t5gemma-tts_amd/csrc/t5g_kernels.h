@@ -26,51 +26,23 @@ struct GemmArgs {
 int pack_p16(const bf16_t* src, int N, int K, long ld, bf16_t* dst, int NGpad, hipStream_t st);
 int gemm_p16(const GemmArgs& a, int epi, hipStream_t st);
 
-// ---- decode-step GEMV family (M <= 16) with fused row prologues (gemv.hip) ----
-// The X rows are produced inside the GEMM, in every block, from the previous
-// sub-block's bf16 output: residual add + the two RMSNorms of PMDecoderLayer
-// (PRO_NORM), or the audio embedding gather (PRO_EMBED). Outputs are whole (no
-// split-K), so the next consumer can run the same prologue on them.
-// PRO_LEAD: blocks 0..M-1 each finish ONE row of the previous sub-block (sum of its
-// fp32 split-K slabs, post-norm, residual add, pre-norm: exactly resid_norm_kernel),
-// publish it (sc1 stores + a per-row flag), and every block stages the rows after
-// polling the M flags -- the separate norm launch disappears from the chain.
-enum { PRO_LOAD = 0, PRO_NORM = 1, PRO_EMBED = 2, PRO_DIRECT = 3, PRO_LEAD = 4 };
+// ---- decode-step GEMV (M <= 16 rows, gemv.hip) ----------------------------------
 struct DecGemmArgs {
     int M, K;                 // rows (<= 16), reduction length (= X row width)
     const bf16_t* W;          // packed P16
     int N, NG, KB;
     const bf16_t* bias;
-    void* Y;                  // bf16 or fp32 [M][ldy]
+    void* Y;                  // bf16 or fp32 [M][ldy] (EPI_F32 split-K: [splits][M][ldy])
     int ldy;
-    const bf16_t* X;          // PRO_LOAD / PRO_DIRECT: [M][ldx]
+    const bf16_t* X;          // [M][ldx], staged through LDS
     int ldx;
-    const bf16_t* v;          // PRO_NORM: sub-block output [M][K] (bf16)
-    const bf16_t* h_in;       // PRO_NORM: residual stream [M][K]
-    const int* ids;           // PRO_EMBED: token ids [M]
-    const bf16_t* table;      // PRO_EMBED: embedding [vocab][K]
-    float scale;              // PRO_EMBED: normalizer
-    const bf16_t* post_w;     // PRO_NORM: RMSNorm(1+w) applied to v before the residual add
-    const bf16_t* pre_w;      // PRO_NORM / PRO_EMBED: RMSNorm(1+w) producing X
-    float eps;
-    bf16_t* h_out;            // block 0 writes the updated residual (may be null)
-    bf16_t* x_out;            // block 0 writes the normed X rows (may be null)
     int nw;                   // waves per block (4, 8 or 16)
     int un;                   // fragments in flight per wave (8 / 16), 0 = default
     int max_grid;             // blocks per launch cap, 0 = one per CU
-    int splits;               // split-K over blockIdx.y (EPI_F32 slabs [splits][M][ldy]; PRO_LOAD/DIRECT)
-    // PRO_LEAD: the row producer's operands (X above is the normed output it publishes;
-    // h_in/h_out the residual stream, post_w/pre_w the two norms)
-    const float* part;        // fp32 split-K slabs [nsplit_p][M][ldp] of the previous Linear
-    int nsplit_p, ldp;
-    unsigned* flags;          // [M] per-row publish words (hold the last step's epoch)
-    unsigned* tmo;            // set to 1 when a bounded flag poll gives up (never expected)
-    const unsigned* epoch;    // this step's epoch (advanced by rope_table_kernel, never 0)
+    int splits;               // split-K over blockIdx.y (EPI_F32 only)
 };
-int gemv_dec(const DecGemmArgs& a, int epi, int pro, hipStream_t st);
-size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int pro, int rg);
-// row-major VALU variant (W = plain [N][K]; GeGLU: gate rows then up rows), M <= 8
-int gemv_rm(const DecGemmArgs& a, int epi, int pro, hipStream_t st);
+int gemv_dec(const DecGemmArgs& a, int epi, hipStream_t st);
+size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int rg);
 
 // ---- row-wise residual / RMSNorm / embedding -------------------------------
 struct NormArgs {
@@ -115,9 +87,7 @@ struct RopeArgs {
 };
 int rope_store(const RopeArgs& a, hipStream_t st);
 // tab[r][i] = bf16(cos(inv_freq[i] * pos[r])), tab[r][D/2 + i] = bf16(sin(...)), r < rows
-// epoch (optional): advanced once per call (the decode step's PRO_LEAD epoch)
-int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st,
-               unsigned* epoch = nullptr);
+int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st);
 
 // ---- attention ----------------------------------------------------------------
 struct AttnArgs {
@@ -134,8 +104,8 @@ struct AttnArgs {
     int window;              // 0 none; causal: k > t-W; bidirectional: |t-k| <= W
     float scale, softcap;
     int eager;               // eager numerics (bf16 scores, normalised bf16 probs)
-    int nsplit, chunk;       // split keys over blockIdx.z
-    float* part;             // partial slabs when nsplit > 1
+    int nsplit, chunk;       // decode: 64-key chunks (nsplit = ceil(kv_cap / 64)); packed: 1, chunk = Lmax
+    float* part;             // decode partial P.V slabs [Mq][Hkv][nsplit][G][D + 2]
     bf16_t* O;               // [Mq][ldo]
     int ldo;
     // decode extras: q straight from the projection's fp32 split-K slabs, PM-RoPE'd in-kernel
@@ -143,7 +113,8 @@ struct AttnArgs {
     int q_nsplit, ldqp;
     const float* pos;        // [rows] float PM positions for the q rotation
     const float* inv_freq;   // [D/2]
-    int* counters;           // [Mq][Hkv] arrival tickets: the last split block merges (zeroed)
+    float* sbuf;             // decode, rows of > 64 keys: scores [Mq][Hkv*G][kv_cap] fp32
+    float* mbuf;             // decode: per-chunk score maxima [Mq][Hkv][nsplit][G]
     const float* rope_tab;   // optional per-row cos/sin table (see rope_table)
     int kv_cap;              // allocated keys per (row, head): speculative loads stay below it
     // decode self-attention: the block holding key t = kv_len-1 builds it from the
@@ -152,7 +123,7 @@ struct AttnArgs {
     int dbg_seq;             // diagnostic timeline slot (T5G_DBG_TS builds only)
 };
 int attention(const AttnArgs& a, hipStream_t st);
-// decode-shaped (64-key blocks, split over blockIdx.z, sdpa numerics); nsplit = ceil(keys/64)
+// decode-shaped (64-key chunks over blockIdx.z + P.V / combine launches, sdpa numerics)
 int attention_decode(const AttnArgs& a, hipStream_t st);
 
 // ---- sampler -------------------------------------------------------------------

@@ -15,8 +15,6 @@ arithmetic on activations runs in the HIP kernels.
 """
 from __future__ import annotations
 
-import os
-
 import ctypes as C
 import math
 from dataclasses import dataclass, field
@@ -150,16 +148,6 @@ class T5GemmaTTSEngine:
             for j, nm in enumerate(names):
                 key = f"{p}.{nm}.weight"
                 lw.norms[j] = keep(w(key)) if key in state_dict else None
-            if side == "decoder" and os.environ.get("T5G_FUSED_DECODE", "") == "1":
-                # plain row-major copies for the opt-in VALU decode GEMVs (csrc/gemv.hip
-                # gemv_rm_kernel: exact N/256 rows per CU, norm prologues fused)
-                lw.rm_qkv = keep(torch.cat([w(f"{p}.self_attn.q_proj.weight"), w(f"{p}.self_attn.k_proj.weight"),
-                                            w(f"{p}.self_attn.v_proj.weight")], 0))
-                lw.rm_o = keep(w(f"{p}.self_attn.o_proj.weight"))
-                lw.rm_gate_up = keep(torch.cat([w(f"{p}.mlp.gate_proj.weight"), w(f"{p}.mlp.up_proj.weight")], 0))
-                lw.rm_down = keep(w(f"{p}.mlp.down_proj.weight"))
-                lw.rm_cross_q = keep(w(f"{p}.cross_attn.q_proj.weight"))
-                lw.rm_cross_o = keep(w(f"{p}.cross_attn.o_proj.weight"))
             if side == "decoder":
                 lw.cross_q = pack(w(f"{p}.cross_attn.q_proj.weight"))
                 lw.cross_kv = pack(torch.cat([w(f"{p}.cross_attn.k_proj.weight"),
@@ -177,8 +165,6 @@ class T5GemmaTTSEngine:
         W.enc_final_norm = keep(w("backbone.model.encoder.norm.weight"))
         W.dec_final_norm = keep(w("backbone.model.decoder.norm.weight"))
         W.head1 = pack(w("predict_layer.0.0.weight"))
-        if os.environ.get("T5G_FUSED_DECODE", "") == "1":
-            W.rm_head1 = keep(w("predict_layer.0.0.weight"))
         W.head1_bias = keep(w("predict_layer.0.0.bias"))
         W.head2 = pack(w("predict_layer.0.2.weight"))
         W.head2_bias = keep(w("predict_layer.0.2.bias"))

@@ -140,41 +140,83 @@ def _eos_token(model_args):
     return getattr(model_args, "eos", getattr(model_args, "eog", None))
 
 
+def parse_silence_tokens(v):
+    """decode_config["silence_tokens"] may be a list or its string form ("[1, 2]"); the
+    reference eval()s the string (inference_tts_utils.py:175-176) -- a literal parse here."""
+    if isinstance(v, str):
+        import ast
+        v = ast.literal_eval(v.strip() or "[]")
+    return [int(s) for s in (v or [])]
+
+
+def _no_audio(audio_fn) -> bool:
+    return audio_fn is None or (isinstance(audio_fn, str) and audio_fn.strip().lower() in {"", "none", "null"})
+
+
+def prompt_codes_from(audio_fn, audio_tokenizer, prompt_end_frame: int, prompt_sample_rate: int):
+    """The reference prompt as codec ids [1, 1, T] (inference_tts_utils.py:182-206).
+
+    ``audio_fn`` is, as in the reference, a path to the reference audio -- loaded, cut to
+    ``prompt_end_frame`` samples (its own rate, > 0), resampled to 16 kHz and encoded by
+    ``audio_tokenizer.encode`` (data/tokenizer.py:125-143) -- or, in this build, already
+    encoded codec ids (list / 1-D / [1, T] / [1, 1, T] / [1, T, 1]), cut to the codes those
+    samples encode to at ``prompt_sample_rate``."""
+    if isinstance(audio_fn, str):
+        from .audio import load_audio, resample
+        n = int(prompt_end_frame) if prompt_end_frame and prompt_end_frame > 0 else -1
+        wav, sr = load_audio(audio_fn, num_frames=n)
+        target = int(getattr(audio_tokenizer, "encode_sample_rate", 16000))
+        if sr != target:
+            wav = resample(wav.float(), sr, target)
+        if wav.shape[0] == 2:
+            wav = wav.mean(dim=0, keepdim=True)
+        return audio_tokenizer.encode(wav.unsqueeze(0))
+    frames = torch.as_tensor(audio_fn, dtype=torch.long)
+    if prompt_end_frame and prompt_end_frame > 0:
+        flat = frames.reshape(-1)
+        frames = flat[:prompt_frames_for_samples(int(prompt_end_frame), int(prompt_sample_rate))]
+    return frames
+
+
 @torch.no_grad()
-def inference_one_sample(model, model_args, text_tokenizer, audio_tokenizer, prompt_codes, target_text, lang,
+def inference_one_sample(model, model_args, text_tokenizer, audio_tokenizer, audio_fn, target_text, lang,
                          device, decode_config, prompt_end_frame, target_generation_length, prefix_transcript=None,
                          quiet=False, repeat_prompt=0, multi_trial=None, return_frames=False, seed=None,
                          parity=True, prompt_sample_rate=CODEC_INPUT_SR):
-    """Same arguments and returns as the reference (inference_tts_utils.py:140-378),
-    except that ``prompt_codes`` (codec ids of the reference audio, or None) replaces
-    ``audio_fn``. ``prompt_end_frame`` keeps the reference's units -- a count of audio
-    SAMPLES of the reference file at ``prompt_sample_rate`` (its own rate, e.g.
-    ``int(cut_off_sec * sr)``) -- and keeps the codes those samples encode to
-    (``prompt_frames_for_samples``). ``parity=True`` (default) draws the sampling noise
-    from torch's global generator like the reference; ``seed`` gives the row its own
-    ``manual_seed`` stream instead. ``lang``/``device`` are accepted for signature
-    compatibility (the engine's device wins)."""
+    """Same arguments, errors and returns as the reference (inference_tts_utils.py:141-379).
+
+    ``audio_fn``: the reference audio (path, encoded by ``audio_tokenizer.encode``) or its
+    codec ids (see ``prompt_codes_from``); None / "none" for no reference.
+    ``prompt_end_frame`` keeps the reference's units -- a count of audio SAMPLES of the
+    reference file (``int(cut_off_sec * sr)``); for code input the file's rate is
+    ``prompt_sample_rate``. Text is normalised like the reference (Japanese only, the
+    language resolved once, ``text.normalize_text_with_lang``). ``parity=True`` (default)
+    draws the sampling noise from torch's global generator like the reference; ``seed``
+    gives the row its own ``manual_seed`` stream instead. ``device`` is accepted for
+    signature compatibility (the engine's device wins)."""
+    from .text import normalize_text_with_lang
     multi_trial = multi_trial or []
     if int(getattr(model_args, "n_codebooks", 1)) != 1:
         raise ValueError("XCodec2 backend supports only n_codebooks=1.")
-    if multi_trial:
-        raise AssertionError("multi_trial is not supported (reference asserts multi_trial == [])")
-    if int(decode_config.get("sample_batch_size", 1) or 1) > 1:
-        raise AssertionError("sample_batch_size must be <= 1 (inference_tts_utils.py:288)")
-    codec_sr = float(decode_config["codec_sr"])
-    silence = decode_config.get("silence_tokens", []) or []
-    if isinstance(silence, str):
-        silence = [int(v) for v in silence.strip("[]() ").split(",") if v.strip()]
-    if prompt_codes is not None and prompt_end_frame and prompt_end_frame > 0:
-        pc = torch.as_tensor(prompt_codes).reshape(-1)
-        prompt_codes = pc[:prompt_frames_for_samples(int(prompt_end_frame), int(prompt_sample_rate))]
+    codec_sr = int(decode_config["codec_sr"])
+    silence = parse_silence_tokens(decode_config.get("silence_tokens", []))
+    has_ref = not _no_audio(audio_fn)
+    prompt_codes = prompt_codes_from(audio_fn, audio_tokenizer, prompt_end_frame, prompt_sample_rate) \
+        if has_ref else None
     original_audio = build_prompt(prompt_codes, getattr(model_args, "y_sep_token", None), codec_sr,
                                   target_generation_length, repeat_prompt,
                                   float(getattr(model_args, "audio_max_length", 40.0)))
-    has_ref = prompt_codes is not None and original_audio.shape[1] > 0
     prompt_frames = original_audio.shape[1]
+    if isinstance(target_text, str):
+        target_text, lang = normalize_text_with_lang(target_text, lang)
+    if prefix_transcript and isinstance(prefix_transcript, str):
+        prefix_transcript, _ = normalize_text_with_lang(prefix_transcript, lang)
     ids = build_text_tokens(target_text, prefix_transcript, text_tokenizer, getattr(model_args, "x_sep_token", None),
                             getattr(model_args, "add_eos_to_text", 0), getattr(model_args, "add_bos_to_text", 0))
+    if int(decode_config.get("sample_batch_size", 1) or 1) > 1:
+        raise AssertionError("sample_batch_size must be <= 1 (inference_tts_utils.py:288)")
+    if multi_trial:
+        raise AssertionError("multi_trial is not supported (reference asserts multi_trial == [])")
     x = torch.LongTensor(ids).unsqueeze(0)
     x_lens = torch.LongTensor([x.shape[-1]])
     tgt = torch.LongTensor([target_length(prompt_frames, codec_sr, target_generation_length,
@@ -184,7 +226,8 @@ def inference_one_sample(model, model_args, text_tokenizer, audio_tokenizer, pro
         x, x_lens, original_audio, tgt_y_lens=tgt, top_k=decode_config["top_k"], top_p=decode_config["top_p"],
         min_p=decode_config.get("min_p", 0.0), temperature=decode_config["temperature"],
         stop_repetition=decode_config.get("stop_repetition", 3), silence_tokens=silence,
-        prompt_frames=prompt_frames, seeds=None if seed is None else [int(seed)], parity=parity)
+        prompt_frames=prompt_frames, **({} if seed is None else {"seeds": [int(seed)]}),
+        **({} if parity else {"parity": False}))
     dt = time.time() - t0
     n = gen_frames.shape[-1]
     if not quiet:

@@ -1,10 +1,10 @@
-"""Decode attention through the C ABI (t5g_attention_decode: the split-K decode kernel +
-combine the engine runs every step) against an fp64 softmax-attention reference of the
-same bf16 q / K / V, at the C3 lengths: self attention over L in {1, 63, 64, 65, 152,
-527, 903} keys (1 to 15 key chunks per (row, kv head), ragged rows in one launch) and
-cross attention over T_x = 60 encoder keys. Reference semantics:
-[tf] T5GemmaSelfAttention :264-304 / PMCrossAttention :167-253 through torch's CPU
-SDPA, whose bf16 path rounds exp(s - max) to bf16 before P.V."""
+"""Decode attention through the C ABI (t5g_attention_decode: the kernels the engine runs
+every step) against the reference's attention numerics -- torch's CPU SDPA on bf16
+([tf] T5GemmaSelfAttention :264-304 / PMCrossAttention :167-253), restated in
+oracle/sdpa_emu.py and pinned bitwise to torch there -- and against exact fp64 softmax
+attention, at the C3 lengths: self attention over L in {1, 63, 64, 65, 152, 527, 903}
+keys (1 to 15 64-key chunks per (row, kv head), one or two aten 512-key blocks, ragged
+rows in one launch) and cross attention over T_x = 60 encoder keys."""
 import ctypes as C
 
 import pytest
@@ -19,24 +19,27 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-def _reference(q, K, V, lens, scale, causal, pround):
-    """fp64 attention per row over its first lens[b] keys (query = last key). pround:
-    exp values rounded to bf16 before P.V (CPU SDPA bf16 numerics); else exact."""
+def _reference(q, K, V, lens, scale, causal):
+    """aten CPU SDPA numerics (oracle/sdpa_emu.py, pinned bitwise to torch here) per row
+    over its first lens[b] keys; the query is the row's last key."""
+    from oracle import sdpa_emu
     B, Hq, D = q.shape
-    Hkv = K.shape[1]
-    G = Hq // Hkv
+    out = torch.zeros(B, Hq, D, dtype=torch.float64)
+    for b in range(B):
+        L = int(lens[b])
+        out[b] = sdpa_emu.attention(q[b][:, None], K[b, :, :L], V[b, :, :L], scale)[:, 0].double()
+    return out
+
+
+def _exact(q, K, V, lens, scale):
+    B, Hq, D = q.shape
+    G = Hq // K.shape[1]
     out = torch.zeros(B, Hq, D, dtype=torch.float64)
     for b in range(B):
         L = int(lens[b])
         for h in range(Hq):
-            k = K[b, h // G, :L].double()
-            v = V[b, h // G, :L].double()
-            s = (k @ q[b, h].double()).float() * scale
-            p = torch.exp((s - s.max()).double())
-            l = p.sum()
-            if pround:
-                p = p.float().to(BF16).double()
-            out[b, h] = (p @ v) / l
+            s = (K[b, h // G, :L].double() @ q[b, h].double()) * scale
+            out[b, h] = torch.softmax(s, 0) @ V[b, h // G, :L].double()
     return out
 
 
@@ -66,29 +69,23 @@ def _run(L, B, lens, Hq=8, Hkv=4, D=256, causal=1, seed=0):
 
 
 @pytest.mark.parametrize("L", [1, 63, 64, 65, 152, 527, 903])
-def test_self_attention_decode_vs_fp64(L):
-    """8 rows x 8 q heads / 4 kv heads x 256 (2b-2b), ragged lengths up to L."""
+def test_self_attention_decode_vs_cpu_sdpa(L):
+    """8 rows x 8 q heads / 4 kv heads x 256 (2b-2b), ragged lengths up to L: rows of > 64
+    keys go through the three-launch path (scores, P.V, combine), the others one launch.
+    Bit-equal to aten's CPU SDPA numerics except fp32 GEMM-order flips (<= 1 ulp)."""
     _need_gpu()
     B = 8
     lens = [L, max(1, L - 1), max(1, L // 2), max(1, L - 64), 1, max(1, L - 3), max(1, (3 * L) // 4), L]
     got, q, K, V = _run(L, B, lens, seed=L)
-    exact = _reference(q, K, V, lens, 256 ** -0.5, True, pround=False)
-    emu = _reference(q, K, V, lens, 256 ** -0.5, True, pround=True)
-    # bf16 output: half an ulp of the result + fp32 accumulation; the P-rounding of the
-    # reference numerics moves a value by at most 2^-9 relative per term, i.e. <= 2^-9 of
-    # sum_j p_j |v_j| / l  (bounded by max |v| <= ~5 for these draws)
-    vmax = V.abs().max().item()
-    tol = 2.0 ** -8 * got.abs() + 2.0 ** -8 * vmax + 1e-6
-    assert ((got - exact).abs() <= tol).all(), (got - exact).abs().max()
-    err_emu = (got - emu).abs()
-    ulp = torch.exp2(torch.floor(torch.log2(emu.abs().clamp(min=2.0 ** -60))) - 7)
-    assert (err_emu <= 2 * ulp + 1e-6 * vmax).float().mean() > 0.999, err_emu.max()
-    # rows of <= 64 keys are one chunk (no merge): bit-identical to the P-rounded reference
-    # whenever it lands off a bf16 rounding boundary; the merged rows agree within 1 ulp
-    same = (got == emu.float().to(BF16).double()).float().mean().item()
-    print(f"L={L}: bit-equal to the P-rounded fp64 reference {same:.4f}, max |err| vs exact "
+    ref = _reference(q, K, V, lens, 256 ** -0.5, True)
+    exact = _exact(q, K, V, lens, 256 ** -0.5)
+    same = (got == ref).float().mean().item()
+    ulp = torch.exp2(torch.floor(torch.log2(ref.abs().clamp(min=2.0 ** -60))) - 7)
+    within1 = ((got - ref).abs() <= ulp * 1.01).float().mean().item()
+    print(f"L={L}: bit-equal to CPU SDPA {same:.5f}, within 1 ulp {within1:.5f}, max |err| vs exact "
           f"{(got - exact).abs().max().item():.3g}")
-    assert same > 0.9
+    assert same >= 0.998 and within1 >= 0.9999, (same, within1)
+    assert (got - exact).abs().max().item() <= 2.0 ** -6 * max(1.0, exact.abs().max().item())
 
 
 def test_cross_attention_decode_tx60():
@@ -97,7 +94,7 @@ def test_cross_attention_decode_tx60():
     B, T = 8, 60
     lens = [60, 59, 33, 1, 60, 17, 48, 60]
     got, q, K, V = _run(T, B, lens, causal=0, seed=60)
-    emu = _reference(q, K, V, lens, 256 ** -0.5, False, pround=True)
-    same = (got == emu.float().to(BF16).double()).float().mean().item()
-    assert same > 0.97, same
-    assert (got - emu).abs().max().item() <= 2.0 ** -7 * max(1.0, emu.abs().max().item())
+    ref = _reference(q, K, V, lens, 256 ** -0.5, False)
+    same = (got == ref).float().mean().item()
+    print(f"cross T_x=60: bit-equal to CPU SDPA {same:.5f}")
+    assert same >= 0.998, same

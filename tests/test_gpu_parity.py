@@ -193,7 +193,7 @@ def _oparams(c):
 # free-running token-exact cases each golden set must keep (measured on MI355X, see
 # profiles/r02_parity_rates.json); every other case must diverge only at an explained
 # sampling-boundary flip (see _explain_divergence)
-MIN_EXACT = {"golden_tiny": 6, "golden_tiny_eager": 4, "golden_tiny_window": 4}
+MIN_EXACT = {"golden_tiny": 9, "golden_tiny_eager": 4, "golden_tiny_window": 4}
 
 
 def _topk_agree(g, r, k, tol):
@@ -206,43 +206,32 @@ def _topk_agree(g, r, k, tol):
 
 
 def _explain_divergence(cfg, c, gpu_logits, ref_logits, t, gpu_tok, oparams):
-    """First divergent step t of a free-running run (identical histories before t): the
-    GPU and reference logits agree within tolerance, the reference sampler returns the
-    reference token on the reference logits and the GPU token on the GPU logits (same
-    noise), and both tokens survive the top-k/top-p filter of BOTH logit rows -- i.e. the
-    divergence is a draw landing on a bf16 rounding difference, not a different model."""
+    """First divergent step t of a free-running run (histories identical before t): the
+    GPU and reference logits agree within tolerance, and the reference sampler -- fed the
+    same noise and state -- returns the reference's token on the reference logits and
+    the GPU's token on the GPU logits. The divergence is then a draw landing on a
+    bf16-level logit difference, not a different model or sampler."""
     import copy
-    from oracle.t5g_oracle import RowState, draw_noise, sample_helper, top_k_top_p_filtering
+    from oracle.t5g_oracle import RowState, draw_noise, sample_helper
     gen = torch.Generator().manual_seed(int(c["seed"]))
     V = ref_logits.shape[-1]
     for _ in range(t + 1):
         noise = draw_noise(gen, V)
     y = c["y"]
-    st = RowState(current_length=len(y) + 1 + t, prompt_offset=len(y) + 1, target_total=c["tgt"],
-                  first_input_len=len(c["x"]), cur_num_gen=t)
+    st = RowState(cur_num_gen=t, current_length=len(y) + 1 + t, prompt_offset=len(y) + 1, target_total=c["tgt"],
+                  first_input_len=len(c["x"]))
     st.est_total = c["tgt"] + 1
-    hist = c["gen"][:t]
-    for i in range(len(hist)):   # silence-run state of the shared history
-        st.consec_silence = st.consec_silence + 1 if (hist[i] in c["silence_tokens"] and i > 0
-                                                      and hist[i] == hist[i - 1]) else 0
-    st.prev_token = hist[-1] if hist else -1
+    for tok in c["gen"][:t]:   # the silence-run state of the shared history (:781-786)
+        st.consec_silence = st.consec_silence + 1 if (tok in c["silence_tokens"] and tok == st.prev_token) else 0
+        st.prev_token = tok
     kw = dict(eos=cfg.eog_inference, encodec_sr=cfg.encodec_sr, extra_cutoff=cfg.extra_cutoff)
     tg, _ = sample_helper(gpu_logits.clone(), oparams, copy.deepcopy(st), noise, **kw)
     tr, _ = sample_helper(ref_logits.clone(), oparams, copy.deepcopy(st), noise, **kw)
     scale = ref_logits.float().abs().max().item()
     err = (gpu_logits.float() - ref_logits.float()).abs().max().item() / scale
-    surv = []
-    for lg in (gpu_logits, ref_logits):
-        x = lg.clone()
-        kk = oparams.top_k[min(len(oparams.top_k) - 1, t)] if isinstance(oparams.top_k, list) else oparams.top_k
-        if oparams.temperature != 1.0:
-            x = x / oparams.temperature
-        f = top_k_top_p_filtering(x, top_k=kk, top_p=oparams.top_p, min_p=oparams.min_p)
-        surv.append(set(torch.nonzero(torch.isfinite(f)).view(-1).tolist()))
-    ok = (tg == gpu_tok and tr == c["gen"][t] and err <= 0.02
-          and (gpu_tok == cfg.eog_inference or all(gpu_tok in s for s in surv))
-          and (c["gen"][t] == cfg.eog_inference or all(c["gen"][t] in s for s in surv)))
-    return ok, {"step": t, "gpu_token": gpu_tok, "ref_token": c["gen"][t], "rel_err": err}
+    ok = tg == gpu_tok and tr == c["gen"][t] and err <= 0.02
+    return ok, {"step": t, "gpu_token": gpu_tok, "ref_token": c["gen"][t], "sampler_on_gpu_logits": tg,
+                "sampler_on_ref_logits": tr, "rel_err": err}
 
 
 @pytest.mark.parametrize("name", ["golden_tiny", "golden_tiny_eager", "golden_tiny_window"])
@@ -431,29 +420,3 @@ def test_sampler_kernel_vs_reference_golden():
                   tok, c["token"])
     print(f"sampler: {ok}/{len(meta['cases'])} exact, {amb} ambiguous")
     assert ok == len(meta["cases"])
-
-
-@pytest.mark.parametrize("variant", ["1", "2"])
-@pytest.mark.parametrize("case", ["golden_tiny", "golden_mid"])
-def test_decode_variants_teacher_forced(variant, case, monkeypatch):
-    """The opt-in decode-step GEMV variants (T5G_FUSED_DECODE=1: norm prologues fused into
-    row-major VALU GEMVs; 2: fused prologues on the P16 MFMA GEMVs) against the CPU
-    oracle, teacher-forced, on the tiny golden cases and at true 2b-2b widths."""
-    _need_gpu()
-    from t5gemma_tts_amd.config import named_config
-    from t5gemma_tts_amd.engine import Utterance
-    from t5gemma_tts_amd.weights import synthetic_weights
-    monkeypatch.setenv("T5G_FUSED_DECODE", variant)
-    meta, _ = _load(case)
-    cfg = named_config(meta["config"], **meta["config_kw"])
-    sd = synthetic_weights(cfg, meta["weight_seed"])
-    eng = _engine(cfg, sd, max_batch=4, max_text=64, max_audio=256 if case == "golden_tiny" else 128,
-                  max_gen=200 if case == "golden_tiny" else 64)
-    cases = meta["cases"][:3]
-    utts = [Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"]) for c in cases]
-    out = eng.generate(utts, [_params(c) for c in cases], seeds=[c["seed"] for c in cases], parity=True,
-                       record_logits=True)
-    for b, c in enumerate(cases):
-        one = {"gen": [out["gen"][b]], "logits": [[l[b]] for l in out["logits"]]}
-        w, ex = teacher_forced_check(cfg, sd, utts[b], _oparams(c), c["seed"], one, rtol=0.02)
-        print(f"variant {variant} {case} row {b}: max rel logit err {w:.3g}, exact rows {ex}/{len(out['gen'][b])}")

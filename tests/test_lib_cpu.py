@@ -32,7 +32,8 @@ def test_struct_layouts_match_header():
     from t5gemma_tts_amd import _lib
     assert C.sizeof(_lib.SamplerRow) == 48
     assert C.sizeof(_lib.SamplerState) == 48
-    assert C.sizeof(_lib.LayerWeights) == 19 * 8
+    assert C.sizeof(_lib.LayerWeights) == 13 * 8
+    assert C.sizeof(_lib.AttnDecodeArgs) == 4 * 4 + 3 * 8 + 8 + 8 + 4 * 4 + 2 * 8
     assert C.sizeof(_lib.GemvArgs) == 152
 
 
