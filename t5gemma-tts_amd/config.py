@@ -94,6 +94,17 @@ class VoiceConfig:
     add_bos_to_text: int = 0
     use_pm_rope: int = 1
     precision: str = "bfloat16"
+    # carried for the host pipeline / provenance (configuration_t5gemma_voice.py:54-88)
+    n_codebooks: int = 1
+    parallel_pattern: int = 0
+    audio_max_length: float = 40.0
+    prune_text_modules: int = 0
+    audio_mask_token: int = 1024
+    audio_tokenizer: str = "xcodec2"
+    codec_audio_sr: Optional[float] = None
+    xcodec2_model_name: Optional[str] = None
+    text_tokenizer_name: Optional[str] = None
+    t5gemma_model_name: str = "google/t5gemma-2b-2b-ul2"
 
     @property
     def n_audio_tokens(self) -> int:
@@ -117,10 +128,30 @@ class VoiceConfig:
     # ------------------------------------------------------------------
     @staticmethod
     def from_hf_dict(d: Dict[str, Any]) -> "VoiceConfig":
-        """Build from an HF ``config.json`` of the reference export."""
+        """Build from the ``config.json`` of the reference's HF export
+        (``scripts/export_t5gemma_voice_hf.py:117-171``), the way
+        ``T5GemmaVoiceForConditionalGeneration.__init__`` reads it (:343-478):
+
+        * backbone shape from ``t5_config_dict`` (``T5GemmaConfig(**t5_config_dict)``, :361-364);
+        * ``attn_implementation`` from the voice config, default ``"eager"`` (:365-367 and
+          configuration_t5gemma_voice.py:59) -- eager applies the 50.0 logit softcap;
+        * ``n_codebooks != 1`` is reset to 1 (:347-349) and a list ``audio_vocab_size``
+          contributes its first entry (:451-459: only codebook 0 is built);
+        * anything the engine does not implement raises ValueError instead of running a
+          different model (activation other than tanh-GELU, attention bias, no PM-RoPE).
+        """
         t5 = d.get("t5_config_dict") or {}
         enc = t5.get("encoder", t5) if isinstance(t5, dict) else {}
         dec = t5.get("decoder", enc) if isinstance(t5, dict) else {}
+        for side in (enc, dec):
+            act = side.get("hidden_activation", "gelu_pytorch_tanh")
+            if act != "gelu_pytorch_tanh":
+                raise ValueError(f"unsupported backbone activation {act!r} (engine implements gelu_pytorch_tanh)")
+            if side.get("attention_bias", False):
+                raise ValueError("unsupported backbone: attention_bias=True")
+        rope = enc.get("rope_parameters") or {}
+        if rope.get("rope_type", "default") != "default":
+            raise ValueError(f"unsupported rope_type {rope.get('rope_type')!r}")
         bb = BackboneDims(
             hidden_size=enc.get("hidden_size", 2304),
             intermediate_size=enc.get("intermediate_size", 9216),
@@ -131,14 +162,17 @@ class VoiceConfig:
             head_dim=enc.get("head_dim", 256),
             text_vocab_size=enc.get("vocab_size", 256000),
             query_pre_attn_scalar=enc.get("query_pre_attn_scalar", 256),
-            rope_theta=(enc.get("rope_parameters") or {}).get("rope_theta", enc.get("rope_theta", 10000.0)),
+            rope_theta=rope.get("rope_theta", enc.get("rope_theta", 10000.0)),
             rms_norm_eps=enc.get("rms_norm_eps", 1e-6),
             sliding_window=enc.get("sliding_window", 4096) or 1 << 30,
             encoder_layer_types=enc.get("layer_types"),
             decoder_layer_types=dec.get("layer_types"),
             attn_logit_softcapping=enc.get("attn_logit_softcapping", 50.0),
-            attn_implementation=d.get("attn_implementation", "eager"),
+            attn_implementation=d.get("attn_implementation") or "eager",
         )
+        for k in ("hidden_size", "intermediate_size", "num_attention_heads", "num_key_value_heads", "head_dim"):
+            if k in dec and dec[k] != enc.get(k, dec[k]):
+                raise ValueError(f"encoder/decoder {k} differ ({enc.get(k)} vs {dec[k]}): unsupported")
         kw = {}
         for f in dataclasses.fields(VoiceConfig):
             if f.name == "backbone":
@@ -146,12 +180,11 @@ class VoiceConfig:
             if f.name in d and d[f.name] is not None:
                 kw[f.name] = d[f.name]
         avs = kw.get("audio_vocab_size")
-        if isinstance(avs, list):
-            if len(avs) != 1:
-                raise ValueError("XCodec2 inference expects n_codebooks=1.")
+        if isinstance(avs, (list, tuple)):
             kw["audio_vocab_size"] = int(avs[0])
-        if int(d.get("n_codebooks", 1)) != 1:
-            raise ValueError("XCodec2 inference expects n_codebooks=1.")
+        kw["n_codebooks"] = 1
+        if int(kw.get("use_pm_rope", 1)) != 1:
+            raise ValueError("use_pm_rope=0 (plain cross-attention) is not implemented by the engine")
         return VoiceConfig(backbone=bb, **kw)
 
     @staticmethod

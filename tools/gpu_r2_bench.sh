@@ -3,6 +3,7 @@
 source tools/gpu_run.sh
 export TMPDIR=/tmp
 rm -rf gpurun_out/prof
+run t_ckpt 300 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_gpu_checkpoint.py
 run bench 900 python -u bench.py
 run bench_e2e 900 python -u bench.py --e2e --steps 2 --warmup 1
 run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
