@@ -325,6 +325,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     constexpr int KPB = KPW * 4;
     constexpr int NIT = DCH / KPB;
     __shared__ float sm[G][DCH];
+    __shared__ float pl[G][DCH + 16];
     __shared__ float stat_l[G];
     __shared__ f32x4 ored[4][G][LPK][2];
     __shared__ float qs[G][D];
@@ -521,15 +522,18 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         T5G_TS(5);
         return;
     }
-    // single-chunk row: one aten kv block of `span` keys
+    // single-chunk row: one aten kv block of `span` keys; every lane computes its key's p
+    // once (the tail's double exp included), the block sum then only chains adds
     if (wave < G) {
         const int g = wave;
         const float s = lane < n ? sm[g][lane] : -INFINITY;
         const float mx = wave_max(s);
-        auto pf = [&](int pos) -> float { return pos < n ? sdpa_p(__fsub_rn(sm[g][pos], mx), pos, span) : 0.f; };
-        const float l = sdpa_block_sum(span, lane, pf);
-        const float p = pf(lane);
+        const float p = lane < n ? sdpa_p(__fsub_rn(s, mx), lane, span) : 0.f;
+        pl[g][lane] = p;
+        if (lane < 16) pl[g][DCH + lane] = 0.f;
         sm[g][lane] = rbf(p);
+        __builtin_amdgcn_wave_barrier();
+        const float l = sdpa_block_sum_lds<DCH>(pl[g], span, lane);
         if (lane == 0) stat_l[g] = l;
     }
     __syncthreads();
@@ -640,9 +644,12 @@ __global__ __launch_bounds__(256, 2) void attn_pv_kernel(AttnArgs a) {
         const float m = lane < cend ? a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + lane) * G + g] : -INFINITY;
         const float mx = wave_max(m);
         if (lane == 0) mrun[g] = mx;
-        const float s = lane < n ? a.sbuf[((long)qi * a.Hkv * G + kvh * G + g) * a.kv_cap + c0 + lane] : 0.f;
+        float* srow = a.sbuf + ((long)qi * a.Hkv * G + kvh * G + g) * a.kv_cap + c0;
+        const float s = lane < n ? srow[lane] : 0.f;
         const int pos = c0 + lane - r.lo - bi * SDPA_KV_BLOCK;
-        sp_p[g][lane] = lane < n ? rbf(sdpa_p(__fsub_rn(s, mx), pos, blen)) : 0.f;
+        const float p = lane < n ? sdpa_p(__fsub_rn(s, mx), pos, blen) : 0.f;
+        sp_p[g][lane] = rbf(p);
+        if (lane < n) srow[lane] = p;   // the exact p replaces the score: read by the combine
     }
     __syncthreads();
     float o[G][8];
@@ -699,6 +706,7 @@ __global__ __launch_bounds__(64 * G) void attn_combine_kernel(AttnArgs a) {
     constexpr int CPB = SDPA_KV_BLOCK / DCH;
     __shared__ float blk_et[G][SDPA_MAX_BLOCKS];
     __shared__ float stat_l[G];
+    __shared__ float pl[G][SDPA_KV_BLOCK + 16];
     const int qi = blockIdx.x, kvh = blockIdx.y;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     T5G_TS(3);
@@ -706,19 +714,36 @@ __global__ __launch_bounds__(64 * G) void attn_combine_kernel(AttnArgs a) {
     if (r.span <= DCH) return;
     const int nch = (r.span + DCH - 1) / DCH;
     const int nblk = (r.span + SDPA_KV_BLOCK - 1) / SDPA_KV_BLOCK;
-    {   // wave g: l of head g with aten's lane-ordered block sums
+    {   // wave g: l of head g with aten's lane-ordered block sums over the exact p values
+        // attn_pv_kernel left in sbuf, staged block by block in LDS; the serial adds run
+        // out of LDS
         const int g = wave;
         const float* mb = a.mbuf + ((long)qi * a.Hkv + kvh) * a.nsplit * G + g;
-        const float* sb = a.sbuf + ((long)qi * a.Hkv * G + kvh * G + g) * a.kv_cap + r.lo;
+        const float* pb = a.sbuf + ((long)qi * a.Hkv * G + kvh * G + g) * a.kv_cap + r.lo;
+        const float cmax = lane < nch ? mb[lane * G] : -INFINITY;   // chunk `lane`'s max
+        // block b's p in registers (8 per lane, coalesced); the next block's loads are
+        // issued before this block's serial adds
+        float pw[SDPA_KV_BLOCK / 64];
+#pragma unroll
+        for (int k = 0; k < SDPA_KV_BLOCK / 64; ++k) {
+            const int pos = 64 * k + lane;
+            pw[k] = pos < r.span ? pb[pos] : 0.f;
+        }
+        if (lane < 16) pl[g][SDPA_KV_BLOCK + lane] = 0.f;
         float m = -INFINITY, l = 0.f;
         for (int b = 0; b < nblk; ++b) {
-            const int ce = min(nch, (b + 1) * CPB), cs = b * CPB;
-            const float cm = (cs + lane < ce) ? mb[(cs + lane) * G] : -INFINITY;
-            const float mn = fmaxf(m, wave_max(cm));
-            const int bs = b * SDPA_KV_BLOCK;
-            const int blen = min(SDPA_KV_BLOCK, r.span - bs);
-            auto pf = [&](int pos) -> float { return sdpa_p(__fsub_rn(sb[bs + pos], mn), pos, blen); };
-            const float ts = sdpa_block_sum(blen, lane, pf);
+            __builtin_amdgcn_wave_barrier();   // the previous block's LDS reads are done
+#pragma unroll
+            for (int k = 0; k < SDPA_KV_BLOCK / 64; ++k) pl[g][64 * k + lane] = pw[k];
+#pragma unroll
+            for (int k = 0; k < SDPA_KV_BLOCK / 64; ++k) {
+                const int pos = (b + 1) * SDPA_KV_BLOCK + 64 * k + lane;
+                pw[k] = pos < r.span ? pb[pos] : 0.f;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const float mn = fmaxf(m, wave_max(lane / CPB == b ? cmax : -INFINITY));
+            const int blen = min(SDPA_KV_BLOCK, r.span - b * SDPA_KV_BLOCK);
+            const float ts = sdpa_block_sum_lds<SDPA_KV_BLOCK>(pl[g], blen, lane);
             const float et = sdpa_block_rescale(m, mn);
             l = fmaf(et, l, ts);
             if (lane == 0) blk_et[g][b] = et;
@@ -736,7 +761,11 @@ __global__ __launch_bounds__(64 * G) void attn_combine_kernel(AttnArgs a) {
     for (int b = 0; b < nblk; ++b) {
         f32x4 blk = {0.f, 0.f, 0.f, 0.f};
         const int ce = min(nch, (b + 1) * CPB);
-        for (int c = b * CPB; c < ce; ++c) blk += *(const f32x4*)(base + (long)c * G * (D + 2));
+#pragma unroll
+        for (int k = 0; k < CPB; ++k) {   // predicated, not a loop-carried wait per chunk
+            const int c = b * CPB + k;
+            if (c < ce) blk += *(const f32x4*)(base + (long)c * G * (D + 2));
+        }
         dst = dst * blk_et[g][b] + blk;
     }
     const float inv = __fdiv_rn(1.0f, stat_l[g]);

@@ -141,6 +141,33 @@ __device__ __forceinline__ float sdpa_block_sum(int blen, int lane, P p) {
     for (int i = n16; i < blen; ++i) s = __fadd_rn(s, p(i));
     return s;
 }
+// The same tmp_sum from the block's p values already staged in LDS (pl[0, blen); pl must
+// hold MAXB + 16 readable floats): every p is computed once, in parallel, by its own
+// lane, and only the fixed-order adds are serial. Positions past the block add +0.0f,
+// which leaves a sum of non-negative terms bit-unchanged, so the chains are unrolled
+// to MAXB without branches. One wave; every lane returns the sum.
+template <int MAXB>
+__device__ __forceinline__ float sdpa_block_sum_lds(const float* pl, int blen, int lane) {
+    const int n16 = blen & ~15;
+    const int l16 = lane & 15;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXB / 16; ++k) {
+        const int i = l16 + 16 * k;
+        acc = __fadd_rn(acc, i < n16 ? pl[i] : 0.f);
+    }
+    acc = __fadd_rn(acc, __shfl_xor(acc, 8, 64));
+    acc = __fadd_rn(acc, __shfl_xor(acc, 4, 64));
+    acc = __fadd_rn(acc, __shfl_xor(acc, 2, 64));
+    acc = __fadd_rn(acc, __shfl_xor(acc, 1, 64));
+    float s = __shfl(acc, 0, 64);
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+        const int i = n16 + k;
+        s = __fadd_rn(s, i < blen ? pl[i] : 0.f);
+    }
+    return s;
+}
 // rescale of the previous blocks' sums when the running max grows (std::expf in aten)
 __device__ __forceinline__ float sdpa_block_rescale(float m_old, float m_new) {
     return m_old == -INFINITY ? 0.f : (float)exp((double)__fsub_rn(m_old, m_new));
