@@ -16,8 +16,8 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "lib", "libt5gtts.so")
-SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "xc2.hip", "host_sampler.cpp"]
-HEADERS = ["common.h", "t5g_kernels.h"]
+SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "xc2.hip", "xc2enc.hip", "host_sampler.cpp"]
+HEADERS = ["common.h", "t5g_kernels.h", "xc2_common.h"]
 ARCH = os.environ.get("T5G_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
          "-I", os.path.join(REPO, "include")]

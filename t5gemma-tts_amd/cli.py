@@ -56,17 +56,24 @@ def load_codec(codec_dir: Optional[str] = None, codec: str = "44k", device="cuda
     """XCodec2 decoder: from a local transformers ``Xcodec2Model`` directory, or seeded
     synthetic weights of the named size."""
     from .codec import AudioTokenizer, CodecConfig, codec_16k, codec_44k, codec_tiny, synthetic_codec_weights
+    from .codec_enc import EncoderConfig, encoder_16k, encoder_tiny, synthetic_encoder_weights
     if codec_dir:
         import json
 
         from .weights import load_hf_checkpoint
         with open(os.path.join(codec_dir, "config.json")) as f:
-            cfg = CodecConfig.from_hf_dict(json.load(f))
+            d = json.load(f)
+        cfg = CodecConfig.from_hf_dict(d)
         sd = {k: v.float() for k, v in load_hf_checkpoint(codec_dir).items()}
+        ecfg = EncoderConfig.from_hf_dict(d)
+        esd = sd if "fc_encoder.weight" in sd else None     # a decoder-only export has no encoder
     else:
         cfg = {"44k": codec_44k, "16k": codec_16k, "tiny": codec_tiny}[codec]()
         sd = synthetic_codec_weights(cfg, seed)
-    return AudioTokenizer(device=device, cfg=cfg, state_dict=sd, max_batch=max_batch, max_frames=max_frames)
+        ecfg = encoder_tiny() if codec == "tiny" else encoder_16k()
+        esd = synthetic_encoder_weights(ecfg, seed + 1)
+    return AudioTokenizer(device=device, cfg=cfg, state_dict=sd, encoder_cfg=ecfg, encoder_state_dict=esd,
+                          max_batch=max_batch, max_frames=max_frames)
 
 
 def load_model(model_dir: Optional[str] = None, synthetic: Optional[str] = None, device="cuda:0",

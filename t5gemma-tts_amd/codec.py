@@ -334,14 +334,18 @@ class XCodec2Decoder:
 
 
 class AudioTokenizer:
-    """Mirror of the reference's ``AudioTokenizer`` (data/tokenizer.py:53-123) for the
-    decode direction. ``decode(frames)`` accepts [B, T] or [B, 1, T] codes and returns the
-    waveform [B, 1, T * hop] (fp32, on the codec's device), as ``decode_code`` does.
-    ``encode`` (w2v-BERT + acoustic encoder) is out of this build's scope (SURVEY 8(f)#1)."""
+    """Mirror of the reference's ``AudioTokenizer`` (data/tokenizer.py:53-123).
+    ``decode(frames)`` accepts [B, T] or [B, 1, T] codes and returns the waveform
+    [B, 1, T * hop] (fp32, on the codec's device), as ``decode_code`` does.
+    ``encode(wav)`` (16 kHz, [B, 1, N] / [1, N] / [N]) returns codes [B, 1, N // 320 + 1]
+    (int64, on the device) through the XCodec2 encoder (codec_enc.py) when encoder weights
+    are given (``encoder_state_dict``, transformers ``Xcodec2Model`` names)."""
 
     def __init__(self, backend: str = "xcodec2", device=None, signature=None, model_name=None,
                  sample_rate: Optional[int] = None, cfg: Optional[CodecConfig] = None,
-                 state_dict: Optional[Dict[str, torch.Tensor]] = None, **kw):
+                 state_dict: Optional[Dict[str, torch.Tensor]] = None, encoder_cfg=None,
+                 encoder_state_dict: Optional[Dict[str, torch.Tensor]] = None, max_encode_seconds: float = 30.0,
+                 **kw):
         if backend != "xcodec2":
             raise ValueError(f"Only xcodec2 backend is supported now (got {backend}).")
         if device is None:
@@ -355,13 +359,26 @@ class AudioTokenizer:
         self.sample_rate = int(sample_rate or cfg.sampling_rate)
         self.encode_sample_rate = 16000
         self.channels = 1
+        self.encoder = None
+        if encoder_state_dict is not None:
+            from .codec_enc import XCodec2Encoder, encoder_16k
+            self.encoder = XCodec2Encoder(encoder_cfg or encoder_16k(), encoder_state_dict, device=device,
+                                          max_seconds=max_encode_seconds)
 
     @property
     def device(self):
         return self._device
 
-    def encode(self, wav):
-        raise NotImplementedError("XCodec2 encoder is not part of this build (SURVEY 8(f) rank 1)")
+    def encode(self, wav: torch.Tensor) -> torch.Tensor:
+        """data/tokenizer.py:105-115: 16 kHz waveform -> codes [B, 1, T] (one utterance per
+        encoder call, as the pip encode_code's semantic features are of row 0 only)."""
+        if self.encoder is None:
+            raise ValueError("AudioTokenizer has no encoder weights (pass encoder_state_dict)")
+        if wav.ndim == 3:
+            wav = wav.squeeze(1)
+        if wav.ndim == 1:
+            wav = wav.unsqueeze(0)
+        return torch.cat([self.encoder.encode(wav[b]) for b in range(wav.shape[0])], dim=0)
 
     def decode(self, frames: torch.Tensor) -> torch.Tensor:
         codes = frames

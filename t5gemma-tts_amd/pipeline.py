@@ -8,9 +8,9 @@ SURVEY 8(a) rows covered here:
   a15  output assembly ``_strip_sep_and_eos`` (:323-357);
   and the codec call on the concatenated / generated frames (:359-366).
 
-Out of scope: text normalisation + SentencePiece (callers pass token ids
-or any tokenizer object with ``encode(text, add_special_tokens=False)``), the XCodec2
-*encoder* (callers pass prompt codes instead of an audio path), Whisper.
+Text normalisation and duration estimation are text.py; the prompt audio is encoded by
+the codec's XCodec2 encoder (codec_enc.py) when ``audio_fn`` is a path. Whisper
+transcription is not part of this build (callers pass the reference transcript).
 
 ``inference_batch`` is the batched form the reference lacks (its batch is asserted to
 1, :288): many utterances through one engine call and one batched codec decode.
@@ -58,7 +58,8 @@ def build_prompt(prompt_codes: Optional[IntList], y_sep_token: Optional[int], co
     if prompt_codes is None:
         frames = torch.empty(1, 1, 0, dtype=torch.long)
     else:
-        frames = torch.as_tensor(prompt_codes, dtype=torch.long)
+        frames = (prompt_codes.detach().cpu() if isinstance(prompt_codes, torch.Tensor)
+                  else torch.as_tensor(prompt_codes)).long()
         if frames.ndim == 1:
             frames = frames.view(1, 1, -1)
         elif frames.ndim == 2:
