@@ -209,9 +209,9 @@ def main():
         alg_bytes = 2 * f * d * 2 + B * d * 2 + B * f * 2
         achieved = alg_bytes / (us_gu * 1e-6) / 1e9
         traffic = None
-        pmc = os.path.join(REPO, "profiles", "pmc_gate_up.json")
+        pmc = os.path.join(REPO, "profiles", "r02_pmc_gate_up.json")
         if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_call")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(achieved / 8000.0, 4), "traffic": traffic,
                 "kernel": _lib.GATE_UP_KERNEL,

@@ -142,7 +142,7 @@ def lib():
 
 # The decode gate/up launch as engine.hip's decoder_pass issues it (gemv_dec, PRO_LOAD,
 # EPI_GEGLU, 8 waves, 8 fragments in flight, one block per CU).
-GATE_UP_KERNEL = "gemv_dec_kernel<8, 1, 3 (GEGLU), 0 (LOAD), 1, 1, 8> (decode gate/up, M=8, 84.9 MB weights)"
+GATE_UP_KERNEL = "gemv_dec_kernel<8, 1, 3 (GEGLU), 8> (decode gate/up, M=8, 84.9 MB weights)"
 
 
 def time_gate_up(X_ptr: int, ldx: int, M: int, W_ptrs, N: int, K: int, Y_ptr: int, iters: int, stream) -> float:

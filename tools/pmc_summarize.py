@@ -1,32 +1,54 @@
-"""Reduce the two rocprofv3 --pmc passes of tools/pmc_gateup.py to
-profiles/pmc_gate_up.json: HBM bytes per gate/up launch with the gfx950 corrections
-of MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of 16 B/lane streaming reads:
-x2; WRITE_SIZE exact; both in KiB)."""
+"""Reduce the two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of a driver script to a
+profiles/*.json: HBM bytes per launch (or per call of a multi-kernel op) with the gfx950
+corrections of MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of 16 B/lane
+streaming reads: x2; WRITE_SIZE exact; both in KiB).
+
+  python tools/pmc_summarize.py gate_up   gpurun_out/pmc_gu   profiles/r02_pmc_gate_up.json
+  python tools/pmc_summarize.py attention gpurun_out/pmc_attn profiles/r02_pmc_attention.json
+"""
 import csv
 import json
 import os
 import sys
 
-KERNEL = "gemv_dec_kernel<8, 1, 3, 0, 1, 1, 8>"
+OPS = {
+    "gate_up": {"kernels": ["gemv_dec_kernel<8, 1, 3, 8>"],
+                "algorithmic": 2 * 9216 * 2304 * 2 + 8 * 2304 * 2 + 8 * 9216 * 2,
+                "what": "decode gate/up GEGLU GEMV, M=8, N=18432, K=2304 (tools/pmc_gateup.py: 26 weight sets "
+                        "rotated, 2.2 GB > 256 MiB Infinity Cache)"},
+    "attention": {"kernels": ["attn_decode_kernel<256, 2>", "attn_pv_kernel<256, 2>", "attn_combine_kernel<256, 2>"],
+                  "algorithmic": None,
+                  "what": "decode self attention (scores + P.V + combine), 8 rows x 8/4 heads x 256, L ~ 527 "
+                          "(tools/pmc_attention.py: 26 KV caches, 436 MB > 256 MiB Infinity Cache)"},
+}
 
 
-def mean_counter(path):
-    rows = [r for r in csv.DictReader(open(path)) if KERNEL in r["Kernel_Name"]]
-    vals = [float(r["Counter_Value"]) for r in rows]
-    return sum(vals) / len(vals), len(vals), rows[0]["Counter_Name"]
+def per_call(path, kernels):
+    tot = {}
+    for r in csv.DictReader(open(path)):
+        for k in kernels:
+            if k in r["Kernel_Name"]:
+                tot.setdefault(k, []).append(float(r["Counter_Value"]))
+    n = min(len(v) for v in tot.values())
+    return sum(sum(v) / len(v) for v in tot.values()), n, {k: sum(v) / len(v) for k, v in tot.items()}
 
 
-def main(out_dir="gpurun_out", dst="profiles/pmc_gate_up.json"):
-    f, nf, cf = mean_counter(os.path.join(out_dir, "pmc_fetch", "pmc_counter_collection.csv"))
-    w, nw, cw = mean_counter(os.path.join(out_dir, "pmc_write", "pmc_counter_collection.csv"))
+def main(op, out_dir, dst):
+    spec = OPS[op]
+    alg = spec["algorithmic"]
+    if alg is None:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from pmc_attention import algorithmic_bytes
+        alg = algorithmic_bytes()
+    f, nf, fk = per_call(os.path.join(out_dir, "fetch", "pmc_counter_collection.csv"), spec["kernels"])
+    w, nw, wk = per_call(os.path.join(out_dir, "write", "pmc_counter_collection.csv"), spec["kernels"])
     hbm = f * 1024 * 2 + w * 1024
-    alg = 2 * 9216 * 2304 * 2 + 8 * 2304 * 2 + 8 * 9216 * 2
-    res = {"kernel": KERNEL + " (decode gate/up GEGLU, M=8, N=18432, K=2304)",
-           "launches": nf, "FETCH_SIZE_KiB_mean": f, "WRITE_SIZE_KiB_mean": w,
+    res = {"op": op, "kernels": spec["kernels"], "what": spec["what"], "launches_per_kernel": nf,
+           "FETCH_SIZE_KiB_per_call": f, "WRITE_SIZE_KiB_per_call": w,
+           "FETCH_SIZE_KiB_by_kernel": fk, "WRITE_SIZE_KiB_by_kernel": wk,
            "correction": "bytes = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (gfx950: FETCH_SIZE is half of 16B/lane reads)",
-           "hbm_bytes_per_launch": int(hbm), "algorithmic_bytes_per_launch": alg,
-           "traffic_over_algorithmic": round(hbm / alg, 4),
-           "workload": "26 distinct weight sets rotated (2.2 GB > 256 MiB Infinity Cache), tools/pmc_gateup.py"}
+           "hbm_bytes_per_call": int(hbm), "algorithmic_bytes_per_call": int(alg),
+           "traffic_over_algorithmic": round(hbm / alg, 4)}
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
