@@ -714,6 +714,26 @@ __global__ __launch_bounds__(64 * G) void attn_combine_kernel(AttnArgs a) {
     if (r.span <= DCH) return;
     const int nch = (r.span + DCH - 1) / DCH;
     const int nblk = (r.span + SDPA_KV_BLOCK - 1) / SDPA_KV_BLOCK;
+    // this thread's output quad, and the partial P.V sums of the first two kv blocks
+    // requested now (unconditional clamped loads), so they land while l is computed
+    constexpr int QPB = (G * D / 4 + combine_cz<D, G>() - 1) / combine_cz<D, G>();
+    const int quad = (int)blockIdx.z * QPB + (int)threadIdx.x;
+    const bool mq = (int)threadIdx.x < QPB && quad < G * D / 4;
+    const int gq = mq ? quad / (D / 4) : 0, d4 = mq ? quad % (D / 4) : 0;
+    const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2)) + gq * (D + 2) + 2 + 4 * d4;
+    constexpr int NPRE = 2;
+    f32x4 pre[NPRE];
+#pragma unroll
+    for (int b = 0; b < NPRE; ++b) {
+        pre[b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int ce = min(nch, (b + 1) * CPB);
+#pragma unroll
+        for (int k = 0; k < CPB; ++k) {
+            const int c = b * CPB + k;
+            const f32x4 v = *(const f32x4*)(base + (long)(c < ce ? c : 0) * G * (D + 2));
+            pre[b] += (c < ce) ? v : (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+    }
     {   // wave g: l of head g with aten's lane-ordered block sums over the exact p values
         // attn_pv_kernel left in sbuf, staged block by block in LDS; the serial adds run
         // out of LDS
@@ -752,19 +772,20 @@ __global__ __launch_bounds__(64 * G) void attn_combine_kernel(AttnArgs a) {
         if (lane == 0) stat_l[g] = l;
     }
     __syncthreads();
-    constexpr int QPB = (G * D / 4 + combine_cz<D, G>() - 1) / combine_cz<D, G>();
-    const int quad = (int)blockIdx.z * QPB + (int)threadIdx.x;
-    if ((int)threadIdx.x >= QPB || quad >= G * D / 4) return;
-    const int g = quad / (D / 4), d4 = quad % (D / 4);
-    const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2)) + g * (D + 2) + 2 + 4 * d4;
+    if (!mq) return;
+    const int g = gq;
     f32x4 dst = {0.f, 0.f, 0.f, 0.f};
     for (int b = 0; b < nblk; ++b) {
         f32x4 blk = {0.f, 0.f, 0.f, 0.f};
-        const int ce = min(nch, (b + 1) * CPB);
+        if (b < NPRE) {
+            blk = b == 0 ? pre[0] : pre[1];
+        } else {
+            const int ce = min(nch, (b + 1) * CPB);
 #pragma unroll
-        for (int k = 0; k < CPB; ++k) {   // predicated, not a loop-carried wait per chunk
-            const int c = b * CPB + k;
-            if (c < ce) blk += *(const f32x4*)(base + (long)c * G * (D + 2));
+            for (int k = 0; k < CPB; ++k) {   // predicated, not a loop-carried wait per chunk
+                const int c = b * CPB + k;
+                if (c < ce) blk += *(const f32x4*)(base + (long)c * G * (D + 2));
+            }
         }
         dst = dst * blk_et[g][b] + blk;
     }

@@ -420,3 +420,25 @@ def test_sampler_kernel_vs_reference_golden():
                   tok, c["token"])
     print(f"sampler: {ok}/{len(meta['cases'])} exact, {amb} ambiguous")
     assert ok == len(meta["cases"])
+
+
+def test_generate_without_target_length():
+    """tgt_y_lens=None (the reference accepts it, modeling_t5gemma_voice.py:624-660: no time
+    budget, decoder progress over a 2 s lookahead) on a default-sized engine: generation
+    stops at EOS or at the engine's capacity, and every step the reference sampler would
+    also have taken is teacher-forced exact (this path used to raise)."""
+    _need_gpu()
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import Utterance
+    from t5gemma_tts_amd.weights import synthetic_weights
+    cfg = named_config("tiny")
+    sd = synthetic_weights(cfg, 7)
+    eng = _engine(cfg, sd, max_batch=2, max_text=32, max_audio=96, max_gen=40)
+    c = {"top_k": 30, "top_p": 0.9, "min_p": 0.0, "temperature": 0.8, "stop_repetition": 3, "silence_tokens": []}
+    u = Utterance(x=[5, 17, 301, 44, 9], y=[3, 60, cfg.y_sep_token], tgt_y_len=None)
+    out = eng.generate([u], _params(c), seeds=[11], parity=True, record_logits=True)
+    g = out["gen"][0].tolist()
+    assert 1 <= len(g) <= 40
+    if g[-1] == cfg.eog_inference and len(g) == 40:   # capacity stop: the last EOS is the engine's
+        out = {"gen": [out["gen"][0][:-1]], "logits": out["logits"][:-1]}
+    teacher_forced_check(cfg, sd, u, _oparams(c), 11, out, rtol=0.02)
