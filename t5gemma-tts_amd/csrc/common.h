@@ -47,6 +47,16 @@ __device__ __forceinline__ f32x2 rbf2(f32x2 x) {
     return (f32x2){__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
 }
 
+// sc1 (write-through store / L1-bypassing load) accessors for in-launch cross-workgroup
+// hand-offs (relaxed agent-scope atomics lower to global_store / global_load ... sc1; the
+// gfx950 form the file header describes)
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -567,14 +567,7 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
 // Rows the fast path cannot take (min_p, top-k off or > FS_KMAX, a slice with more
 // than FS_CAP candidates, more than FS_SMAX survivors) are flagged in fs_slow and
 // finished by the single-block kernel launched right after.
-// sc1 (write-through store / L1-bypassing load) accessors for the fast path's cross-block
-// candidate hand-off (relaxed agent-scope atomics lower to global_store/load ... sc1)
-template <typename T>
-__device__ __forceinline__ void st_sc1(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-template <typename T>
-__device__ __forceinline__ T ld_sc1(const T* p) {
-    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// st_sc1 / ld_sc1 (common.h): the fast path's cross-block candidate hand-off
 
 constexpr int FT = 256;
 __device__ __forceinline__ bool lane_ok(int t) { return t < FS_NB; }

@@ -140,6 +140,73 @@ __global__ void aa_snake_kernel(const float* X, float* Y, int T, int C, const fl
     Y[idx] = y;
 }
 
+// Same activation, 4 consecutive outputs of one channel per thread: their 18 up-sampled
+// values come from 14 input rows held in registers (the per-output form rebuilds 48 up
+// values from 288 loads). Same operations in the same order, so bit-identical to
+// aa_snake_kernel. Groups whose up-sample window reaches the replicate-padded edges
+// (t0 < 3 or t0 > T - 7) take the per-output form. Needs T % 4 == 0.
+__global__ void aa_snake4_kernel(const float* X, float* Y, int T, int C, const float* alpha_log,
+                                 const float* beta_log, const float* fu, const float* fd) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)(T / 4) * C) return;
+    const int tg = (int)(idx / C), c = (int)(idx - (long)tg * C);
+    const int t0 = 4 * tg;
+    const float a = expf(alpha_log[c]);
+    const float ib = 1.0f / (expf(beta_log[c]) + 1e-9f);
+    float fuv[12], fdv[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        fuv[k] = fu[k];
+        fdv[k] = fd[k];
+    }
+    if (t0 >= 3 && t0 <= T - 7) {
+        float x[14];
+#pragma unroll
+        for (int r = 0; r < 14; ++r) x[r] = X[(long)min(max(t0 + r - 5, 0), T - 1) * C + c];
+        float z[18];
+#pragma unroll
+        for (int j = 0; j < 18; ++j) {
+            // u = 2 t0 - 5 + j, o = u + 15: i = (o >> 1) - jj = t0 + 5 + (j >> 1) - jj,
+            // tap kk = o - 2 i = (j & 1) + 2 jj, input row i - 5 -> x[(i - t0)]
+            float up = 0.f;
+#pragma unroll
+            for (int jj = 0; jj < 6; ++jj) up += x[5 + (j >> 1) - jj] * fuv[(j & 1) + 2 * jj];
+            up *= 2.0f;
+            const float sn = sinf(up * a);
+            z[j] = up + ib * (sn * sn);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float y = 0.f;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) y += fdv[k] * z[2 * q + k];
+            Y[(long)(t0 + q) * C + c] = y;
+        }
+        return;
+    }
+    const int T2 = 2 * T;
+    for (int q = 0; q < 4; ++q) {
+        const int t = t0 + q;
+        float y = 0.f;
+        for (int k = 0; k < 12; ++k) {
+            const int u = min(max(2 * t + k - 5, 0), T2 - 1);
+            const int o = u + 15;
+            const int i_hi = o >> 1;
+            float up = 0.f;
+            for (int j = 0; j < 6; ++j) {
+                const int i = i_hi - j;
+                const int ts = min(max(i - 5, 0), T - 1);
+                up += X[(long)ts * C + c] * fuv[o - 2 * i];
+            }
+            up *= 2.0f;
+            const float sn = sinf(up * a);
+            const float z = up + ib * (sn * sn);
+            y += fdv[k] * z;
+        }
+        Y[(long)t * C + c] = y;
+    }
+}
+
 // ------------------------------------------------- conformer convolution module middle
 // [tf] Wav2Vec2BertConvolutionModule :196-227 between the two pointwise convs:
 // GLU over the pointwise_conv1 output (a * sigmoid(b), a = first H channels), causal
@@ -388,6 +455,13 @@ static int conv(xc2_encoder* e, const xc2e_conv& c, const float* X, int T_in, fl
 }
 
 static int snake(const float* X, float* Y, int T, int C, const xc2e_snake& s, const xc2e_weights& w, hipStream_t st) {
+    if (T % 4 == 0 && T >= 8) {
+        const long n = (long)(T / 4) * C;
+        hipLaunchKernelGGL(aa_snake4_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, X, Y, T, C,
+                           s.alpha, s.beta, w.aa_up, w.aa_down);
+        XE_LAUNCHED();
+        return 0;
+    }
     const long n = (long)T * C;
     hipLaunchKernelGGL(aa_snake_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, X, Y, T, C, s.alpha,
                        s.beta, w.aa_up, w.aa_down);
