@@ -16,7 +16,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "lib", "libt5gtts.so")
-SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "xc2.hip", "xc2enc.hip", "host_sampler.cpp"]
+SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "xc2.hip", "xc2enc.hip", "whisper.hip", "host_sampler.cpp"]
 HEADERS = ["common.h", "t5g_kernels.h", "xc2_common.h"]
 ARCH = os.environ.get("T5G_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
@@ -31,7 +31,7 @@ def _hipcc() -> str:
 
 
 def _newest_dep() -> float:
-    deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", h) for h in ("t5gtts.h", "xc2.h")]
+    deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", h) for h in ("t5gtts.h", "xc2.h", "whisper.h")]
     return max(os.path.getmtime(p) for p in deps if os.path.exists(p))
 
 

@@ -14,8 +14,11 @@ Differences, all explicit:
 * ``synthetic="2b2b" | "tiny"`` runs seeded random weights of that architecture (and of the
   codec, ``codec`` "44k" | "16k" | "tiny") with a byte-level stand-in tokenizer -- for
   smoke runs and benchmarks only, the output is not speech;
-* Whisper auto-transcription of ``reference_speech`` (:144-150) is not part of this build:
-  pass ``reference_text`` with ``reference_speech``;
+* Whisper auto-transcription of ``reference_speech`` without ``reference_text``
+  (:144-150) runs ``whisper_asr.load_model(whisper_model).transcribe(...)`` on the GPU;
+  ``whisper_model`` names a local openai checkpoint (``~/.cache/whisper/<name>.pt``, the
+  path whisper.load_model reads) or a transformers Whisper directory -- nothing is
+  downloaded; ``asr_model`` may pass a loaded recognizer;
 * ``fire`` is not installed: ``main`` parses the same flag names with argparse.
 """
 from __future__ import annotations
@@ -95,10 +98,11 @@ def run_inference(reference_speech=None, target_text="こんにちは、私はAI
                   codec_sr=50, top_k=30, top_p=0.9, min_p=0, temperature=0.8, silence_tokens=None, multi_trial=None,
                   repeat_prompt=0, stop_repetition=3, sample_batch_size=1, seed=1, output_dir="./generated_tts",
                   cut_off_sec=100, dump_tokens=False, lang=None, codec_dir=None, tokenizer_dir=None, synthetic=None,
-                  codec="44k", device="cuda:0", model=None, audio_tokenizer=None, text_tokenizer=None):
+                  codec="44k", device="cuda:0", whisper_model="large-v3-turbo", model=None, audio_tokenizer=None,
+                  text_tokenizer=None, asr_model=None):
     """inference_commandline_hf.py:72-242. ``model`` / ``audio_tokenizer`` /
-    ``text_tokenizer`` may be passed pre-built (then nothing is loaded). Returns the path
-    of the written wav."""
+    ``text_tokenizer`` / ``asr_model`` may be passed pre-built (then nothing is loaded).
+    Returns the path of the written wav."""
     from .audio import audio_info, write_wav
     from .pipeline import inference_one_sample, parse_silence_tokens
     from .text import estimate_duration, load_text_tokenizer, normalize_text_with_lang
@@ -127,9 +131,13 @@ def run_inference(reference_speech=None, target_text="こんにちは、私はAI
                          "Please supply a reference_speech or omit reference_text.")
     if no_reference_audio:
         prefix_transcript = ""
-    elif not has_reference_text:
-        raise NotImplementedError("Whisper auto-transcription of reference_speech is not part of this build; "
-                                  "pass reference_text")
+    elif not has_reference_text:                               # :144-150
+        if asr_model is None:
+            from .whisper_asr import load_model as load_whisper
+            asr_model = load_whisper(whisper_model, device=device)
+        result = asr_model.transcribe(reference_speech)
+        prefix_transcript = result["text"]
+        print(f"[Info] Whisper transcribed text: {prefix_transcript}")
     else:
         prefix_transcript = reference_text
 
@@ -193,7 +201,7 @@ def _arg(v: str):
 
 _SIGNATURE_OF = run_inference   # the flags (main() calls whatever run_inference is bound to)
 _STR_ARGS = {"reference_speech", "target_text", "model_dir", "reference_text", "output_dir", "lang", "codec_dir",
-             "tokenizer_dir", "synthetic", "codec", "device"}
+             "tokenizer_dir", "synthetic", "codec", "device", "whisper_model"}
 
 
 def main(argv=None) -> None:
@@ -201,7 +209,7 @@ def main(argv=None) -> None:
     sig = inspect.signature(_SIGNATURE_OF)
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     for name, p in sig.parameters.items():
-        if name in ("model", "audio_tokenizer", "text_tokenizer"):
+        if name in ("model", "audio_tokenizer", "text_tokenizer", "asr_model"):
             continue
         ap.add_argument(f"--{name}", type=str if name in _STR_ARGS else _arg, default=p.default)
     args = ap.parse_args(argv)

@@ -40,7 +40,8 @@ __device__ __forceinline__ float bsum(float v, float* red) {
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 
 // --------------------------------------------------------------------------- GEMM
-enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RELU = 2, EPI_LOG = 3 };   // EPI_LOG: log(max(v, 1.1920929e-7))
+// EPI_LOG: log(max(v, 1.1920929e-7)); EPI_GELU: exact (erf) GELU; EPI_LOG10: log10(max(v, 1e-10))
+enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RELU = 2, EPI_LOG = 3, EPI_GELU = 4, EPI_LOG10 = 5 };
 
 struct GemmArgs {
     const float* A;
@@ -155,6 +156,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
                 if (a.epi == EPI_SILU) v = silu(v);
                 else if (a.epi == EPI_RELU) v = fmaxf(v, 0.f);
                 else if (a.epi == EPI_LOG) v = logf(fmaxf(v, 1.1920929e-7f));
+                else if (a.epi == EPI_GELU) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+                else if (a.epi == EPI_LOG10) v = log10f(fmaxf(v, 1e-10f));
                 if (a.alpha != 0.f) v = a.alpha * v;
                 const long row = rowaddr(a.cm, m);
                 if (a.resid) v = a.resid[row * a.ldc + n] + v;

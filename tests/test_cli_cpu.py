@@ -68,10 +68,37 @@ def test_reference_text_without_speech_is_an_error():
             _run(td, target_text="hi", reference_text="ref", target_duration=1.0)
 
 
-def test_speech_without_transcript_needs_whisper():
+class FakeASR:
+    def __init__(self):
+        self.calls = []
+
+    def transcribe(self, audio):
+        self.calls.append(audio)
+        return {"text": " whisper said this", "segments": [], "language": "en"}
+
+
+def test_speech_without_transcript_is_transcribed_by_whisper(capsys):
+    """:144-150: reference audio without reference_text -> Whisper's transcript becomes the
+    prompt text (normalised like a given reference_text)."""
+    from t5gemma_tts_amd.audio import write_wav
     with tempfile.TemporaryDirectory() as td:
-        with pytest.raises(NotImplementedError):
-            _run(td, target_text="hi", reference_speech="a.wav", target_duration=1.0)
+        ref = os.path.join(td, "ref.wav")
+        write_wav(ref, np.zeros(16000), 16000)
+        asr = FakeASR()
+        _, model, _ = _run(td, target_text="hi", reference_speech=ref, target_duration=1.0, asr_model=asr)
+        assert asr.calls == [ref]
+        assert "[Info] Whisper transcribed text:  whisper said this" in capsys.readouterr().out
+        x = model.calls[0]["x"][0]
+        with_text = _run(td, target_text="hi", reference_speech=ref, target_duration=1.0,
+                         reference_text=" whisper said this")[1].calls[0]["x"][0]
+        assert x == with_text
+
+
+def test_whisper_checkpoint_is_never_downloaded(monkeypatch):
+    with tempfile.TemporaryDirectory() as td:
+        monkeypatch.setenv("XDG_CACHE_HOME", td)
+        with pytest.raises(FileNotFoundError):
+            _run(td, target_text="hi", reference_speech="a.wav", target_duration=1.0, whisper_model="large-v3-turbo")
 
 
 def test_estimated_duration_and_sample_cut_of_reference_audio():
