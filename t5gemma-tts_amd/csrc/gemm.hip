@@ -282,15 +282,9 @@ int pack_p16(const bf16_t* src, int N, int K, long ld, bf16_t* dst, int NGpad, h
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// shortest per-wave k-stream that stages X in LDS (T5G_XLDS_MIN, default 16). Read once.
-static int xlds_min() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("T5G_XLDS_MIN");
-        v = e ? atoi(e) : 16;
-    }
-    return v;
-}
+// shortest per-wave k-stream that stages X in LDS (r01 probe: the staging barrier costs
+// ~1 us, repaid from 16 fragments per wave)
+constexpr int XLDS_MIN = 16;
 
 template <int MT, int WPG, int KS, int EPI>
 static void launch_t(const GemmArgs& a, int mblocks, hipStream_t st) {
@@ -299,7 +293,7 @@ static void launch_t(const GemmArgs& a, int mblocks, hipStream_t st) {
     const int per = (a.KB + a.splits - 1) / a.splits;
     // decode with a long K stream per wave: stage the X rows in LDS once per block (the
     // staging barrier costs ~1 us, repaid only when each wave streams >= 16 fragments)
-    if (WPG == KS && MT == 1 && per / KS >= xlds_min() && min(16, a.M) * per * 4 <= 256 * 18) {
+    if (WPG == KS && MT == 1 && per / KS >= XLDS_MIN && min(16, a.M) * per * 4 <= 256 * 18) {
         const size_t shm = (size_t)min(16, a.M) * (per * 32 + 8) * sizeof(bf16_t);
         hipLaunchKernelGGL((gemm_p16_kernel<MT, WPG, KS, EPI, true>), grid, dim3(256), shm, st, a);
     } else {
@@ -307,16 +301,6 @@ static void launch_t(const GemmArgs& a, int mblocks, hipStream_t st) {
     }
 }
 
-// GeGLU K-interleave: 2 (default; decode block = 2 row groups x 2 waves) or 4
-// (T5G_GEGLU_KS4=1: decode block = 1 row group x 4 waves, twice the blocks). Read once.
-static int geglu_ks() {
-    static int ks = 0;
-    if (!ks) {
-        const char* v = getenv("T5G_GEGLU_KS4");
-        ks = (v && v[0] == '1') ? 4 : 2;
-    }
-    return ks;
-}
 
 // decode (WPG = KS) and prefill (WPG = 1) instantiate the same slice order
 template <int MT, bool PREFILL>
@@ -327,10 +311,9 @@ static int launch_epi(const GemmArgs& a, int epi, int mblocks, hipStream_t st) {
         case EPI_BF16: launch_t<MT, W4, 4, EPI_BF16>(a, mblocks, st); break;
         case EPI_BIAS_BF16: launch_t<MT, W4, 4, EPI_BIAS_BF16>(a, mblocks, st); break;
         case EPI_BIAS_GELU: launch_t<MT, W4, 4, EPI_BIAS_GELU>(a, mblocks, st); break;
-        case EPI_GEGLU:
-            if (geglu_ks() == 4) launch_t<MT, W4, 4, EPI_GEGLU>(a, mblocks, st);
-            else launch_t<MT, W2, 2, EPI_GEGLU>(a, mblocks, st);
-            break;
+        // GeGLU: 2 row groups x 2-way K interleave per decode block (r01 probe: 1 group x 4
+        // waves, twice the blocks, was not faster)
+        case EPI_GEGLU: launch_t<MT, W2, 2, EPI_GEGLU>(a, mblocks, st); break;
         case EPI_F32: launch_t<MT, W4, 4, EPI_F32>(a, mblocks, st); break;
         default: return -4;
     }
