@@ -140,3 +140,4 @@ def test_gemv_batch_invariant():
     full = run(list(range(M)))
     for m in (0, 3, 7):
         assert torch.equal(run([m])[0], full[m])
+

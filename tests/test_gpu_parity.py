@@ -316,6 +316,32 @@ def test_batched_rows_equal_single_rows():
             assert torch.equal(one["logits"][t][0], batch["logits"][t][b]), (b, t)
 
 
+def test_batch32_rows_equal_single_rows():
+    """At B = 32 (C5; decode GEMMs on the tiled kernel instead of the <= 16-row GEMV) rows
+    of a 32-row batch equal the same utterances run alone (tokens bitwise), on the
+    on-device sampler."""
+    _need_gpu()
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import SamplingParams, Utterance
+    from t5gemma_tts_amd.weights import synthetic_weights
+    cfg = named_config("tiny")
+    sd = synthetic_weights(cfg, 7)
+    eng = _engine(cfg, sd, max_batch=32, max_text=64, max_audio=256, max_gen=200)
+    rng = np.random.default_rng(4)
+    utts = []
+    for b in range(32):
+        x = rng.integers(3, 500, size=int(rng.integers(3, 30))).tolist()
+        tp = int(rng.integers(0, 12))
+        y = rng.integers(0, 64, size=tp).tolist() + ([cfg.y_sep_token] if tp else [])
+        utts.append(Utterance(x=x, y=y, tgt_y_len=len(y) + int(rng.integers(10, 40))))
+    p = SamplingParams(top_k=20, top_p=0.9, temperature=0.9)
+    seeds = list(range(100, 132))
+    batch = eng.generate(utts, p, seeds=seeds)
+    for b in (0, 15, 16, 31):
+        one = eng.generate([utts[b]], p, seeds=[seeds[b]])
+        assert one["gen"][0].tolist() == batch["gen"][b].tolist(), b
+
+
 def test_graph_fast_path_matches_eager_launches():
     """hipGraph replay == plain launches (production Philox noise, same seeds)."""
     _need_gpu()

@@ -15,6 +15,38 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def main32():
+    """B = 32: the 17..32-row GEMV against the tiled decode GEMM (gemm_p16) it replaces."""
+    from t5gemma_tts_amd import _lib
+    L = _lib.lib()
+    dev = torch.device("cuda:0")
+    M, d, f = 32, 2304, 9216
+    N = 2 * f
+    st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    Ws = []
+    for i in range(8):
+        raw = (torch.randn(N, d, generator=g) * 0.02).to(torch.bfloat16).to(dev)
+        dst = torch.empty(int(L.t5g_packed_bytes(N, d)) // 2, dtype=torch.bfloat16, device=dev)
+        _lib.check(L.t5g_pack_weight(C.c_void_p(raw.data_ptr()), N, d, d, C.c_void_p(dst.data_ptr()), st), "pack")
+        Ws.append(dst)
+    X = torch.randn(M, d, device=dev).to(torch.bfloat16)
+    Y = torch.empty(M, f, dtype=torch.bfloat16, device=dev)
+    arr = (C.c_void_p * len(Ws))(*[w.data_ptr() for w in Ws])
+    alg = N * d * 2 + M * d * 2 + M * f * 2
+    for m in (16, 24, 32):
+        a = _lib.GemvArgs()
+        a.M, a.K, a.N, a.epi, a.pro, a.nw, a.un = m, d, N, 3, 0, 8, 8
+        a.X, a.ldx, a.Y, a.ldy, a.splits, a.layout, a.max_grid = X.data_ptr(), d, Y.data_ptr(), f, 1, 0, 0
+        us = C.c_float()
+        _lib.check(L.t5g_time_gemv(C.byref(a), arr, len(Ws), 240, st, C.byref(us)), "gemv")
+        us2 = C.c_float()
+        _lib.check(L.t5g_time_gemm(C.c_void_p(X.data_ptr()), d, m, arr, len(Ws), N, d, 1, C.c_void_p(Y.data_ptr()), f,
+                                   3, 240, st, C.byref(us2)), "gemm")
+        print(json.dumps({"M": m, "gemv_us": round(us.value, 2), "gemm_p16_us": round(us2.value, 2),
+                          "gemv_GBps": round(alg / (us.value * 1e-6) / 1e9, 1)}), flush=True)
+
+
 def main():
     from t5gemma_tts_amd import _lib
     L = _lib.lib()
@@ -49,4 +81,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main32() if "--m32" in sys.argv else main()
