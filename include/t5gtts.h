@@ -231,7 +231,8 @@ typedef struct {
     int32_t un;               /* tuning: fragments in flight per wave (8 / 16), 0 = default */
     int32_t max_grid;         /* tuning: blocks per launch cap, 0 = one per CU */
     int32_t splits;           /* split-K (epi 4): fp32 slabs [splits][M][ldy]; 0/1 = none */
-    int32_t layout;           /* reserved (0: W packed P16) */
+    int32_t layout;           /* 0: the LDS-staged-X GEMV (M <= 16); 1: the register-resident-X
+                                 GEMV (M <= 32, K = 2304, no split); W packed P16 either way */
 } t5g_gemv_args;
 int t5g_gemv(const t5g_gemv_args* args, void* stream);
 /* hipEvent-timed `iters` launches rotating over packed weights Wp_list[i % n_w]

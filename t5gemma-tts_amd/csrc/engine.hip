@@ -525,12 +525,14 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         RC(gemm(att, e->q_dim, M, L.cross_o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
                 s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode));
         RC(resid(s_o, L.norms[3], L.norms[4]));
-        // --- GeGLU MLP (decode: the one-block-per-CU GEMV)
-        if (decode && M <= 16) {
+        // --- GeGLU MLP (decode: the one-block-per-CU GEMV; register-resident X at the
+        // 2b-2b width, up to 32 rows)
+        if (decode && (M <= 16 || (M <= 32 && d == 2304))) {
             DecGemmArgs g = dec_args(M, L.gate_up, 2 * f, d, act, f, 8);
             g.X = xn;
             g.ldx = d;
             g.un = 8;
+            g.layout_rx = d == 2304;
             RC(gemv_dec(g, EPI_GEGLU, st));
         } else {
             RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st, !decode));
@@ -882,7 +884,7 @@ static_assert(sizeof(t5g_gemv_args) == 152, "t5g_gemv_args layout");
 
 static int gemv_from_abi(const t5g_gemv_args* g, const void* W, DecGemmArgs* out) {
     if (!g || !W || !g->Y || g->M <= 0 || g->N <= 0 || g->K <= 0 || g->K % 32) return T5G_EINVAL;
-    if (g->pro != 0 || g->layout != 0) return T5G_EUNSUPPORTED;   // prologue variants were removed
+    if (g->pro != 0 || g->layout < 0 || g->layout > 1) return T5G_EUNSUPPORTED;   // prologue variants were removed
     DecGemmArgs a = dec_args(g->M, W, g->N, g->K, g->Y, g->ldy, g->nw);
     a.X = (const bf16_t*)g->X;
     a.ldx = g->ldx;
@@ -890,6 +892,7 @@ static int gemv_from_abi(const t5g_gemv_args* g, const void* W, DecGemmArgs* out
     a.un = g->un;
     a.max_grid = g->max_grid;
     a.splits = g->splits > 1 ? g->splits : 1;
+    a.layout_rx = g->layout == 1;
     *out = a;
     return T5G_OK;
 }

@@ -193,6 +193,117 @@ __global__ __launch_bounds__(NW * 64) void gemv_dec_kernel(DecGemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Register-resident X variant for 1..32 rows (MT = 1 or 2 sixteen-row MFMA tiles): all
+// NW waves share each unit's K stream (wave ks takes k-steps ks, ks + NW, ...: SPU of
+// them, a compile-time count, so one unit = one batch of SPU fragments per wave), and the
+// X fragments of a wave's k-steps never change from unit to unit -- they are loaded once
+// into registers before the stream starts. No X staging in LDS (32 rows x K = 2304 would
+// not fit beside the partial sums) and no barrier before the first MFMA. Batches are
+// double-buffered per unit: unit i + 1's fragments are in flight while unit i multiplies.
+// Per-row results are bitwise those of gemv_dec_kernel (same k-step order per wave, same
+// fixed-order wave reduction).
+template <int NW, int MT, int EPI, int SPU>
+__global__ __launch_bounds__(NW * 64) void gemv_rx_kernel(DecGemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    f32x4* red = (f32x4*)smem;   // [umax][MT][NW][64]
+    const int nb = (int)gridDim.x, bu = (int)blockIdx.x;
+    const int nu = (a.NG - bu + nb - 1) / nb;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int KB = a.KB;
+    const int per = (KB + a.splits - 1) / a.splits;
+    const int kb_lo = (int)blockIdx.y * per;
+    const int KBs = max(0, min(KB, kb_lo + per) - kb_lo);
+    const int xr = lane & 15;
+    const __amdgpu_buffer_rsrc_t wr = frag_rsrc(a.W, (uint32_t)a.NG * (uint32_t)KB * 1024u);
+    auto wbatch = [&](int i, bf16x8_s(&w)[SPU]) __attribute__((always_inline)) {
+        const int g = bu + i * nb;
+#pragma unroll
+        for (int j = 0; j < SPU; ++j) {
+            const int kb = wave + j * NW;
+            const int off = (i < nu && kb < KBs) ? ((g * KB + kb_lo + kb) * 64 + lane) * 16 : (int)0xfffffff0u;
+            w[j] = __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 2));
+        }
+    };
+    bf16x8_s wa[SPU], wb[SPU];
+    wbatch(0, wa);
+    // this wave's X fragments (rows >= M and k-steps past the slice are zero)
+    bf16x8_s xf[MT][SPU];
+    const bf16x8_s z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        const int row = 16 * t + xr;
+        const bf16_t* xp = a.X + (long)min(row, a.M - 1) * a.ldx + kb_lo * 32 + 8 * (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < SPU; ++j) {
+            const int kb = min(wave + j * NW, KBs - 1);
+            const bf16x8_s v = *(const bf16x8_s*)(xp + kb * 32);
+            xf[t][j] = (row < a.M && wave + j * NW < KBs) ? v : z8;
+        }
+    }
+    auto mul = [&](int i, bf16x8_s(&w)[SPU]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < SPU; ++j) acc = mfma16(w[j], xf[t][j], acc);
+            if (i < nu) red[((i * MT + t) * NW + wave) * 64 + lane] = acc;
+        }
+    };
+    for (int i = 0; i < nu; i += 2) {
+        wbatch(i + 1, wb);
+        mul(i, wa);
+        wbatch(i + 2, wa);
+        mul(i + 1, wb);
+    }
+    __syncthreads();
+
+    constexpr bool GLU = EPI == EPI_GEGLU;
+    if (GLU && lane >= 32) return;
+    const int n_out = GLU ? a.N / 2 : a.N;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        const int m = 16 * t + xr;
+        if (m >= a.M) continue;
+        for (int i = wave; i < nu; i += NW) {
+            const f32x4* ri = red + (size_t)(i * MT + t) * NW * 64 + lane;
+            const int n0 = (bu + i * nb) * (GLU ? 8 : 16) + 4 * (lane >> 4);
+            float v[4];
+            if constexpr (GLU) {
+                f32x4 gs = {0.f, 0.f, 0.f, 0.f}, us = gs;
+#pragma unroll
+                for (int s2 = 0; s2 < NW; ++s2) {
+                    gs += ri[s2 * 64];
+                    us += ri[s2 * 64 + 32];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_tanh(rbf(gs[r]))) * rbf(us[r]);
+            } else {
+                f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s2 = 0; s2 < NW; ++s2) s4 += ri[s2 * 64];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = s4[r];
+            }
+            if constexpr (EPI == EPI_F32) {
+                float* y = (float*)a.Y + ((long)blockIdx.y * a.M + m) * a.ldy;
+                for (int r = 0; r < 4; ++r)
+                    if (n0 + r < n_out) y[n0 + r] = v[r];
+            } else {
+                bf16_t* y = (bf16_t*)a.Y + (long)m * a.ldy;
+                for (int r = 0; r < 4; ++r) {
+                    float x = v[r];
+                    if constexpr (EPI == EPI_BIAS_BF16 || EPI == EPI_BIAS_GELU) {
+                        if (n0 + r < n_out) x = x + bf2f(a.bias[n0 + r]);
+                    }
+                    if constexpr (EPI == EPI_BIAS_GELU) x = gelu_erf(rbf(x));
+                    if (n0 + r < n_out) y[n0 + r] = f2bf(x);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 constexpr size_t GD_LDS_MAX = 160 * 1024;   // gfx950: 160 KB LDS per workgroup
 
 static int cu_count() {
@@ -251,8 +362,39 @@ size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int rg) {
     return (size_t)umax * a.nw * 64 * 16 + (size_t)a.M * (per * 32 + 8) * sizeof(bf16_t);
 }
 
+// the register-resident-X kernel for the shapes it is instantiated for (8 waves sharing
+// each unit's K stream, SPU = 9 k-steps per wave: K = 2304, no split) -- 0 if launched
+template <int MT, int EPI>
+static int launch_rx(const DecGemmArgs& a, hipStream_t st) {
+    auto* fn = gemv_rx_kernel<8, MT, EPI, 9>;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GD_LDS_MAX);
+        attr = true;
+    }
+    const int grid = gd_grid(a, 1);
+    const size_t shm = (size_t)((a.NG + grid - 1) / grid) * MT * 8 * 64 * 16;
+    if (shm > GD_LDS_MAX) return -1;
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid, 1u), dim3(8 * 64), shm, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int gemv_rx(const DecGemmArgs& a, int epi, hipStream_t st) {
+    if (a.M <= 0 || a.M > 32 || a.KB != 72 || a.K != 2304 || a.splits > 1 || a.NG % 4 || a.NG * 16 < a.N) return -1;
+    if (!a.X || a.ldx < a.K || a.ldx % 8) return -1;
+    if ((epi == EPI_BIAS_BF16 || epi == EPI_BIAS_GELU) && !a.bias) return -1;
+    const bool two = a.M > 16;
+    switch (epi) {
+        case EPI_BF16: return two ? launch_rx<2, EPI_BF16>(a, st) : launch_rx<1, EPI_BF16>(a, st);
+        case EPI_BIAS_BF16: return two ? launch_rx<2, EPI_BIAS_BF16>(a, st) : launch_rx<1, EPI_BIAS_BF16>(a, st);
+        case EPI_GEGLU: return two ? launch_rx<2, EPI_GEGLU>(a, st) : launch_rx<1, EPI_GEGLU>(a, st);
+        default: return -1;
+    }
+}
+
 int gemv_dec(const DecGemmArgs& a, int epi, hipStream_t st) {
     if (a.M <= 0) return 0;
+    if (a.layout_rx) return gemv_rx(a, epi, st);
     if (a.M > 16 || a.K % 32 || a.KB * 32 != a.K || a.NG % 4 || a.NG * 16 < a.N) return -1;
     if (a.splits < 1 || a.splits > 64 || (a.splits > 1 && epi != EPI_F32)) return -1;
     if (a.nw != 4 && a.nw != 8 && a.nw != 16) return -1;

@@ -40,6 +40,7 @@ struct DecGemmArgs {
     int un;                   // fragments in flight per wave (8 / 16), 0 = default
     int max_grid;             // blocks per launch cap, 0 = one per CU
     int splits;               // split-K over blockIdx.y (EPI_F32 only)
+    int layout_rx;            // 1: register-resident-X kernel (1..32 rows, K = 2304)
 };
 int gemv_dec(const DecGemmArgs& a, int epi, hipStream_t st);
 size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int rg);

@@ -61,7 +61,7 @@ CASES = [  # epi, M, N, K, nw, splits
 ]
 
 
-def _run(epi, M, N, K, nw, splits, seed, max_grid=0, X=None, W=None):
+def _run(epi, M, N, K, nw, splits, seed, max_grid=0, X=None, W=None, layout=0):
     from t5gemma_tts_amd import _lib
     L = _lib.lib()
     dev = "cuda"
@@ -78,6 +78,7 @@ def _run(epi, M, N, K, nw, splits, seed, max_grid=0, X=None, W=None):
     bd, Xd = bias.to(dev), X.to(dev)
     a = _lib.GemvArgs()
     a.M, a.K, a.N, a.epi, a.pro, a.nw, a.splits, a.max_grid = M, K, N, epi, 0, nw, splits, max_grid
+    a.layout = layout
     a.W, a.bias, a.Y, a.ldy, a.ldx, a.X = Wp.data_ptr(), bd.data_ptr(), Y.data_ptr(), n_out, K, Xd.data_ptr()
     assert L.t5g_gemv(C.byref(a), st) == 0
     torch.cuda.synchronize()
@@ -141,3 +142,23 @@ def test_gemv_batch_invariant():
     for m in (0, 3, 7):
         assert torch.equal(run([m])[0], full[m])
 
+
+
+@pytest.mark.parametrize("epi,M", [(3, 8), (3, 1), (3, 16), (0, 8), (3, 32), (3, 24), (1, 17)])
+def test_gemv_register_x_variant(epi, M):
+    """layout 1 (register-resident X, 1..32 rows, K = 2304): vs the fp32 reference, and
+    bitwise equal to the LDS-staged kernel on every 16-row slice of the batch."""
+    _need_gpu()
+    N, K = (18432, 2304) if epi == 3 else (6000, 2304)
+    g = torch.Generator(device="cpu").manual_seed(M + epi)
+    W = (torch.randn(N, K, generator=g) * 0.02).to(BF16)
+    X = torch.randn(M, K, generator=g).to(BF16)
+    got, _, _, bias = _run(epi, M, N, K, 8, 1, seed=3, X=X, W=W, layout=1)
+    ref = _epilogue(X.float() @ W.float().t(), epi, bias)
+    if epi == 3:
+        assert (got - ref).abs().max() <= 2 ** -6 * ref.abs().max()
+    else:
+        _close_bf16(got, ref, frac=0.97)
+    parts = [_run(epi, min(16, M - r0), N, K, 8, 1, seed=3, X=X[r0:r0 + 16].contiguous(), W=W, layout=0)[0]
+             for r0 in range(0, M, 16)]
+    assert torch.equal(got, torch.cat(parts)), "register-X rows differ from the LDS-staged kernel"

@@ -34,17 +34,23 @@ def main32():
     Y = torch.empty(M, f, dtype=torch.bfloat16, device=dev)
     arr = (C.c_void_p * len(Ws))(*[w.data_ptr() for w in Ws])
     alg = N * d * 2 + M * d * 2 + M * f * 2
-    for m in (16, 24, 32):
-        a = _lib.GemvArgs()
-        a.M, a.K, a.N, a.epi, a.pro, a.nw, a.un = m, d, N, 3, 0, 8, 8
-        a.X, a.ldx, a.Y, a.ldy, a.splits, a.layout, a.max_grid = X.data_ptr(), d, Y.data_ptr(), f, 1, 0, 0
-        us = C.c_float()
-        _lib.check(L.t5g_time_gemv(C.byref(a), arr, len(Ws), 240, st, C.byref(us)), "gemv")
+    for m in (1, 8, 16, 24, 32):
+        res = {}
+        for layout in (0, 1):
+            if layout == 0 and m > 16:
+                continue
+            a = _lib.GemvArgs()
+            a.M, a.K, a.N, a.epi, a.pro, a.nw, a.un = m, d, N, 3, 0, 8, 8
+            a.X, a.ldx, a.Y, a.ldy, a.splits, a.layout, a.max_grid = X.data_ptr(), d, Y.data_ptr(), f, 1, layout, 0
+            us = C.c_float()
+            _lib.check(L.t5g_time_gemv(C.byref(a), arr, len(Ws), 240, st, C.byref(us)), "gemv")
+            res[layout] = round(us.value, 2)
         us2 = C.c_float()
         _lib.check(L.t5g_time_gemm(C.c_void_p(X.data_ptr()), d, m, arr, len(Ws), N, d, 1, C.c_void_p(Y.data_ptr()), f,
                                    3, 240, st, C.byref(us2)), "gemm")
-        print(json.dumps({"M": m, "gemv_us": round(us.value, 2), "gemm_p16_us": round(us2.value, 2),
-                          "gemv_GBps": round(alg / (us.value * 1e-6) / 1e9, 1)}), flush=True)
+        print(json.dumps({"M": m, "gemv_lds_x_us": res.get(0), "gemv_reg_x_us": res[1],
+                          "gemm_p16_us": round(us2.value, 2),
+                          "reg_x_GBps": round(alg / (res[1] * 1e-6) / 1e9, 1)}), flush=True)
 
 
 def main():
