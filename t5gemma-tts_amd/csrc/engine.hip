@@ -294,6 +294,7 @@ extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t*
         if (l == 0) {
             n.ids = ids;
             n.table = (const bf16_t*)e->w.enc_embed;
+            n.n_table = c.text_vocab;
             n.scale = c.normalizer;
         } else {
             n.delta = e->tmp;  // previous layer's down-proj output
@@ -476,6 +477,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             NormArgs n = norm_args(M, d, c.rms_eps);
             n.ids = ids;
             n.table = (const bf16_t*)e->w.audio_embed;
+            n.n_table = c.n_audio_tokens;
             n.scale = c.normalizer;
             n.pre_w = (const bf16_t*)L.norms[0];
             n.resid_out = h;

@@ -68,7 +68,10 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
     const u32x4 rw = *(const u32x4*)(a.resid + (long)m * d + 8 * cc);
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (SRC == 1) {
-        unpack8(*(const u32x4*)(a.table + (long)a.ids[m] * d + 8 * cc), v);
+        // the host rejects out-of-range ids (engine.py); the clamp only keeps a bad id
+        // passed through the C ABI from reading outside the table
+        const int id = min(max(a.ids[m], 0), a.n_table - 1);
+        unpack8(*(const u32x4*)(a.table + (long)id * d + 8 * cc), v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = rbf(v[j] * a.scale);
     } else if constexpr (SRC == 2) {
@@ -126,6 +129,7 @@ int resid_norm(const NormArgs& a_in, hipStream_t st) {
     const int threads = ((a.d / 8 + 63) / 64) * 64;
     const int src = a.ids ? 1 : (a.part ? 2 : 0);
     if (src == 0 && !a.delta) return -1;
+    if (src == 1 && (!a.table || a.n_table <= 0)) return -1;
     if (src == 2 && (a.nsplit < 1 || a.nsplit > 8)) return -1;
     const dim3 g((unsigned)a.M), b(threads);
 #define T5G_NORM(NS_, SRC_) \

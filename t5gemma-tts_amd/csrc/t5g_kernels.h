@@ -50,6 +50,7 @@ struct NormArgs {
     int M, d;
     const int* ids;          // optional: v = bf16(table[ids[m]] * scale)
     const bf16_t* table;
+    int n_table;             // rows of table: ids are clamped into [0, n_table) (no OOB read)
     float scale;
     const bf16_t* delta;     // [M][d] bf16 (if ids == null and part == null)
     const float* part;       // fp32 partial slabs [nsplit][M][ldp]

@@ -299,6 +299,10 @@ class T5GemmaTTSEngine:
                 raise ValueError("empty text")
             if len(x) > self.max_text:
                 raise ValueError(f"text length {len(x)} > max_text {self.max_text}")
+            n_text = cfg.backbone.text_vocab_size
+            if min(x) < 0 or max(x) >= n_text:
+                # nn.Embedding in the reference: "index out of range in self"
+                raise IndexError(f"text id out of range [0, {n_text}): index out of range in self")
             ids += x
             trow += [b] * len(x)
             tt += list(range(len(x)))
@@ -307,6 +311,9 @@ class T5GemmaTTSEngine:
             y = [int(v) for v in u.y]
             if cfg.special_first:
                 y = [v + int(cfg.n_special) for v in y]
+            if y and (min(y) < 0 or max(y) >= self.V):
+                raise IndexError(f"audio token out of range [0, {self.V}) (codec codes must match the model's "
+                                 "audio vocabulary): index out of range in self")
             y_rows.append(y)
             cated = [cfg.empty_token] + y
             cur_len = len(cated)

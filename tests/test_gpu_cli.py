@@ -32,3 +32,62 @@ def test_run_inference_synthetic_tiny_matches_drop_in():
                                  temperature=0.8, stop_repetition=3, silence_tokens=[], prompt_frames=0)
     want = strip_sep_and_eos(gen, cfg.y_sep_token, cfg.eos)
     assert frames.reshape(-1).tolist() == want.reshape(-1).tolist()
+
+
+def test_run_inference_transcribes_reference_speech_with_whisper(tmp_path, monkeypatch):
+    """reference_speech without reference_text (inference_commandline_hf.py:144-150): the
+    CLI loads a local openai-format Whisper checkpoint by name from the whisper cache
+    directory (here a seeded tiny one plus a synthetic tiktoken vocabulary), transcribes
+    the reference WAV on the GPU, and the transcript becomes the prompt text -- the same
+    prompt run_inference builds when that text is passed as reference_text."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import sys
+    from t5gemma_tts_amd import cli, whisper_asr
+    from t5gemma_tts_amd.audio import write_wav
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "oracle"))
+    sys.path.insert(0, os.path.join(repo, "tests", "golden"))
+    from make_golden_codec_enc import test_wave
+    from whisper_oracle import write_synthetic_tiktoken
+    cache = tmp_path / "whisper"
+    cache.mkdir()
+    d = whisper_asr.dims_tiny()
+    torch.save({"dims": dict(d.__dict__), "model_state_dict": whisper_asr.synthetic_weights(d, 41)},
+               str(cache / "tiny-test.pt"))
+    write_synthetic_tiktoken(str(cache / "multilingual.tiktoken"), 50257, 0)
+    monkeypatch.setenv("XDG_CACHE_HOME", str(tmp_path))
+    ref = str(tmp_path / "ref.wav")
+    write_wav(ref, test_wave(16000 * 2, 3), 16000)
+    model = cli.load_model(synthetic="tiny", max_text=2048, max_audio=512)
+
+    class TinyVocabCodec:
+        """The tiny codec with its codes folded into the tiny voice model's 64 audio tokens
+        (the two synthetic configs do not share a vocabulary)."""
+        def __init__(self, c):
+            self.c = c
+
+        def __getattr__(self, k):
+            return getattr(self.c, k)
+
+        def encode(self, wav):
+            return self.c.encode(wav) % 64
+    codec = TinyVocabCodec(cli.load_codec(codec="tiny", max_batch=1, max_frames=512))
+    tok = cli.ByteTokenizer()
+    asr = whisper_asr.load_model("tiny-test", device="cuda:0", max_seconds=5)
+    text = asr.transcribe(ref)["text"]
+    seen = []
+    import t5gemma_tts_amd.pipeline as pl
+    orig = pl.inference_one_sample
+
+    def spy(**kw):
+        seen.append(kw["prefix_transcript"])
+        return orig(**kw)
+    monkeypatch.setattr(pl, "inference_one_sample", spy)
+    with tempfile.TemporaryDirectory() as td:
+        cli.run_inference(reference_speech=ref, target_text="hi", target_duration=0.4, seed=3, output_dir=td,
+                          model=model, audio_tokenizer=codec, text_tokenizer=tok, whisper_model="tiny-test")
+        assert os.path.getsize(os.path.join(td, "generated.wav")) > 44
+    from t5gemma_tts_amd.text import normalize_text_with_lang
+    _, lang_code = normalize_text_with_lang("hi", None)
+    assert seen and seen[0] == normalize_text_with_lang(text, lang_code)[0]

@@ -342,6 +342,25 @@ def test_batch32_rows_equal_single_rows():
         assert one["gen"][0].tolist() == batch["gen"][b].tolist(), b
 
 
+def test_out_of_range_ids_raise_before_any_launch():
+    """Text ids >= the text vocabulary and prompt codes >= the audio vocabulary raise
+    IndexError (the reference's nn.Embedding does) instead of reaching the embedding
+    gathers; the engine keeps working afterwards."""
+    _need_gpu()
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import SamplingParams, Utterance
+    from t5gemma_tts_amd.weights import synthetic_weights
+    cfg = named_config("tiny")
+    eng = _engine(cfg, synthetic_weights(cfg, 7), max_batch=1, max_text=64, max_audio=256, max_gen=64)
+    p = SamplingParams(top_k=20, top_p=0.9)
+    with pytest.raises(IndexError):
+        eng.generate([Utterance(x=[5, cfg.backbone.text_vocab_size], y=[], tgt_y_len=10)], p, seeds=[1])
+    with pytest.raises(IndexError):
+        eng.generate([Utterance(x=[5, 6], y=[1, 65535, 2], tgt_y_len=20)], p, seeds=[1])
+    out = eng.generate([Utterance(x=[5, 6], y=[1, 2], tgt_y_len=20)], p, seeds=[1])
+    assert len(out["gen"][0]) > 0
+
+
 def test_graph_fast_path_matches_eager_launches():
     """hipGraph replay == plain launches (production Philox noise, same seeds)."""
     _need_gpu()
