@@ -244,7 +244,8 @@ int t5g_time_gemv(const t5g_gemv_args* args, const void* const* Wp_list, int32_t
  * engine's decode step runs for self / cross attention ([tf] T5GemmaSelfAttention
  * :264-304 with the KV cache of cache_utils.py:127-144; PMCrossAttention :167-253) --
  * keys split in chunks of <= 64 over workgroups, exp values rounded to bf16 before P.V
- * like torch's CPU SDPA, partials merged by the combine kernel. For parity tests. */
+ * like torch's CPU SDPA, then one P.V + combine launch over 32-dimension slices of the
+ * output for rows of > 64 keys. For parity tests. */
 typedef struct {
     int32_t B, n_heads, n_kv_heads, head_dim;
     const void* q;            /* bf16 [B][n_heads * head_dim], PM-RoPE already applied */
@@ -256,7 +257,7 @@ typedef struct {
     int32_t window;           /* sliding window (0: none) */
     float scale;
     void* out;                /* bf16 [B][n_heads * head_dim] */
-    void* work;               /* fp32 partials, t5g_attention_decode_work_bytes() */
+    void* work;               /* fp32 scores + chunk maxima, t5g_attention_decode_work_bytes() */
 } t5g_attn_decode_args;
 int64_t t5g_attention_decode_work_bytes(int32_t B, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
                                         int32_t cap);

@@ -311,10 +311,9 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 //    rounded, PM-RoPE'd in-kernel), the step's own k/v appended to the cache by the
 //    chunk holding t, scores of the chunk. A row of <= 64 keys is finished here (softmax,
 //    P.V, output). Longer rows publish scores + chunk maxima for:
-//  * attn_pv_kernel: the chunk's p against its block's running max (known only once
-//    every chunk of the block has its scores), bf16 P, partial P.V;
-//  * attn_combine_kernel: l with aten's lane-ordered block sums, the partial P.V summed
-//    per block, rescaled across blocks, scaled by 1/l.
+//  * attn_pvc_kernel: per (row, kv head, 32-dimension slice) the exact p of every key
+//    against its block's running max, l with aten's lane-ordered block sums, bf16 P.V
+//    over the slice, rescaled across blocks, scaled by 1/l.
 constexpr int QSMAX = 4;   // q / appended-k/v projection slabs read by the decode kernel
 constexpr int DCH = 64;    // keys per decode chunk
 
@@ -604,214 +603,202 @@ __device__ __forceinline__ DecRow dec_row(const AttnArgs& a, int qi) {
     return {lo, hi, max(hi - lo, 0)};
 }
 
+// P.V and combine of the rows of > 64 keys in ONE launch (attn_pvc_kernel). Workgroup
+// (row, kv head, z) owns PVC_DZ of the D output dimensions of the G heads, for every key
+// of the row, so nothing is handed between workgroups: it recomputes the exact p of each
+// aten 512-key block from the published scores and chunk maxima (cheap: <= 2 x 4096
+// exps), takes l from aten's lane-ordered block sums of them, and streams only its
+// PVC_DZ-wide slice of V (64 B per key at D = 256, all 8 slices of a row on one XCD
+// under round-robin placement, so a 128-B line is fetched once).
+// The fp32 sums keep the order of the former per-chunk P.V + combine pair, so results are
+// bit-identical to it: per 64-key chunk, KPB key slots (slot = wave * KPW + kg of the
+// chunk kernel's lane map) each accumulate NIT keys j = c0 + i * KPB + slot in i order;
+// the KPW slots of a wave fold as a pairwise (xor-butterfly) tree, the 4 waves in order;
+// the chunks of a block are summed in order from 0; dst = dst * exp(m_old - m) + block.
+constexpr int PVC_DZ = 32;   // output dimensions per workgroup
+
 template <int D, int G>
-__global__ __launch_bounds__(256, 2) void attn_pv_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
     constexpr int LPK = D / 8;
     constexpr int KPW = 64 / LPK;
-    constexpr int KPB = KPW * 4;
-    constexpr int NIT = DCH / KPB;
-    constexpr int CPB = SDPA_KV_BLOCK / DCH;   // chunks per aten kv block
-    __shared__ float sp_p[G][DCH];
-    __shared__ float mrun[G];
-    __shared__ f32x4 ored[4][G][LPK][2];
-    const int qi = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int kg = lane / LPK, dl = lane % LPK;
+    constexpr int KPB = KPW * 4;                // key slots per chunk
+    constexpr int NIT = DCH / KPB;              // keys per slot chain
+    constexpr int NOCT = PVC_DZ / 8;            // 16-byte dimension octets per workgroup
+    constexpr int TPC = KPB * NOCT;             // threads per chunk
+    constexpr int CPR = 256 / TPC;              // chunks per sub-round
+    constexpr int CPB = SDPA_KV_BLOCK / DCH;    // chunks per aten kv block
+    constexpr int RPB = CPB / CPR;              // sub-rounds per kv block
+    constexpr int PPT = SDPA_KV_BLOCK / 256;    // block positions per thread when staging p
+    static_assert(256 % TPC == 0 && CPB % CPR == 0 && D % PVC_DZ == 0, "pvc geometry");
+    __shared__ float pex[G][SDPA_KV_BLOCK + 16];   // exact p of the current block (l)
+    __shared__ float pbf[G][SDPA_KV_BLOCK];        // bf16-rounded p (P.V)
+    __shared__ float mrun[G][SDPA_MAX_BLOCKS];     // running max through block b
+    __shared__ float et_s[G], stat_l[G];
+    __shared__ float ol[CPR][KPB][G][PVC_DZ];      // slot chain sums of the sub-round
+    const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    T5G_TS(0);
     const int row = a.q_row ? a.q_row[qi] : qi;
     const DecRow r = dec_row(a, qi);
     if (r.span <= DCH) return;                  // finished by attn_decode_kernel
-    const int c0 = r.lo + sp * DCH;
-    if (c0 >= r.hi) return;
-    const int c1 = min(r.hi, c0 + DCH);
-    const int n = c1 - c0;
-    // V rows of the chunk first (in flight while the maxima and scores are read)
-    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
-    const __amdgpu_buffer_rsrc_t vrs = frag_rsrc(Vb, (uint32_t)a.kv_cap * D * 2u);
-    u32x4 vr[NIT];
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-        const int j = c0 + i * KPB + wave * KPW + kg;
-        const int off = j < c1 ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
-        vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
-    }
-    const int bi = sp / CPB;                                  // aten kv block of this chunk
-    const int nch = (r.span + DCH - 1) / DCH;
-    const int blen = min(SDPA_KV_BLOCK, r.span - bi * SDPA_KV_BLOCK);
-    if (wave < G) {
-        const int g = wave;
-        // running max through the end of this chunk's block
-        const int cend = min(nch, (bi + 1) * CPB);
-        const float m = lane < cend ? a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + lane) * G + g] : -INFINITY;
-        const float mx = wave_max(m);
-        if (lane == 0) mrun[g] = mx;
-        float* srow = a.sbuf + ((long)qi * a.Hkv * G + kvh * G + g) * a.kv_cap + c0;
-        const float s = lane < n ? srow[lane] : 0.f;
-        const int pos = c0 + lane - r.lo - bi * SDPA_KV_BLOCK;
-        const float p = lane < n ? sdpa_p(__fsub_rn(s, mx), pos, blen) : 0.f;
-        sp_p[g][lane] = rbf(p);
-        if (lane < n) srow[lane] = p;   // the exact p replaces the score: read by the combine
-    }
-    __syncthreads();
-    float o[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-        const int jl = i * KPB + wave * KPW + kg;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float p = sp_p[g][jl];
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                o[g][2 * jj] += p * bf_lo(vr[i][jj]);
-                o[g][2 * jj + 1] += p * bf_hi(vr[i][jj]);
-            }
-        }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj)
-#pragma unroll
-            for (int off = LPK; off < 64; off <<= 1) o[g][jj] += __shfl_xor(o[g][jj], off, 64);
-    if (kg == 0) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            ored[wave][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
-            ored[wave][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
-        }
-    }
-    __syncthreads();
-    float* pbase = a.part + (((long)qi * a.Hkv + kvh) * a.nsplit + sp) * (G * (D + 2));
-    for (int idx = threadIdx.x; idx < G * LPK; idx += 256) {
-        const int g = idx / LPK, d8 = idx % LPK;
-        const f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
-        const f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
-        float* pg = pbase + g * (D + 2);
-        if (d8 == 0) pg[0] = mrun[g];
-        *(f32x4*)(pg + 2 + 8 * d8) = lo4;
-        *(f32x4*)(pg + 6 + 8 * d8) = hi4;
-    }
-}
-
-// Each (row, kv head) is combined by CZ blocks of 64*G threads, one slice of the (g, d4)
-// quads each (a single block per (row, kv head) was per-CU-bandwidth bound).
-template <int D, int G>
-constexpr int combine_cz() { return (G * D / 4 + 31) / 32; }
-
-template <int D, int G>
-__global__ __launch_bounds__(64 * G) void attn_combine_kernel(AttnArgs a) {
-    constexpr int CPB = SDPA_KV_BLOCK / DCH;
-    __shared__ float blk_et[G][SDPA_MAX_BLOCKS];
-    __shared__ float stat_l[G];
-    __shared__ float pl[G][SDPA_KV_BLOCK + 16];
-    const int qi = blockIdx.x, kvh = blockIdx.y;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    T5G_TS(3);
-    const DecRow r = dec_row(a, qi);
-    if (r.span <= DCH) return;
     const int nch = (r.span + DCH - 1) / DCH;
     const int nblk = (r.span + SDPA_KV_BLOCK - 1) / SDPA_KV_BLOCK;
-    // this thread's output quad, and the partial P.V sums of the first two kv blocks
-    // requested now (unconditional clamped loads), so they land while l is computed
-    constexpr int QPB = (G * D / 4 + combine_cz<D, G>() - 1) / combine_cz<D, G>();
-    const int quad = (int)blockIdx.z * QPB + (int)threadIdx.x;
-    const bool mq = (int)threadIdx.x < QPB && quad < G * D / 4;
-    const int gq = mq ? quad / (D / 4) : 0, d4 = mq ? quad % (D / 4) : 0;
-    const float* base = a.part + ((long)qi * a.Hkv + kvh) * a.nsplit * (G * (D + 2)) + gq * (D + 2) + 2 + 4 * d4;
-    constexpr int NPRE = 2;
-    f32x4 pre[NPRE];
+    const int nsr = nblk * RPB;
+    const int cr = tid / TPC, slot = (tid % TPC) / NOCT, od = tid % NOCT;
+    // V slices of sub-rounds 0 and 1 and the scores of blocks 0 and 1 first (all loads
+    // unconditional; keys past the row read as zeros through the buffer range check)
+    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
+    const __amdgpu_buffer_rsrc_t vrs = frag_rsrc(Vb, (uint32_t)a.kv_cap * D * 2u);
+    auto vload = [&](u32x4 (&v)[NIT], int sr) {
+        const int c = (sr / RPB) * CPB + (sr % RPB) * CPR + cr;
 #pragma unroll
-    for (int b = 0; b < NPRE; ++b) {
-        pre[b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        const int ce = min(nch, (b + 1) * CPB);
-#pragma unroll
-        for (int k = 0; k < CPB; ++k) {
-            const int c = b * CPB + k;
-            const f32x4 v = *(const f32x4*)(base + (long)(c < ce ? c : 0) * G * (D + 2));
-            pre[b] += (c < ce) ? v : (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < NIT; ++i) {
+            const int j = r.lo + c * DCH + i * KPB + slot;
+            const int off = (sr < nsr && j < r.hi) ? (j * D + PVC_DZ * z + 8 * od) * 2 : (int)0x7ffffff0;
+            v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
         }
-    }
-    {   // wave g: l of head g with aten's lane-ordered block sums over the exact p values
-        // attn_pv_kernel left in sbuf, staged block by block in LDS; the serial adds run
-        // out of LDS
-        const int g = wave;
-        const float* mb = a.mbuf + ((long)qi * a.Hkv + kvh) * a.nsplit * G + g;
-        const float* pb = a.sbuf + ((long)qi * a.Hkv * G + kvh * G + g) * a.kv_cap + r.lo;
-        const float cmax = lane < nch ? mb[lane * G] : -INFINITY;   // chunk `lane`'s max
-        // block b's p in registers (8 per lane, coalesced); the next block's loads are
-        // issued before this block's serial adds
-        float pw[SDPA_KV_BLOCK / 64];
+    };
+    u32x4 vn[NIT];
+    vload(vn, 0);
+    const float* sb = a.sbuf + ((long)qi * a.Hkv * G + kvh * G) * a.kv_cap + r.lo;
+    auto sload = [&](float (&sc)[G][PPT], int b) {
 #pragma unroll
-        for (int k = 0; k < SDPA_KV_BLOCK / 64; ++k) {
-            const int pos = 64 * k + lane;
-            pw[k] = pos < r.span ? pb[pos] : 0.f;
-        }
-        if (lane < 16) pl[g][SDPA_KV_BLOCK + lane] = 0.f;
-        float m = -INFINITY, l = 0.f;
-        for (int b = 0; b < nblk; ++b) {
-            __builtin_amdgcn_wave_barrier();   // the previous block's LDS reads are done
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int k = 0; k < SDPA_KV_BLOCK / 64; ++k) pl[g][64 * k + lane] = pw[k];
-#pragma unroll
-            for (int k = 0; k < SDPA_KV_BLOCK / 64; ++k) {
-                const int pos = (b + 1) * SDPA_KV_BLOCK + 64 * k + lane;
-                pw[k] = pos < r.span ? pb[pos] : 0.f;
+            for (int k = 0; k < PPT; ++k) {
+                const int pos = b * SDPA_KV_BLOCK + tid + 256 * k;
+                sc[g][k] = sb[(long)g * a.kv_cap + (pos < r.span ? pos : 0)];
             }
-            __builtin_amdgcn_wave_barrier();
-            const float mn = fmaxf(m, wave_max(lane / CPB == b ? cmax : -INFINITY));
-            const int blen = min(SDPA_KV_BLOCK, r.span - b * SDPA_KV_BLOCK);
-            const float ts = sdpa_block_sum_lds<SDPA_KV_BLOCK>(pl[g], blen, lane);
-            const float et = sdpa_block_rescale(m, mn);
-            l = fmaf(et, l, ts);
-            if (lane == 0) blk_et[g][b] = et;
-            m = mn;
+    };
+    float scn[G][PPT];
+    sload(scn, 0);
+    if (wave < G) {   // running maxima through each block, from the chunk maxima
+        const int g = wave;
+        const float cm = lane < nch ? a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + lane) * G + g] : -INFINITY;
+        for (int b = 0; b < nblk; ++b) {
+            const float mb = wave_max(lane < min(nch, (b + 1) * CPB) ? cm : -INFINITY);
+            if (lane == 0) mrun[g][b] = mb;
         }
-        if (lane == 0) stat_l[g] = l;
+        if (lane < 16) pex[g][SDPA_KV_BLOCK + lane] = 0.f;
     }
     __syncthreads();
-    if (!mq) return;
-    const int g = gq;
-    f32x4 dst = {0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < nblk; ++b) {
-        f32x4 blk = {0.f, 0.f, 0.f, 0.f};
-        if (b < NPRE) {
-            blk = b == 0 ? pre[0] : pre[1];
-        } else {
-            const int ce = min(nch, (b + 1) * CPB);
+    float l = 0.f, m_old = -INFINITY;            // wave g < G: head g's running sum
+    float dst = 0.f, blk = 0.f;                  // fold thread (g, dd)
+    const bool folder = tid < G * PVC_DZ;
+    const int fg = tid / PVC_DZ, fdd = tid % PVC_DZ;
+    auto stage = [&](const float (&sc)[G][PPT], int b) {   // exact p of block b -> LDS
+        const int blen = min(SDPA_KV_BLOCK, r.span - b * SDPA_KV_BLOCK);
 #pragma unroll
-            for (int k = 0; k < CPB; ++k) {   // predicated, not a loop-carried wait per chunk
-                const int c = b * CPB + k;
-                if (c < ce) blk += *(const f32x4*)(base + (long)c * G * (D + 2));
+        for (int g = 0; g < G; ++g) {
+            const float mb = mrun[g][b];
+#pragma unroll
+            for (int k = 0; k < PPT; ++k) {
+                const int pos = tid + 256 * k;
+                const float p = pos < blen ? sdpa_p(__fsub_rn(sc[g][k], mb), pos, blen) : 0.f;
+                pex[g][pos] = p;
+                pbf[g][pos] = rbf(p);
             }
         }
-        dst = dst * blk_et[g][b] + blk;
+        __syncthreads();
+        if (wave < G) {
+            const int g = wave;
+            const float ts = sdpa_block_sum_lds<SDPA_KV_BLOCK>(pex[g], blen, lane);
+            const float mb = mrun[g][b];
+            const float et = sdpa_block_rescale(m_old, mb);
+            l = fmaf(et, l, ts);
+            m_old = mb;
+            if (lane == 0) et_s[g] = et;
+        }
+    };
+    auto subround = [&](const u32x4 (&v)[NIT], int sr) {
+        const int b = sr / RPB, rr = sr % RPB;
+        const int jb = (rr * CPR + cr) * DCH;   // chunk start within the block
+        float o[G][8];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int jl = jb + i * KPB + slot;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float p = pbf[g][jl];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    o[g][2 * jj] += p * bf_lo(v[i][jj]);
+                    o[g][2 * jj + 1] += p * bf_hi(v[i][jj]);
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) ol[cr][slot][g][8 * od + jj] = o[g][jj];
+        __syncthreads();
+        if (folder) {
+            if (rr == 0) blk = 0.f;
+#pragma unroll
+            for (int c = 0; c < CPR; ++c) {
+                float w4[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    float t[KPW];
+#pragma unroll
+                    for (int k = 0; k < KPW; ++k) t[k] = ol[c][w * KPW + k][fg][fdd];
+#pragma unroll
+                    for (int st = 1; st < KPW; st <<= 1)
+#pragma unroll
+                        for (int k = 0; k < KPW; k += 2 * st) t[k] = t[k] + t[k + st];
+                    w4[w] = t[0];
+                }
+                const float pc = ((w4[0] + w4[1]) + w4[2]) + w4[3];
+                if (b * CPB + rr * CPR + c < nch) blk += pc;
+            }
+            if (rr == RPB - 1) dst = dst * et_s[fg] + blk;
+        }
+        __syncthreads();   // ol / pbf / et_s are rewritten by the next sub-round
+    };
+    // one sub-round per iteration; the next sub-round's V slice (and at a block start
+    // the next block's scores) are requested before this one is computed
+    for (int sr = 0; sr < nsr; ++sr) {
+        if (sr % RPB == 0) {
+            const int b = sr / RPB;
+            float sc[G][PPT];
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < PPT; ++k) sc[g][k] = scn[g][k];
+            sload(scn, b + 1 < nblk ? b + 1 : b);
+            stage(sc, b);
+        }
+        u32x4 v[NIT];
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) v[i] = vn[i];
+        vload(vn, sr + 1);
+        subround(v, sr);
     }
-    const float inv = __fdiv_rn(1.0f, stat_l[g]);
-    uint2 o;
-    o.x = pack2(__fmul_rn(dst[0], inv), __fmul_rn(dst[1], inv));
-    o.y = pack2(__fmul_rn(dst[2], inv), __fmul_rn(dst[3], inv));
-    *(uint2*)(a.O + (long)qi * a.ldo + (kvh * G + g) * D + 4 * d4) = o;
-    T5G_TS(6);
+    if (wave < G && lane == 0) stat_l[wave] = l;
+    __syncthreads();
+    T5G_TS(1);
+    if (!folder) return;
+    const float inv = __fdiv_rn(1.0f, stat_l[fg]);
+    a.O[(long)qi * a.ldo + (kvh * G + fg) * D + PVC_DZ * z + fdd] = f2bf(__fmul_rn(dst, inv));
 }
 
 template <int D, int G>
 static int launch_decode(const AttnArgs& a, hipStream_t st) {
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
     hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, a);
-    if (a.nsplit > 1) {
-        hipLaunchKernelGGL((attn_pv_kernel<D, G>), grid, dim3(256), 0, st, a);
-        hipLaunchKernelGGL((attn_combine_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, combine_cz<D, G>()),
-                           dim3(64 * G), 0, st, a);
-    }
+    if (a.nsplit > 1)
+        hipLaunchKernelGGL((attn_pvc_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(D / PVC_DZ)),
+                           dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int attention_decode(const AttnArgs& a, hipStream_t st) {
     if (a.Mq <= 0) return 0;
-    if (a.eager || !a.part || a.kv_cap <= 0 || a.kv_cap > SDPA_KV_BLOCK * SDPA_MAX_BLOCKS) return -1;
+    if (a.eager || a.kv_cap <= 0 || a.kv_cap > SDPA_KV_BLOCK * SDPA_MAX_BLOCKS) return -1;
     if (a.nsplit != (a.kv_cap + DCH - 1) / DCH) return -1;   // 64-key chunks from the row start
     if (a.nsplit > 1 && (!a.sbuf || !a.mbuf || a.nsplit > 64)) return -1;
     if (a.append && (!a.Qpart || !a.rope_tab || (a.G + 2) * a.D / 4 > 256)) return -1;

@@ -44,8 +44,7 @@ struct t5g_engine {
     // packed-token activations (encode / prefill)
     bf16_t *h, *xn, *qkv, *q, *att, *act, *tmp, *mem;
     float* part;          // split-K slabs (max over uses)
-    float* apart;         // decode attention partial P.V slabs
-    int64_t part_elems, apart_elems;
+    int64_t part_elems;
     bf16_t *enc_k, *enc_v;                 // encoder self K/V [B][Hkv][max_text][D]
     std::vector<bf16_t*> ck, cv, sk, sv;   // per decoder layer cross / self caches
     int* enc_len;                          // [B] text lengths
@@ -161,8 +160,6 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     const int nsplit_dec = (c.max_audio + 63) / 64, nsplit_x = (c.max_text + 63) / 64;
     const int nsplit_max = nsplit_dec > nsplit_x ? nsplit_dec : nsplit_x;
     const int cap_max = c.max_audio > c.max_text ? c.max_audio : c.max_text;
-    e->apart_elems = (int64_t)B * Hkv * nsplit_max * G * (D + 2);
-    rc |= alloc(e, &e->apart, e->apart_elems);
     rc |= alloc(e, &e->asbuf, (int64_t)B * c.n_heads * cap_max);
     rc |= alloc(e, &e->ambuf, (int64_t)B * Hkv * nsplit_max * G);
     const int64_t enc_cache = (int64_t)B * Hkv * c.max_text * D;
@@ -405,7 +402,6 @@ static int decode_attention(t5g_engine* e, int M, const bf16_t* K, const bf16_t*
     a.chunk = 64;
     a.nsplit = (cap + 63) / 64;
     a.kv_cap = cap;
-    a.part = e->apart;
     a.sbuf = e->asbuf;
     a.mbuf = e->ambuf;
     a.Qpart = e->part + q_col0;   // q columns of the projection's fp32 split-K slabs
@@ -833,19 +829,18 @@ extern "C" int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, 
     return T5G_OK;
 }
 
-// work = partial P.V slabs | scores | chunk maxima (fp32)
-static void attn_work_layout(int B, int Hq, int Hkv, int D, int cap, int64_t* part, int64_t* sc, int64_t* mx) {
+// work = scores | chunk maxima (fp32)
+static void attn_work_layout(int B, int Hq, int Hkv, int cap, int64_t* sc, int64_t* mx) {
     const int64_t nsplit = (cap + 63) / 64;
-    *part = (int64_t)B * Hkv * nsplit * (Hq / Hkv) * (D + 2);
     *sc = (int64_t)B * Hq * cap;
     *mx = (int64_t)B * Hkv * nsplit * (Hq / Hkv);
 }
 
 extern "C" int64_t t5g_attention_decode_work_bytes(int32_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t cap) {
     if (B <= 0 || Hkv <= 0 || Hq % Hkv || D <= 0 || cap <= 0) return -1;
-    int64_t p, s, m;
-    attn_work_layout(B, Hq, Hkv, D, cap, &p, &s, &m);
-    return (p + s + m) * 4;
+    int64_t s, m;
+    attn_work_layout(B, Hq, Hkv, cap, &s, &m);
+    return (s + m) * 4;
 }
 
 extern "C" int t5g_attention_decode(const t5g_attn_decode_args* g, void* stream) {
@@ -873,10 +868,9 @@ extern "C" int t5g_attention_decode(const t5g_attn_decode_args* g, void* stream)
     a.chunk = 64;
     a.nsplit = (g->cap + 63) / 64;
     a.kv_cap = g->cap;
-    int64_t np, ns, nm;
-    attn_work_layout(g->B, g->n_heads, g->n_kv_heads, g->head_dim, g->cap, &np, &ns, &nm);
-    a.part = (float*)g->work;
-    a.sbuf = a.part + np;
+    int64_t ns, nm;
+    attn_work_layout(g->B, g->n_heads, g->n_kv_heads, g->cap, &ns, &nm);
+    a.sbuf = (float*)g->work;
     a.mbuf = a.sbuf + ns;
     RC(attention_decode(a, (hipStream_t)stream));
     return T5G_OK;

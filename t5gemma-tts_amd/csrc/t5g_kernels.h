@@ -107,7 +107,6 @@ struct AttnArgs {
     float scale, softcap;
     int eager;               // eager numerics (bf16 scores, normalised bf16 probs)
     int nsplit, chunk;       // decode: 64-key chunks (nsplit = ceil(kv_cap / 64)); packed: 1, chunk = Lmax
-    float* part;             // decode partial P.V slabs [Mq][Hkv][nsplit][G][D + 2]
     bf16_t* O;               // [Mq][ldo]
     int ldo;
     // decode extras: q straight from the projection's fp32 split-K slabs, PM-RoPE'd in-kernel
@@ -125,7 +124,7 @@ struct AttnArgs {
     int dbg_seq;             // diagnostic timeline slot (T5G_DBG_TS builds only)
 };
 int attention(const AttnArgs& a, hipStream_t st);
-// decode-shaped (64-key chunks over blockIdx.z + P.V / combine launches, sdpa numerics)
+// decode-shaped (64-key chunks over blockIdx.z + one P.V / combine launch, sdpa numerics)
 int attention_decode(const AttnArgs& a, hipStream_t st);
 
 // ---- sampler -------------------------------------------------------------------
