@@ -30,6 +30,8 @@ using namespace t5g;
         if (_rc) return _rc == -1 ? T5G_EINVAL : (_rc == -3 ? T5G_EUNSUPPORTED : T5G_EHIP); \
     } while (0)
 
+constexpr int GRAPH_STEPS = 8;   // decode iterations per multi-step graph
+
 static inline int ng_pad(int N) { return ((N + 15) / 16 + 3) / 4 * 4; }
 
 struct t5g_engine {
@@ -80,9 +82,10 @@ struct t5g_engine {
     int B = 0;            // rows of the current call
     const bf16_t* noise = nullptr;
     int noise_steps = 0;
-    // graph
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t gexec = nullptr;
+    // graphs of one and of GRAPH_STEPS decode iterations (a replay boundary costs
+    // ~10 us; back-to-back iterations inside one graph only the kernel boundaries)
+    hipGraph_t graph = nullptr, graph_n = nullptr;
+    hipGraphExec_t gexec = nullptr, gexec_n = nullptr;
     int graph_B = -1;
     hipStream_t graph_stream = nullptr;
     hipStream_t cap_stream = nullptr;
@@ -111,10 +114,18 @@ extern "C" int t5g_pack_weight(const void* src, int32_t N, int32_t K, int64_t ld
     return T5G_OK;
 }
 
+static void drop_graphs(t5g_engine* e) {
+    if (e->gexec) hipGraphExecDestroy(e->gexec);
+    if (e->gexec_n) hipGraphExecDestroy(e->gexec_n);
+    if (e->graph) hipGraphDestroy(e->graph);
+    if (e->graph_n) hipGraphDestroy(e->graph_n);
+    e->gexec = e->gexec_n = nullptr;
+    e->graph = e->graph_n = nullptr;
+}
+
 extern "C" int t5g_engine_destroy(t5g_engine* e) {
     if (!e) return T5G_OK;
-    if (e->gexec) hipGraphExecDestroy(e->gexec);
-    if (e->graph) hipGraphDestroy(e->graph);
+    drop_graphs(e);
     if (e->cap_stream) hipStreamDestroy(e->cap_stream);
     for (void* p : e->allocs) hipFree(p);
     delete e;
@@ -614,15 +625,8 @@ extern "C" int t5g_sampler_setup(t5g_engine* e, int32_t B, const t5g_sampler_row
     if (n_silence > 0)
         HIPCHK(hipMemcpyAsync(e->silence, silence, n_silence * sizeof(int), hipMemcpyHostToDevice, st));
     if (e->noise != (const bf16_t*)noise || e->noise_steps != noise_steps) {
-        // noise pointer is baked into the captured graph
-        if (e->gexec) {
-            hipGraphExecDestroy(e->gexec);
-            e->gexec = nullptr;
-        }
-        if (e->graph) {
-            hipGraphDestroy(e->graph);
-            e->graph = nullptr;
-        }
+        // noise pointer is baked into the captured graphs
+        drop_graphs(e);
     }
     e->noise = (const bf16_t*)noise;
     e->noise_steps = noise_steps;
@@ -682,25 +686,33 @@ extern "C" int t5g_decode(t5g_engine* e, int32_t n_steps, int32_t use_graph, voi
         return T5G_OK;
     }
     if (!e->gexec || e->graph_B != e->B) {
-        if (e->gexec) hipGraphExecDestroy(e->gexec);
-        if (e->graph) hipGraphDestroy(e->graph);
-        e->gexec = nullptr;
-        e->graph = nullptr;
+        drop_graphs(e);
         if (!e->cap_stream) HIPCHK(hipStreamCreateWithFlags(&e->cap_stream, hipStreamNonBlocking));
-        HIPCHK(hipStreamBeginCapture(e->cap_stream, hipStreamCaptureModeThreadLocal));
-        int rc = decode_iter(e, e->cap_stream);
-        hipGraph_t g = nullptr;
-        hipError_t ec = hipStreamEndCapture(e->cap_stream, &g);
-        if (rc) {
-            if (g) hipGraphDestroy(g);
-            return rc;
+        for (int which = 0; which < 2; ++which) {
+            HIPCHK(hipStreamBeginCapture(e->cap_stream, hipStreamCaptureModeThreadLocal));
+            int rc = T5G_OK;
+            for (int i = 0; i < (which ? GRAPH_STEPS : 1) && !rc; ++i) rc = decode_iter(e, e->cap_stream);
+            hipGraph_t g = nullptr;
+            hipError_t ec = hipStreamEndCapture(e->cap_stream, &g);
+            if (rc || ec != hipSuccess) {
+                if (g) hipGraphDestroy(g);
+                drop_graphs(e);
+                return rc ? rc : T5G_EHIP;
+            }
+            hipGraphExec_t x = nullptr;
+            if (hipGraphInstantiate(&x, g, nullptr, nullptr, 0) != hipSuccess) {
+                hipGraphDestroy(g);
+                drop_graphs(e);
+                return T5G_EHIP;
+            }
+            (which ? e->graph_n : e->graph) = g;
+            (which ? e->gexec_n : e->gexec) = x;
         }
-        if (ec != hipSuccess) return T5G_EHIP;
-        e->graph = g;
-        HIPCHK(hipGraphInstantiate(&e->gexec, g, nullptr, nullptr, 0));
         e->graph_B = e->B;
     }
-    for (int i = 0; i < n_steps; ++i) HIPCHK(hipGraphLaunch(e->gexec, st));
+    int i = 0;
+    for (; i + GRAPH_STEPS <= n_steps; i += GRAPH_STEPS) HIPCHK(hipGraphLaunch(e->gexec_n, st));
+    for (; i < n_steps; ++i) HIPCHK(hipGraphLaunch(e->gexec, st));
     return T5G_OK;
 }
 

@@ -1,4 +1,4 @@
-# Merged P.V + combine attention launch: every GPU test, smoke, C3 bench, step timeline.
+# Decode changes: every GPU test, smoke, C3 bench, step timeline.
 source tools/gpu_run.sh
 export TMPDIR=/tmp
 rm -rf gpurun_out/prof
