@@ -608,16 +608,15 @@ __device__ __forceinline__ DecRow dec_row(const AttnArgs& a, int qi) {
 // of the row, so nothing is handed between workgroups: it recomputes the exact p of each
 // aten 512-key block from the published scores and chunk maxima (cheap: <= 2 x 4096
 // exps), takes l from aten's lane-ordered block sums of them, and streams only its
-// PVC_DZ-wide slice of V (64 B per key at D = 256, all 8 slices of a row on one XCD
-// under round-robin placement, so a 128-B line is fetched once).
+// DZ-wide slice of V (DZ = 32: 64 B per key at D = 256, all 8 slices of a row on one XCD
+// under round-robin placement, so a 128-B line is fetched once; DZ = 64 when 32-wide
+// slices would need more than two workgroups per CU, e.g. 32 rows).
 // The fp32 sums keep the order of the former per-chunk P.V + combine pair, so results are
 // bit-identical to it: per 64-key chunk, KPB key slots (slot = wave * KPW + kg of the
 // chunk kernel's lane map) each accumulate NIT keys j = c0 + i * KPB + slot in i order;
 // the KPW slots of a wave fold as a pairwise (xor-butterfly) tree, the 4 waves in order;
 // the chunks of a block are summed in order from 0; dst = dst * exp(m_old - m) + block.
-constexpr int PVC_DZ = 32;   // output dimensions per workgroup
-
-template <int D, int G>
+template <int D, int G, int PVC_DZ>   // PVC_DZ: output dimensions per workgroup
 __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
     constexpr int LPK = D / 8;
     constexpr int KPW = 64 / LPK;
@@ -790,9 +789,15 @@ template <int D, int G>
 static int launch_decode(const AttnArgs& a, hipStream_t st) {
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
     hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, a);
-    if (a.nsplit > 1)
-        hipLaunchKernelGGL((attn_pvc_kernel<D, G>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(D / PVC_DZ)),
-                           dim3(256), 0, st, a);
+    if (a.nsplit > 1) {
+        // one round of workgroups: 32-wide slices while they fit two per CU, else 64-wide
+        if (D >= 64 && (long)a.Mq * a.Hkv * (D / 32) > 512)
+            hipLaunchKernelGGL((attn_pvc_kernel<D, G, 64>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(D / 64)),
+                               dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL((attn_pvc_kernel<D, G, 32>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(D / 32)),
+                               dim3(256), 0, st, a);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -446,6 +446,136 @@ static int gemm_prefill(const GemmArgs& a, int epi, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// Decode GEMM whose block stages the X rows of its K slice in LDS once and shares them
+// among RG row groups (4 waves each: the 4 k-slices of the KS = 4 order, every slice
+// chained in k order and the slices summed in order, so outputs are bitwise those of
+// gemm_p16_kernel<MT, 4, 4, EPI, *>). At M = 32 the X fragments are two of every three
+// 16-byte loads of the fragment-per-MFMA kernel; here they are read from LDS.
+constexpr int DX_XCH = 18;   // X staging chunks per thread
+template <int MT, int RG, int EPI>
+__global__ __launch_bounds__(256 * RG) void gemm_dx_kernel(GemmArgs a) {
+    constexpr int KS = 4, UN = 8, STEP = UN * KS, XCH = (DX_XCH + RG - 1) / RG;
+    extern __shared__ bf16_t xs[];
+    __shared__ f32x4 red[RG * 4][MT][64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int rgl = wave >> 2, ks = wave & 3;
+    const int g = blockIdx.x * RG + rgl;
+    const int per = (a.KB + a.splits - 1) / a.splits;
+    const int kb_lo = blockIdx.y * per;
+    const int kb_hi = min(a.KB, kb_lo + per);
+    const int rows = min(16 * MT, a.M);
+    const int kspan = max(0, kb_hi - kb_lo);
+    const int ldsx = kspan * 32 + 8;
+    int kb = kb_lo + ks;
+    const __amdgpu_buffer_rsrc_t wr = frag_rsrc(a.W + (long)g * a.KB * 512, (uint32_t)max(kb_hi, 0) * 1024u);
+    bf16x8_s wcur[UN];
+    {
+        // every X chunk of the thread first, then the first weight group (vmcnt retires
+        // in issue order: the LDS writes wait for the X rows only)
+        const int total = rows * kspan * 4;
+        const __amdgpu_buffer_rsrc_t xrs = frag_rsrc(a.X, (uint32_t)rows * a.ldx * 2u);
+        bf16x8_s xv[XCH];
+#pragma unroll
+        for (int i = 0; i < XCH; ++i) {
+            const int idx = threadIdx.x + 256 * RG * i;
+            const int r = idx / max(1, kspan * 4), c = idx - r * (kspan * 4);
+            const int off = idx < total ? (r * a.ldx + kb_lo * 32 + 8 * c) * 2 : 0x7ffffff0;
+            xv[i] = __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+        }
+#pragma unroll
+        for (int u = 0; u < UN; ++u) wcur[u] = frag_load(wr, kb + u * KS, lane);
+#pragma unroll
+        for (int i = 0; i < XCH; ++i) {
+            const int idx = threadIdx.x + 256 * RG * i;
+            const int r = idx / max(1, kspan * 4), c = idx - r * (kspan * 4);
+            if (idx < total) *(bf16x8_s*)(xs + r * ldsx + 8 * c) = xv[i];
+        }
+    }
+    __syncthreads();
+    const int xr = lane & 15;
+    f32x4 acc[MT];
+    const bf16_t* xrow[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        xrow[mt] = xs + min(16 * mt + xr, rows - 1) * ldsx + 8 * (lane >> 4) - kb_lo * 32;
+    }
+    for (; kb < kb_hi; kb += STEP) {
+        bf16x8_s wnext[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) wnext[u] = frag_load(wr, kb + STEP + u * KS, lane);
+#pragma unroll
+        for (int u = 0; u < UN; ++u)
+            if (kb + u * KS < kb_hi) {   // uniform
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    const bf16x8_s xv = *(const bf16x8_s*)(xrow[mt] + (kb + u * KS) * 32);
+                    const bf16x8_s xf = 16 * mt + xr < rows ? xv : (bf16x8_s){0, 0, 0, 0, 0, 0, 0, 0};
+                    acc[mt] = mfma16(wcur[u], xf, acc[mt]);
+                }
+            }
+#pragma unroll
+        for (int u = 0; u < UN; ++u) wcur[u] = wnext[u];
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[mt];
+    __syncthreads();
+    if (ks != 0) return;
+    const int n_out = a.N;
+    const int n0 = g * 16 + 4 * (lane >> 4);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + xr;
+        if (m >= a.M) continue;
+        f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) s4 += red[rgl * KS + s][mt][lane];
+        if constexpr (EPI == EPI_F32) {
+            float* y = (float*)a.Y + ((long)blockIdx.y * a.M + m) * a.ldy;
+            if (n0 + 3 < n_out) {
+                *(f32x4*)(y + n0) = s4;
+            } else {
+                for (int r = 0; r < 4; ++r)
+                    if (n0 + r < n_out) y[n0 + r] = s4[r];
+            }
+        } else {
+            bf16_t* y = (bf16_t*)a.Y + (long)m * a.ldy;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n0 + r;
+                if (n >= n_out) continue;
+                float x = s4[r];
+                if constexpr (EPI == EPI_BIAS_BF16 || EPI == EPI_BIAS_GELU) x = x + bf2f(a.bias[n]);
+                if constexpr (EPI == EPI_BIAS_GELU) x = gelu_erf(rbf(x));
+                y[n] = f2bf(x);
+            }
+        }
+    }
+}
+
+// 1: launched, 0: not eligible. Measured (tools/probe_dx.py, profiles/r02_probe_dx.jsonl):
+// at M = 17..32 sharing the staged X between 2 row groups makes the split-K projections
+// with K = 2304 faster (qkv 8.97 -> 7.19 us, cross-q 5.52 -> 5.17); at M <= 16, for the
+// o projections (16 k-steps per slice) and for down it is slower or equal.
+static int try_dx(const GemmArgs& a, int epi, hipStream_t st, int* rc) {
+    constexpr int RG = 2;
+    if (epi != EPI_F32 || a.M <= 16 || a.M > 32 || a.KB * 32 > 2304 || a.splits < 2) return 0;
+    const int per = (a.KB + a.splits - 1) / a.splits;
+    if (per < 18 || a.M * per * 4 > 256 * RG * ((DX_XCH + RG - 1) / RG) || a.NG % RG) return 0;
+    const size_t shm = (size_t)a.M * (per * 32 + 8) * sizeof(bf16_t);
+    auto* fn = gemm_dx_kernel<2, RG, EPI_F32>;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) != hipSuccess)
+            return 0;
+        attr = true;
+    }
+    if (shm > 96 * 1024) return 0;
+    hipLaunchKernelGGL(fn, dim3((unsigned)(a.NG / RG), (unsigned)a.splits), dim3(256 * RG), shm, st, a);
+    *rc = 0;
+    return 1;
+}
+
 // Dispatch: decode-shaped (M <= 64) streams weights with K split over the
 // block's 4 waves (GEGLU: 2 waves per gate/up group); larger M uses 4 row groups
 // per block sharing X fragments.
@@ -458,7 +588,9 @@ int gemm_p16(const GemmArgs& a_in, int epi, hipStream_t st) {
     // many-token phases (encoder, decoder prefill): the register-tiled MFMA kernel
     if (a.prefill && epi != EPI_F32) return gemm_prefill(a, epi, st);
     int rc;
-    if (a.M <= 16) {
+    if (try_dx(a, epi, st, &rc)) {
+        if (rc) return rc;
+    } else if (a.M <= 16) {
         rc = launch_epi<1, false>(a, epi, 1, st);
     } else if (a.M <= 32) {
         rc = launch_epi<2, false>(a, epi, 1, st);

@@ -387,6 +387,7 @@ int gemv_rx(const DecGemmArgs& a, int epi, hipStream_t st) {
     switch (epi) {
         case EPI_BF16: return two ? launch_rx<2, EPI_BF16>(a, st) : launch_rx<1, EPI_BF16>(a, st);
         case EPI_BIAS_BF16: return two ? launch_rx<2, EPI_BIAS_BF16>(a, st) : launch_rx<1, EPI_BIAS_BF16>(a, st);
+        case EPI_BIAS_GELU: return two ? launch_rx<2, EPI_BIAS_GELU>(a, st) : launch_rx<1, EPI_BIAS_GELU>(a, st);
         case EPI_GEGLU: return two ? launch_rx<2, EPI_GEGLU>(a, st) : launch_rx<1, EPI_GEGLU>(a, st);
         default: return -1;
     }

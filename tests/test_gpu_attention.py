@@ -88,6 +88,21 @@ def test_self_attention_decode_vs_cpu_sdpa(L):
     assert (got - exact).abs().max().item() <= 2.0 ** -6 * max(1.0, exact.abs().max().item())
 
 
+def test_self_attention_decode_batch32():
+    """32 rows (the C5 batch): the P.V / combine launch takes 64-dimension slices (one
+    round of workgroups); the same CPU-SDPA bit-equality as at 8 rows."""
+    _need_gpu()
+    B, L = 32, 527
+    lens = [max(1, L - 17 * i) for i in range(B)]
+    got, q, K, V = _run(L, B, lens, seed=32)
+    ref = _reference(q, K, V, lens, 256 ** -0.5, True)
+    same = (got == ref).float().mean().item()
+    ulp = torch.exp2(torch.floor(torch.log2(ref.abs().clamp(min=2.0 ** -60))) - 7)
+    within1 = ((got - ref).abs() <= ulp * 1.01).float().mean().item()
+    print(f"B=32 L<={L}: bit-equal to CPU SDPA {same:.5f}, within 1 ulp {within1:.5f}")
+    assert same >= 0.998 and within1 >= 0.9999, (same, within1)
+
+
 def test_cross_attention_decode_tx60():
     """PMCrossAttention shape: T_x = 60 encoder keys (non-causal), 8 rows, ragged text."""
     _need_gpu()

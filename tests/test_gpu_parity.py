@@ -36,6 +36,8 @@ PREFILL = 0x100   # include/t5gtts.h T5G_GEMM_PREFILL: the encoder / prefill ker
 
 @pytest.mark.parametrize("M,N,K,epi,splits", [
     (1, 4096, 2304, 0, 1), (8, 4096, 2304, 0, 1), (8, 2304, 2048, 4, 4), (16, 2304, 9216, 4, 8),
+    # 17..32 rows, K = 2304 k-sliced: X staged in LDS and shared by 2 row groups (gemm_dx_kernel)
+    (32, 4096, 2304, 4, 2), (20, 2048, 2304, 4, 4), (32, 2304, 9216, 4, 8),
     (8, 18432, 2304, 3, 1), (8, 2304, 2304, 2, 1), (8, 65541, 2304, 1, 1), (40, 4096, 2304, 0, 1),
     (200, 2304, 2048, 0, 1), (300, 18432, 2304, 3, 1), (5, 300, 128, 0, 1),
     # many-token kernel: encoder (B*T_x) / prefill (B*(T_p+1)) shapes, ragged tails, tiny widths
@@ -103,6 +105,30 @@ def test_gemm_p16_vs_fp32(M, N, K, epi, splits):
         bad = diff > ulp * k * 1.01 + floor32 + 1e-7
         assert not bad.any(), (int(bad.sum()), diff[bad].max(), ref[bad][:4], got[bad][:4])
     assert (diff == 0).float().mean() > 0.97
+
+
+def test_gemm_decode_rows_bitwise_across_kernels():
+    """The 17..32-row decode GEMM (X staged in LDS, gemm_dx_kernel) keeps the k-slice order
+    of the 1..16-row kernel: rows 0..7 of a 32-row launch equal an 8-row launch bitwise."""
+    _need_gpu()
+    import ctypes as C
+    from t5gemma_tts_amd import _lib
+    L = _lib.lib()
+    for N, K, splits in ((4096, 2304, 2), (2048, 2304, 4)):
+        g = torch.Generator(device="cpu").manual_seed(N + splits)
+        X = torch.randn(32, K, generator=g).to(BF16).cuda()
+        W = (torch.randn(N, K, generator=g) * 0.02).to(BF16).cuda()
+        st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        Wp = torch.empty(L.t5g_packed_bytes(N, K) // 2, dtype=BF16, device="cuda")
+        assert L.t5g_pack_weight(C.c_void_p(W.data_ptr()), N, K, K, C.c_void_p(Wp.data_ptr()), st) == 0
+        outs = []
+        for M in (32, 8):
+            Y = torch.zeros(splits, M, N, dtype=torch.float32, device="cuda")
+            assert L.t5g_gemm(C.c_void_p(X.data_ptr()), K, M, C.c_void_p(Wp.data_ptr()), N, K, splits, None,
+                              C.c_void_p(Y.data_ptr()), N, 4, st) == 0
+            outs.append(Y)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0][:, :8], outs[1])
 
 
 def test_gemm_prefill_batch_invariant():
