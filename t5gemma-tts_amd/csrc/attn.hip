@@ -181,8 +181,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-#pragma unroll
-            for (int o = LPK / 2; o > 0; o >>= 1) s[g] += __shfl_xor(s[g], o, 64);
+            s[g] = xsum<LPK>(s[g]);
         }
         if (dl == 0 && j < hi) {
 #pragma unroll
@@ -499,8 +498,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         }
 #pragma unroll
         for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int o = LPK / 2; o > 0; o >>= 1) s[g] += __shfl_xor(s[g], o, 64);
+            s[g] = xsum<LPK>(s[g]);
         const int jl = i * KPB + wave * KPW + kg;
         if (dl == 0) {
 #pragma unroll

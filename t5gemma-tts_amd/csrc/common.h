@@ -57,11 +57,42 @@ __device__ __forceinline__ T ld_sc1(const T* p) {
     return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The value of lane (lane ^ O) for a 32-bit v: the same partner as __shfl_xor(v, O, 64),
+// so butterflies built on it add the same pairs in the same order (bit-identical sums),
+// but on cheaper paths than ds_bpermute: quad_perm DPP for 1 / 2, row_ror:8 DPP for 8,
+// ds_swizzle bit-mode (xor within 32 lanes) for 4 / 16; 32 stays a ds_bpermute.
+template <int O>
+__device__ __forceinline__ float xlane(float v) {
+    static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16 || O == 32, "xor partner");
+    if constexpr (O == 1) return __builtin_amdgcn_update_dpp(0.f, v, 0xB1, 0xf, 0xf, false);
+    else if constexpr (O == 2) return __builtin_amdgcn_update_dpp(0.f, v, 0x4E, 0xf, 0xf, false);
+    else if constexpr (O == 8) return __builtin_amdgcn_update_dpp(0.f, v, 0x128, 0xf, 0xf, false);
+    else if constexpr (O == 4 || O == 16)
+        return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1f | (O << 10)));
+    else return __shfl_xor(v, 32, 64);
+}
+// butterfly sum over the lanes l ^ {HI/2 ... 1} (HI = a power of two <= 64), largest
+// stride first, as `for (o = HI/2; o > 0; o >>= 1) v += __shfl_xor(v, o)`
+template <int HI>
+__device__ __forceinline__ float xsum(float v) {
+    if constexpr (HI >= 64) v += xlane<32>(v);
+    if constexpr (HI >= 32) v += xlane<16>(v);
+    if constexpr (HI >= 16) v += xlane<8>(v);
+    if constexpr (HI >= 8) v += xlane<4>(v);
+    if constexpr (HI >= 4) v += xlane<2>(v);
+    if constexpr (HI >= 2) v += xlane<1>(v);
+    return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
+    if constexpr (sizeof(T) == 4 && __is_same(T, float)) {
+        return xsum<64>(v);
+    } else {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        return v;
+    }
 }
 // wave64 sum on the DPP network (4 in-row steps, no LDS) + 2 cross-row shuffles; fixed
 // order, every lane ends with the total
@@ -79,8 +110,12 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
     return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    v = fmaxf(v, xlane<32>(v));
+    v = fmaxf(v, xlane<16>(v));
+    v = fmaxf(v, xlane<8>(v));
+    v = fmaxf(v, xlane<4>(v));
+    v = fmaxf(v, xlane<2>(v));
+    v = fmaxf(v, xlane<1>(v));
     return v;
 }
 
@@ -143,10 +178,10 @@ __device__ __forceinline__ float sdpa_block_sum(int blen, int lane, P p) {
     float acc = 0.f;
     if (lane < 16)
         for (int i = lane; i < n16; i += 16) acc = __fadd_rn(acc, p(i));
-    acc = __fadd_rn(acc, __shfl_xor(acc, 8, 64));
-    acc = __fadd_rn(acc, __shfl_xor(acc, 4, 64));
-    acc = __fadd_rn(acc, __shfl_xor(acc, 2, 64));
-    acc = __fadd_rn(acc, __shfl_xor(acc, 1, 64));
+    acc = __fadd_rn(acc, xlane<8>(acc));
+    acc = __fadd_rn(acc, xlane<4>(acc));
+    acc = __fadd_rn(acc, xlane<2>(acc));
+    acc = __fadd_rn(acc, xlane<1>(acc));
     float s = __shfl(acc, 0, 64);
     for (int i = n16; i < blen; ++i) s = __fadd_rn(s, p(i));
     return s;
@@ -166,10 +201,10 @@ __device__ __forceinline__ float sdpa_block_sum_lds(const float* pl, int blen, i
         const int i = l16 + 16 * k;
         acc = __fadd_rn(acc, i < n16 ? pl[i] : 0.f);
     }
-    acc = __fadd_rn(acc, __shfl_xor(acc, 8, 64));
-    acc = __fadd_rn(acc, __shfl_xor(acc, 4, 64));
-    acc = __fadd_rn(acc, __shfl_xor(acc, 2, 64));
-    acc = __fadd_rn(acc, __shfl_xor(acc, 1, 64));
+    acc = __fadd_rn(acc, xlane<8>(acc));
+    acc = __fadd_rn(acc, xlane<4>(acc));
+    acc = __fadd_rn(acc, xlane<2>(acc));
+    acc = __fadd_rn(acc, xlane<1>(acc));
     float s = __shfl(acc, 0, 64);
 #pragma unroll
     for (int k = 0; k < 15; ++k) {
