@@ -71,6 +71,28 @@ __device__ __forceinline__ float xlane(float v) {
         return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1f | (O << 10)));
     else return __shfl_xor(v, 32, 64);
 }
+template <int O>
+__device__ __forceinline__ int xlane(int v) {
+    return __float_as_int(xlane<O>(__int_as_float(v)));
+}
+// argmax step against lane l ^ O: larger value wins, ties to the lower index
+template <int O>
+__device__ __forceinline__ void xargmax_step(float& v, int& idx) {
+    const float ov = xlane<O>(v);
+    const int oi = xlane<O>(idx);
+    if (ov > v || (ov == v && oi < idx)) {
+        v = ov;
+        idx = oi;
+    }
+}
+__device__ __forceinline__ void wave_argmax(float& v, int& idx) {
+    xargmax_step<32>(v, idx);
+    xargmax_step<16>(v, idx);
+    xargmax_step<8>(v, idx);
+    xargmax_step<4>(v, idx);
+    xargmax_step<2>(v, idx);
+    xargmax_step<1>(v, idx);
+}
 // butterfly sum over the lanes l ^ {HI/2 ... 1} (HI = a power of two <= 64), largest
 // stride first, as `for (o = HI/2; o > 0; o >>= 1) v += __shfl_xor(v, o)`
 template <int HI>

@@ -63,12 +63,7 @@ struct Packed {
 __device__ __forceinline__ int eidx(int tid, int j) { return 2 * (tid + SN * (j >> 1)) + (j & 1); }
 
 __device__ __forceinline__ int block_argmax(float v, int idx, float* redv, int* redi) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        float ov = __shfl_xor(v, o, 64);
-        int oi = __shfl_xor(idx, o, 64);
-        if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
-    }
+    wave_argmax(v, idx);
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     __syncthreads();
     if (l == 0) { redv[w] = v; redi[w] = idx; }
@@ -574,12 +569,7 @@ __device__ __forceinline__ bool lane_ok(int t) { return t < FS_NB; }
 constexpr int FEPT = 24;   // V <= FS_NB * FT * FEPT = 98304
 
 __device__ __forceinline__ float block_argmax_v(float v, int& idx, float* redv, int* redi) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        float ov = __shfl_xor(v, o, 64);
-        int oi = __shfl_xor(idx, o, 64);
-        if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
-    }
+    wave_argmax(v, idx);
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     __syncthreads();
     if (l == 0) { redv[w] = v; redi[w] = idx; }
@@ -737,12 +727,7 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
             sh_int[5] = badm != 0ull;
             a.fs_ticket[b] = 0;
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const float ov = __shfl_xor(mv, o, 64);
-            const int oi = __shfl_xor(mi, o, 64);
-            if (ov > mv || (ov == mv && oi < mi)) { mv = ov; mi = oi; }
-        }
+        wave_argmax(mv, mi);
         if (tid == 0) sh_int[6] = mi;
     }
     __syncthreads();
