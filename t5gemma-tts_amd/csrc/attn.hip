@@ -353,8 +353,11 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     const int n = c1 - c0;
     // the block whose keys include t appends the step's own key/value (a.append)
     const bool has_t = a.append && a.Qpart && t >= c0 && t < c1;
-    const bf16_t* Kb = a.K + row * a.kv_bstride + kvh * a.kv_hstride;
-    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
+    // head_split > 1 (single-chunk rows, no append: cross attention): blockIdx.y is a q
+    // head run alone (G = 1) against kv head blockIdx.y / head_split
+    const int kvc = kvh / a.head_split;
+    const bf16_t* Kb = a.K + row * a.kv_bstride + kvc * a.kv_hstride;
+    const bf16_t* Vb = a.V + row * a.kv_bstride + kvc * a.kv_hstride;
     // Issue order = wait order (vmcnt is in-order): first what the q path needs (the
     // projection's split-K slabs, the PM-RoPE table), then the K (and, for a single-chunk
     // row, V) stream, so q can be summed, staged and rotated while they are in flight.
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
             const int idx = tq - G * D / 4;
             role = 1 + idx / (D / 4);   // 1: key, 2: value
             c4 = idx % (D / 4);
-            col = (role == 1 ? a.k_col0 : a.v_col0) + kvh * D + 4 * c4;
+            col = (role == 1 ? a.k_col0 : a.v_col0) + kvc * D + 4 * c4;
         }
 #pragma unroll
         for (int s = 0; s < QSMAX; ++s)
@@ -784,7 +787,22 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
 }
 
 template <int D, int G>
-static int launch_decode(const AttnArgs& a, hipStream_t st) {
+static int launch_decode(const AttnArgs& a_in, hipStream_t st) {
+    AttnArgs a = a_in;
+    a.head_split = 1;
+    if constexpr (G == 2) {
+        // one chunk and nothing appended (cross attention): one workgroup per q head
+        // instead of per kv group -- half the serial work per workgroup, twice the CUs;
+        // each head's sums are the same as in the G = 2 kernel (bit-identical)
+        if (a.nsplit == 1 && !a.append) {
+            a.head_split = 2;
+            a.Hkv *= 2;
+            a.G = 1;
+            hipLaunchKernelGGL((attn_decode_kernel<D, 1>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, 1u), dim3(256), 0, st,
+                               a);
+            return hipGetLastError() == hipSuccess ? 0 : -2;
+        }
+    }
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
     hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, a);
     if (a.nsplit > 1) {

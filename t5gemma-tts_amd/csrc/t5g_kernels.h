@@ -122,6 +122,7 @@ struct AttnArgs {
     // projection slabs (k rotated by PM-RoPE, v as is), uses it and appends it to K/V
     int append, k_col0, v_col0;
     int dbg_seq;             // diagnostic timeline slot (T5G_DBG_TS builds only)
+    int head_split;          // set by the decode launcher: q heads run one per workgroup
 };
 int attention(const AttnArgs& a, hipStream_t st);
 // decode-shaped (64-key chunks over blockIdx.z + one P.V / combine launch, sdpa numerics)
