@@ -235,6 +235,11 @@ typedef struct {
                                  GEMV (M <= 32, K = 2304, no split); W packed P16 either way */
 } t5g_gemv_args;
 int t5g_gemv(const t5g_gemv_args* args, void* stream);
+/* The decode step's residual + RMSNorm pair on caller buffers (norm.hip, [tf] T5GemmaRMSNorm
+ * :61-78 wired as PMDecoderLayer :285-323): resid_out = bf16(resid + RMSNorm(1+post_w)(delta)),
+ * normed_out = RMSNorm(1+pre_w)(resid_out); bf16 [M][d] rows. For parity tests. */
+int t5g_resid_norm(int32_t M, int32_t d, const void* delta, const void* resid, const void* post_w,
+                   const void* pre_w, float eps, void* resid_out, void* normed_out, void* stream);
 /* hipEvent-timed `iters` launches rotating over packed weights Wp_list[i % n_w]
  * (see t5g_time_gemm); average microseconds per launch in *avg_us. */
 int t5g_time_gemv(const t5g_gemv_args* args, const void* const* Wp_list, int32_t n_w, int32_t iters, void* stream,

@@ -111,6 +111,7 @@ SIGNATURES = {
     "t5g_copy_logits": (C.c_int, [_P, _P, _I, _P]),
     "t5g_sample_only": (C.c_int, [_P, _I, _P, _I, _P]),
     "t5g_gemm": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _I, _I, _P]),
+    "t5g_resid_norm": (C.c_int, [_I, _I, _P, _P, _P, _P, _F, _P, _P, _P]),
     "t5g_time_gemm": (C.c_int, [_P, _I, _I, C.POINTER(_P), _I, _I, _I, _I, _P, _I, _I, _I, _P, C.POINTER(_F)]),
     "t5g_time_decode_step": (C.c_int, [_P, _I, _P, C.POINTER(_F)]),
     "t5g_gemv": (C.c_int, [C.POINTER(GemvArgs), _P]),

@@ -900,6 +900,20 @@ extern "C" int t5g_attention_decode(const t5g_attn_decode_args* g, void* stream)
     return T5G_OK;
 }
 
+extern "C" int t5g_resid_norm(int32_t M, int32_t d, const void* delta, const void* resid, const void* post_w,
+                              const void* pre_w, float eps, void* resid_out, void* normed_out, void* stream) {
+    if (M <= 0 || d <= 0 || d % 8 || !delta || !resid_out) return T5G_EINVAL;
+    NormArgs n = norm_args(M, d, eps);
+    n.delta = (const bf16_t*)delta;
+    n.resid = (const bf16_t*)resid;
+    n.post_w = (const bf16_t*)post_w;
+    n.pre_w = (const bf16_t*)pre_w;
+    n.resid_out = (bf16_t*)resid_out;
+    n.normed_out = (bf16_t*)normed_out;
+    RC(resid_norm(n, (hipStream_t)stream));
+    return T5G_OK;
+}
+
 static_assert(sizeof(t5g_gemv_args) == 152, "t5g_gemv_args layout");
 
 static int gemv_from_abi(const t5g_gemv_args* g, const void* W, DecGemmArgs* out) {

@@ -162,3 +162,35 @@ def test_gemv_register_x_variant(epi, M):
     parts = [_run(epi, min(16, M - r0), N, K, 8, 1, seed=3, X=X[r0:r0 + 16].contiguous(), W=W, layout=0)[0]
              for r0 in range(0, M, 16)]
     assert torch.equal(got, torch.cat(parts)), "register-X rows differ from the LDS-staged kernel"
+
+
+@pytest.mark.parametrize("M", [8, 3, 16])
+def test_resid_norm_vs_fp32(M):
+    """The decode step's residual + RMSNorm kernel (t5g_resid_norm; norm.hip): against a
+    PyTorch fp32 restatement of [tf] T5GemmaRMSNorm :61-78 wired as the residual add of
+    PMDecoderLayer :285-323 -- within the bf16 roundings of the two norms."""
+    _need_gpu()
+    from t5gemma_tts_amd import _lib
+    L = _lib.lib()
+    dev = "cuda"
+    K = 2304
+    g = torch.Generator(device="cpu").manual_seed(77 + M)
+    delta = (torch.randn(M, K, generator=g) * 3.0).to(BF16)
+    h = torch.randn(M, K, generator=g).to(BF16)
+    post_w = (torch.randn(K, generator=g) * 0.1).to(BF16)
+    pre_w = (torch.randn(K, generator=g) * 0.1).to(BF16)
+    dd, hd, pd, qd = delta.to(dev), h.to(dev), post_w.to(dev), pre_w.to(dev)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    h1 = torch.empty_like(hd)
+    xn = torch.empty_like(hd)
+    assert L.t5g_resid_norm(M, K, C.c_void_p(dd.data_ptr()), C.c_void_p(hd.data_ptr()), C.c_void_p(pd.data_ptr()),
+                            C.c_void_p(qd.data_ptr()), C.c_float(EPS), C.c_void_p(h1.data_ptr()),
+                            C.c_void_p(xn.data_ptr()), st) == 0
+    torch.cuda.synchronize()
+    hr = (h.float() + _rms(delta, post_w).float()).to(BF16)
+    xr = _rms(hr, pre_w)
+    for got, ref in ((h1.cpu(), hr), (xn.cpu(), xr)):
+        diff = (got.float() - ref.float()).abs()
+        ulp = ref.float().abs().clamp(min=2.0 ** -20) * 2 ** -7
+        assert (diff <= 2 * ulp).all(), diff.max()
+        assert (diff == 0).float().mean() > 0.95
