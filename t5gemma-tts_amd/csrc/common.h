@@ -298,7 +298,20 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
                     __builtin_amdgcn_s_getreg((31 << 11) | 4);                                     \
         }                                                                                          \
     } while (0)
+// the block-start clock read now, stored later (T5G_TS_START / T5G_TS_COMMIT): a block
+// that exits early (a finished sampler row) leaves the previous record intact
+#define T5G_TS_START() const unsigned long long t5g_ts0_ = __builtin_amdgcn_s_memrealtime()
+#define T5G_TS_COMMIT()                                                                            \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && t5g_dbg_ts_buf) {                                                 \
+            const size_t blin_ = (size_t)a.dbg_seq * 4096 +                                         \
+                                 blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);   \
+            t5g_dbg_ts_buf[blin_ * 8] = t5g_ts0_;                                                  \
+        }                                                                                          \
+    } while (0)
 #else
 #define T5G_TS_UNIT(unit)
 #define T5G_TS(k) do { } while (0)
+#define T5G_TS_START() do { } while (0)
+#define T5G_TS_COMMIT() do { } while (0)
 #endif

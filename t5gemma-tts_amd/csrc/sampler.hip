@@ -597,7 +597,7 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
     __shared__ int is_last;
 
     const int sl = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, wid = tid >> 6;
-    T5G_TS(0);
+    T5G_TS_START();
     // the slice's logits depend on nothing: request them first (clamped addresses, no
     // branch), so the row's state / parameters / silence list arrive meanwhile
     const int V = a.V;
@@ -609,6 +609,7 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
     for (int j = 0; j < FEPT; ++j) raw[j] = lg[max(0, min(i0 + tid + FT * j, i1 - 1))];
     SamplerState st = a.state[b];
     if (st.done) return;
+    T5G_TS_COMMIT();
     const SamplerRow pr = a.rows[b];
     int kk = pr.top_k;
     if (pr.top_k_list_len > 0) kk = a.top_k_list[pr.top_k_list_off + min(pr.top_k_list_len - 1, st.cur_num_gen)];

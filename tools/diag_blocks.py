@@ -51,7 +51,8 @@ def main():
     # norm: the last layer's final norm (blocks 0-7); gemm: head1 (blocks 0-143); blocks past
     # those hold older launches (prefill) and are not read
     groups = [("norm", "norm (final, 8 rows)", 0, 8), ("attn", "attn cross", 0, 32), ("attn", "attn pvc", 32, 256),
-              ("attn", "attn scores", 256, 480), ("gemm", "gemm head1", 0, 144)]
+              ("attn", "attn scores", 256, 480), ("gemm", "gemm head1", 0, 144),
+              ("sampler", "sampler_fast (last step with live rows)", 0, 128)]
     for u, name, lo, hi in groups:
         a = bufs[u].view(-1, 8).cpu().numpy()[lo:hi]
         rows = a[(a[:, 0] > 0)]
