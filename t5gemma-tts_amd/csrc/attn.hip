@@ -611,7 +611,7 @@ __device__ __forceinline__ DecRow dec_row(const AttnArgs& a, int qi) {
 // exps), takes l from aten's lane-ordered block sums of them, and streams only its
 // DZ-wide slice of V (DZ = 32: 64 B per key at D = 256, all 8 slices of a row on one XCD
 // under round-robin placement, so a 128-B line is fetched once; DZ = 64 when 32-wide
-// slices would need more than two workgroups per CU, e.g. 32 rows).
+// slices would need more than one workgroup per CU, e.g. 16 or 32 rows).
 // The fp32 sums keep the order of the former per-chunk P.V + combine pair, so results are
 // bit-identical to it: per 64-key chunk, KPB key slots (slot = wave * KPW + kg of the
 // chunk kernel's lane map) each accumulate NIT keys j = c0 + i * KPB + slot in i order;
@@ -635,6 +635,11 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
     __shared__ float mrun[G][SDPA_MAX_BLOCKS];     // running max through block b
     __shared__ float et_s[G], stat_l[G];
     __shared__ float ol[CPR][KPB][G][PVC_DZ];      // slot chain sums of the sub-round
+    // second block of the one-pass path (rows of <= 1024 keys)
+    __shared__ float pex1[G][SDPA_KV_BLOCK + 16];
+    __shared__ float pbf1[G][SDPA_KV_BLOCK];
+    __shared__ float ol1[CPR][KPB][G][PVC_DZ];
+    __shared__ float tsum[G][2];
     const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     T5G_TS(0);
@@ -658,8 +663,9 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
             v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
         }
     };
-    u32x4 vn[NIT];
+    u32x4 vn[NIT], v1[NIT];
     vload(vn, 0);
+    if constexpr (RPB == 1) vload(v1, 1);   // the second block's slice (zeros if none)
     const float* sb = a.sbuf + ((long)qi * a.Hkv * G + kvh * G) * a.kv_cap + r.lo;
     auto sload = [&](float (&sc)[G][PPT], int b) {
 #pragma unroll
@@ -670,8 +676,9 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
                 sc[g][k] = sb[(long)g * a.kv_cap + (pos < r.span ? pos : 0)];
             }
     };
-    float scn[G][PPT];
+    float scn[G][PPT], sc1[G][PPT];
     sload(scn, 0);
+    if constexpr (RPB == 1) sload(sc1, 1);
     if (wave < G) {   // running maxima through each block, from the chunk maxima
         const int g = wave;
         const float cm = lane < nch ? a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + lane) * G + g] : -INFINITY;
@@ -679,13 +686,110 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
             const float mb = wave_max(lane < min(nch, (b + 1) * CPB) ? cm : -INFINITY);
             if (lane == 0) mrun[g][b] = mb;
         }
-        if (lane < 16) pex[g][SDPA_KV_BLOCK + lane] = 0.f;
+        if (lane < 16) {
+            pex[g][SDPA_KV_BLOCK + lane] = 0.f;
+            pex1[g][SDPA_KV_BLOCK + lane] = 0.f;
+        }
     }
     __syncthreads();
-    float l = 0.f, m_old = -INFINITY;            // wave g < G: head g's running sum
-    float dst = 0.f, blk = 0.f;                  // fold thread (g, dd)
     const bool folder = tid < G * PVC_DZ;
     const int fg = tid / PVC_DZ, fdd = tid % PVC_DZ;
+    if constexpr (RPB == 1) {
+        if (nblk <= 2) {
+            // rows of <= 1024 keys: both blocks in one pass -- every p staged at once, the
+            // (head, block) sums on separate waves, the chains of both blocks before one
+            // fold. The same operations and order as the block loop below (bit-identical),
+            // two barriers instead of five.
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+                if (bb < nblk) {
+                    const int blen = min(SDPA_KV_BLOCK, r.span - bb * SDPA_KV_BLOCK);
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        const float mb = mrun[g][bb];
+#pragma unroll
+                        for (int k = 0; k < PPT; ++k) {
+                            const int pos = tid + 256 * k;
+                            const float scv = bb ? sc1[g][k] : scn[g][k];
+                            const float p = pos < blen ? sdpa_p(__fsub_rn(scv, mb), pos, blen) : 0.f;
+                            (bb ? pex1 : pex)[g][pos] = p;
+                            (bb ? pbf1 : pbf)[g][pos] = rbf(p);
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            if (wave < G * nblk) {
+                const int g = wave % G, bb = wave / G;
+                const int blen = min(SDPA_KV_BLOCK, r.span - bb * SDPA_KV_BLOCK);
+                const float ts = sdpa_block_sum_lds<SDPA_KV_BLOCK>(bb ? pex1[g] : pex[g], blen, lane);
+                if (lane == 0) tsum[g][bb] = ts;
+            }
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+                if (bb < nblk) {
+                    const int jb = cr * DCH;
+                    float o[G][8];
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+#pragma unroll
+                        for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
+#pragma unroll
+                    for (int i = 0; i < NIT; ++i) {
+                        const int jl = jb + i * KPB + slot;
+                        const u32x4 vv = bb ? v1[i] : vn[i];
+#pragma unroll
+                        for (int g = 0; g < G; ++g) {
+                            const float p = (bb ? pbf1 : pbf)[g][jl];
+#pragma unroll
+                            for (int jj = 0; jj < 4; ++jj) {
+                                o[g][2 * jj] += p * bf_lo(vv[jj]);
+                                o[g][2 * jj + 1] += p * bf_hi(vv[jj]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+#pragma unroll
+                        for (int jj = 0; jj < 8; ++jj) (bb ? ol1 : ol)[cr][slot][g][8 * od + jj] = o[g][jj];
+                }
+            }
+            __syncthreads();
+            T5G_TS(1);
+            if (!folder) return;
+            float lsum = 0.f, mo = -INFINITY, dd = 0.f;
+            for (int bb = 0; bb < nblk; ++bb) {
+                const float mb = mrun[fg][bb];
+                const float et = sdpa_block_rescale(mo, mb);
+                lsum = fmaf(et, lsum, tsum[fg][bb]);
+                mo = mb;
+                float bk = 0.f;
+#pragma unroll
+                for (int c = 0; c < CPR; ++c) {
+                    float w4[4];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        float t[KPW];
+#pragma unroll
+                        for (int k = 0; k < KPW; ++k) t[k] = (bb ? ol1 : ol)[c][w * KPW + k][fg][fdd];
+#pragma unroll
+                        for (int st = 1; st < KPW; st <<= 1)
+#pragma unroll
+                            for (int k = 0; k < KPW; k += 2 * st) t[k] = t[k] + t[k + st];
+                        w4[w] = t[0];
+                    }
+                    const float pc = ((w4[0] + w4[1]) + w4[2]) + w4[3];
+                    if (bb * CPB + c < nch) bk += pc;
+                }
+                dd = dd * et + bk;
+            }
+            const float inv = __fdiv_rn(1.0f, lsum);
+            a.O[(long)qi * a.ldo + (kvh * G + fg) * D + PVC_DZ * z + fdd] = f2bf(__fmul_rn(dd, inv));
+            return;
+        }
+    }
+    float l = 0.f, m_old = -INFINITY;            // wave g < G: head g's running sum
+    float dst = 0.f, blk = 0.f;                  // fold thread (g, dd)
     auto stage = [&](const float (&sc)[G][PPT], int b) {   // exact p of block b -> LDS
         const int blen = min(SDPA_KV_BLOCK, r.span - b * SDPA_KV_BLOCK);
 #pragma unroll
@@ -806,8 +910,9 @@ static int launch_decode(const AttnArgs& a_in, hipStream_t st) {
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
     hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, a);
     if (a.nsplit > 1) {
-        // one round of workgroups: 32-wide slices while they fit two per CU, else 64-wide
-        if (D >= 64 && (long)a.Mq * a.Hkv * (D / 32) > 512)
+        // one round of workgroups: 32-wide slices (one workgroup per CU: 256 VGPRs) while
+        // they fit, else 64-wide (two per CU)
+        if (D >= 64 && (long)a.Mq * a.Hkv * (D / 32) > 256)
             hipLaunchKernelGGL((attn_pvc_kernel<D, G, 64>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(D / 64)),
                                dim3(256), 0, st, a);
         else

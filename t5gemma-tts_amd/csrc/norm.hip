@@ -35,11 +35,24 @@ __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
     return w;
 }
 
+// block_sum without its leading barrier: each rms8 call of a launch gets its own `red`
+// (nothing reads it before), so one barrier per reduction; the same fixed-order sum
+__device__ __forceinline__ float block_sum_once(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int nw = (blockDim.x + 63) >> 6;
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    float s = 0.f;
+    for (int i = 0; i < nw; ++i) s += red[i];
+    return s;
+}
+
 __device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, u32x4 w8, float eps, float* red) {
     float ss = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
-    float tot = block_sum(active ? ss : 0.f, red);
+    float tot = block_sum_once(active ? ss : 0.f, red);
     float r = 1.0f / sqrtf(tot / (float)d + eps);
     if (!active) return;
     float wf[8];
@@ -55,7 +68,7 @@ __device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, u32x4 w8
 // serialised two memory round trips here.
 template <int NS, int SRC>   // NS: split-K slabs of the part path; SRC: 0 delta, 1 ids, 2 part
 __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_post, int has_resid, int has_pre) {
-    __shared__ float red[32];
+    __shared__ float red[2][32];   // one per RMSNorm of the launch
     T5G_TS(0);
     const int mi = blockIdx.x;
     const int m = a.out_rows ? a.out_rows[mi] : mi;
@@ -95,7 +108,7 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
     } else {
         unpack8(*(const u32x4*)(a.delta + (long)m * d + 8 * cc), v);
     }
-    if (has_post) rms8(v, active, d, w_post, a.eps, red);
+    if (has_post) rms8(v, active, d, w_post, a.eps, red[0]);
     T5G_TS(1);
     if (has_resid) {
         float r8[8];
@@ -106,7 +119,7 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
     const long orow = a.out_rows ? (long)mi : (long)m;
     if (a.resid_out && active) *(u32x4*)(a.resid_out + orow * d + 8 * c) = pack8(v);
     if (has_pre) {
-        rms8(v, active, d, w_pre, a.eps, red);
+        rms8(v, active, d, w_pre, a.eps, red[1]);
         if (active) *(u32x4*)(a.normed_out + orow * d + 8 * c) = pack8(v);
     }
     T5G_TS(2);
