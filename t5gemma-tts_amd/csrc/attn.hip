@@ -80,21 +80,6 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
     dst[i + H2] = f2bf(o2);
 }
 
-__global__ void rope_table_kernel(const float* pos, const float* inv_freq, int D, float* tab) {
-    const int r = blockIdx.x, H2 = D / 2;
-    for (int i = threadIdx.x; i < H2; i += blockDim.x) {
-        const float ang = inv_freq[i] * pos[r];
-        tab[(long)r * D + i] = rbf(cosf(ang));
-        tab[(long)r * D + H2 + i] = rbf(sinf(ang));
-    }
-}
-
-int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st) {
-    if (rows <= 0) return 0;
-    hipLaunchKernelGGL(rope_table_kernel, dim3((unsigned)rows), dim3(128), 0, st, pos, inv_freq, D, tab);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
 int rope_store(const RopeArgs& a, hipStream_t st) {
     if (a.M <= 0) return 0;
     if (a.nq && a.Qout == a.X && a.ldq != a.ldx) return -1;

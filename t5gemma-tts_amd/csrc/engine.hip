@@ -441,11 +441,8 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
     // split-K factors (decode: spread the weight streams over >= 512 blocks)
     const int s_qkv = decode ? e->s_qkv : 1, s_o = decode ? e->s_o : 1, s_down = decode ? e->s_down : 1;
     // one cos/sin table per step: every layer's q/k rotation uses the same positions
-    const float* tab = nullptr;
-    if (decode) {
-        RC(rope_table(pos, e->w.inv_freq, M, D, e->rope_tab, st));
-        tab = e->rope_tab;
-    }
+    // (written by layer 0's embedding-norm launch below)
+    const float* tab = decode ? e->rope_tab : nullptr;
     // norm after a Linear: h = h + RMSNorm_post(delta), xn = RMSNorm_pre(h)
     auto resid = [&](int splits, const void* post_w, const void* pre_w) -> int {
         NormArgs n = norm_args(M, d, c.rms_eps);
@@ -489,6 +486,12 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             n.pre_w = (const bf16_t*)L.norms[0];
             n.resid_out = h;
             n.normed_out = xn;
+            if (decode) {   // and the step's RoPE table, in the same launch
+                n.rope_pos = pos;
+                n.rope_inv_freq = e->w.inv_freq;
+                n.rope_tab = e->rope_tab;
+                n.rope_D = D;
+            }
             RC(resid_norm(n, st));
         }
         // --- self attention

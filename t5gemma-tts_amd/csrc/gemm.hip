@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void gemm_p16_kernel(GemmArgs a) {
     } else if constexpr (WPG == KS) {
         // one slice per wave: kb = kb_lo + ks, +KS, ...; every group of UD k-steps is
         // issued at once (predicated), so a short slice costs a single memory round trip
-        constexpr int UD = (MT == 1) ? 16 : 8;
+        constexpr int UD = (MT == 1) ? 16 : (MT == 2 ? 12 : 8);
         for (int kb = kb_lo + ks; kb < kb_hi; kb += UD * KS) {
             bf16x8_s wf[UD];
             bf16x8_s xf[UD][MT];

@@ -71,6 +71,14 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
     __shared__ float red[2][32];   // one per RMSNorm of the launch
     T5G_TS(0);
     const int mi = blockIdx.x;
+    if (a.rope_tab) {   // the decode step's per-row cos/sin table (used by every layer's attention)
+        const int H2 = a.rope_D / 2;
+        for (int i = threadIdx.x; i < H2; i += blockDim.x) {
+            const float ang = a.rope_inv_freq[i] * a.rope_pos[mi];
+            a.rope_tab[(long)mi * a.rope_D + i] = rbf(cosf(ang));
+            a.rope_tab[(long)mi * a.rope_D + H2 + i] = rbf(sinf(ang));
+        }
+    }
     const int m = a.out_rows ? a.out_rows[mi] : mi;
     const int d = a.d;
     const int c = threadIdx.x;          // chunk of 8 elements

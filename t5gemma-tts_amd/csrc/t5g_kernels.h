@@ -63,6 +63,11 @@ struct NormArgs {
     bf16_t* normed_out;      // [M][d] or null
     const int* out_rows;     // optional: process only rows out_rows[i] (i < M), write compact
     int dbg_seq;             // diagnostic timeline slot (T5G_DBG_TS builds only)
+    // optional: each row block also writes that row's RoPE cos/sin table
+    const float* rope_pos;   // [M] positions
+    const float* rope_inv_freq;
+    float* rope_tab;         // [M][rope_D]
+    int rope_D;
 };
 int resid_norm(const NormArgs& a, hipStream_t st);
 
@@ -88,8 +93,8 @@ struct RopeArgs {
     const float* rope_tab;   // optional [rows][D]: bf16-rounded cos (D/2) | sin (D/2) per row
 };
 int rope_store(const RopeArgs& a, hipStream_t st);
-// tab[r][i] = bf16(cos(inv_freq[i] * pos[r])), tab[r][D/2 + i] = bf16(sin(...)), r < rows
-int rope_table(const float* pos, const float* inv_freq, int rows, int D, float* tab, hipStream_t st);
+// (the decode step's per-row table tab[r][i] = bf16(cos(inv_freq[i] * pos[r])),
+// tab[r][D/2 + i] = bf16(sin(...)) is written by layer 0's embedding-norm launch: NormArgs.rope_*)
 
 // ---- attention ----------------------------------------------------------------
 struct AttnArgs {
@@ -116,7 +121,7 @@ struct AttnArgs {
     const float* inv_freq;   // [D/2]
     float* sbuf;             // decode, rows of > 64 keys: scores [Mq][Hkv*G][kv_cap] fp32
     float* mbuf;             // decode: per-chunk score maxima [Mq][Hkv][nsplit][G]
-    const float* rope_tab;   // optional per-row cos/sin table (see rope_table)
+    const float* rope_tab;   // optional per-row cos/sin table (written with layer 0's embedding norm)
     int kv_cap;              // allocated keys per (row, head): speculative loads stay below it
     // decode self-attention: the block holding key t = kv_len-1 builds it from the
     // projection slabs (k rotated by PM-RoPE, v as is), uses it and appends it to K/V
