@@ -81,6 +81,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--batch", type=int, default=0, help="utterances per GPU (default 8, --e2e 32)")
+    ap.add_argument("--natural-eos", action="store_true",
+                    help="accept EOS when sampled (SURVEY 8(d)'s second run) instead of throughput mode")
     ap.add_argument("--e2e", action="store_true", help="C5: generate + XCodec2 decode in the timed region")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo (CPU collectives; lets N ranks share one GPU "
@@ -141,7 +143,8 @@ def main():
     if rank == 0:
         rows = [[len(x), tgt] + x + y for x, y, tgt in make_batch(cfg, G, seed=20251226)]
         costs = [r[1] for r in rows]
-    params = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3, eos_disabled=True)
+    params = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3,
+                            eos_disabled=not args.natural_eos)
     gen_tokens = [0]
     audio_frames = [0]
 
@@ -253,7 +256,8 @@ def main():
                 "vs_baseline": None, "dtype": "bf16",
                 "data": "synthetic (seeded random 2b-2b weights, random text/prompt codes)",
                 "config": {"workload": f"C3 voice-clone: 2b-2b bf16, {B} utterances/GPU, T_x 60, T_p 151, "
-                                       "10 s target (751 tokens/utterance), top-k 30/top-p 0.9/T 0.8",
+                                       "10 s target (751 tokens/utterance), top-k 30/top-p 0.9/T 0.8"
+                                       + (", EOS accepted when sampled" if args.natural_eos else ""),
                            "global_batch": B * world, "seq_len": T_P + 1 + n_tok_row,
                            "parallelism": f"dp{world} (utterance shards)"},
                 "rtf_audio_s_per_wall_s": round(value / 50.0, 3),
