@@ -68,11 +68,12 @@ def _run(L, B, lens, Hq=8, Hkv=4, D=256, causal=1, seed=0):
     return got, q, K, V
 
 
-@pytest.mark.parametrize("L", [1, 63, 64, 65, 152, 527, 903])
+@pytest.mark.parametrize("L", [1, 63, 64, 65, 152, 527, 903, 1500, 2100])
 def test_self_attention_decode_vs_cpu_sdpa(L):
     """8 rows x 8 q heads / 4 kv heads x 256 (2b-2b), ragged lengths up to L: rows of > 64
-    keys go through the three-launch path (scores, P.V, combine), the others one launch.
-    Bit-equal to aten's CPU SDPA numerics except fp32 GEMM-order flips (<= 1 ulp)."""
+    keys go through the two-launch path (scores, then P.V / combine: one pass for rows of
+    <= 1024 keys, the block loop beyond), the others one launch. Bit-equal to aten's CPU
+    SDPA numerics except fp32 GEMM-order flips (<= 1 ulp)."""
     _need_gpu()
     B = 8
     lens = [L, max(1, L - 1), max(1, L // 2), max(1, L - 64), 1, max(1, L - 3), max(1, (3 * L) // 4), L]
