@@ -213,7 +213,8 @@ int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, float* avg_
  * be 0 / NULL (the fused-prologue variants measured slower in round 1 were removed). */
 typedef struct {
     int32_t M, K, N;
-    int32_t epi, pro, nw;     /* pro: reserved (0); nw: waves per block, 4 / 8 / 16 (GeGLU 4 / 8) */
+    int32_t epi, pro, nw;     /* pro: reserved (0); nw: waves per block -- layout 0: 4 / 8 / 16
+                                 (GeGLU 4 / 8); layout 1: 4 / 6 / 8 / 9 / 12 (others: 8) */
     const void* W;            /* packed [N][K] */
     const void* bias;         /* bf16 [N] (epi 1) */
     void* Y;                  /* bf16 or fp32 [M][ldy] */

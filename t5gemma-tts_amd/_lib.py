@@ -144,14 +144,14 @@ def lib():
 # The decode gate/up launch as engine.hip's decoder_pass issues it at the 2b-2b width
 # (gemv_dec with layout_rx: register-resident X, EPI_GEGLU, 8 waves sharing each unit's K
 # stream, 9 fragments per wave per unit, one block per CU).
-GATE_UP_KERNEL = "gemv_rx_kernel<8, 1, 3 (GEGLU), 9> (decode gate/up, M=8, 84.9 MB weights)"
+GATE_UP_KERNEL = "gemv_rx_kernel<12, 1, 3 (GEGLU), 6> (decode gate/up, M=8, 84.9 MB weights)"
 
 
 def time_gate_up(X_ptr: int, ldx: int, M: int, W_ptrs, N: int, K: int, Y_ptr: int, iters: int, stream) -> float:
     """hipEvent-timed decode gate/up launches on `stream`, rotating over the packed weight
     sets W_ptrs (one per layer, so every launch streams from HBM); avg us per launch."""
     a = GemvArgs()
-    a.M, a.K, a.N, a.epi, a.pro, a.nw, a.un = M, K, N, 3, 0, 8, 8
+    a.M, a.K, a.N, a.epi, a.pro, a.nw, a.un = M, K, N, 3, 0, 12 if K == 2304 else 8, 8   # as the engine
     a.X, a.ldx, a.Y, a.ldy, a.splits, a.layout, a.max_grid = X_ptr, ldx, Y_ptr, N // 2, 1, int(K == 2304), 0
     arr = (C.c_void_p * len(W_ptrs))(*W_ptrs)
     us = C.c_float()

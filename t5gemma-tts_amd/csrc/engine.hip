@@ -540,7 +540,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         // --- GeGLU MLP (decode: the one-block-per-CU GEMV; register-resident X at the
         // 2b-2b width, up to 32 rows)
         if (decode && (M <= 16 || (M <= 32 && d == 2304))) {
-            DecGemmArgs g = dec_args(M, L.gate_up, 2 * f, d, act, f, 8);
+            DecGemmArgs g = dec_args(M, L.gate_up, 2 * f, d, act, f, d == 2304 ? 12 : 8);
             g.X = xn;
             g.ldx = d;
             g.un = 8;

@@ -364,19 +364,32 @@ size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int rg) {
 
 // the register-resident-X kernel for the shapes it is instantiated for (8 waves sharing
 // each unit's K stream, SPU = 9 k-steps per wave: K = 2304, no split) -- 0 if launched
-template <int MT, int EPI>
-static int launch_rx(const DecGemmArgs& a, hipStream_t st) {
-    auto* fn = gemv_rx_kernel<8, MT, EPI, 9>;
+template <int NW, int MT, int EPI>
+static int launch_rx_nw(const DecGemmArgs& a, hipStream_t st) {
+    constexpr int SPU = 72 / NW;
+    auto* fn = gemv_rx_kernel<NW, MT, EPI, SPU>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GD_LDS_MAX);
         attr = true;
     }
     const int grid = gd_grid(a, 1);
-    const size_t shm = (size_t)((a.NG + grid - 1) / grid) * MT * 8 * 64 * 16;
+    const size_t shm = (size_t)((a.NG + grid - 1) / grid) * MT * NW * 64 * 16;
     if (shm > GD_LDS_MAX) return -1;
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid, 1u), dim3(8 * 64), shm, st, a);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid, 1u), dim3(NW * 64), shm, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+// a.nw picks the waves sharing each unit's K stream (72 k-steps split evenly; the decode
+// gate/up runs 12: 17.9 vs 18.5 us for 8 at 8 rows, tools/probe_rx_nw.py)
+template <int MT, int EPI>
+static int launch_rx(const DecGemmArgs& a, hipStream_t st) {
+    switch (a.nw) {
+        case 4: return launch_rx_nw<4, MT, EPI>(a, st);
+        case 6: return launch_rx_nw<6, MT, EPI>(a, st);
+        case 9: return launch_rx_nw<9, MT, EPI>(a, st);
+        case 12: return launch_rx_nw<12, MT, EPI>(a, st);
+        default: return launch_rx_nw<8, MT, EPI>(a, st);
+    }
 }
 
 int gemv_rx(const DecGemmArgs& a, int epi, hipStream_t st) {
