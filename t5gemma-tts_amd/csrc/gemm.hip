@@ -332,8 +332,16 @@ static int launch_epi(const GemmArgs& a, int epi, int mblocks, hipStream_t st) {
 // other's lines in L1. Next k-step's fragments are in flight while this one multiplies.
 // Accumulation is one MFMA chain in k order per output: deterministic, and a token's
 // result does not depend on the other tokens of the launch (batch-invariant).
-template <int EPI>
+// S k-steps of fragments are in flight per wave (a ring of S register stages): at the
+// decoder prefill's 1 216 tokens a launch has 1-2 blocks per CU, one wave per SIMD, so
+// the ring depth -- not the MFMA rate -- sets how long each k-step waits for its loads.
+// Stage s of a ring turn feeds chain s & 1, so every S gives the same k order per chain.
+#ifndef PF_STAGES
+#define PF_STAGES 4
+#endif
+template <int EPI, int S>
 __global__ __launch_bounds__(256) void gemm_pf_kernel(GemmArgs a) {
+    static_assert(S % 2 == 0, "even ring: stage parity = k-step parity");
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wr = wave >> 1, wc = wave & 1;
     const int g0 = blockIdx.x * 8 + wr * 4;                 // first row group of this wave
@@ -370,13 +378,15 @@ __global__ __launch_bounds__(256) void gemm_pf_kernel(GemmArgs a) {
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) c[rg][mt] = mfma16(w[rg], x[mt], c[rg][mt]);
     };
-    bf16x8_s wa[4], xa[4], wb[4], xb[4];
-    load(wa, xa, 0);
-    for (int kb = 0; kb < KB; kb += 2) {
-        load(wb, xb, kb + 1);
-        mma(wa, xa, acc);
-        load(wa, xa, kb + 2);
-        mma(wb, xb, acc2);
+    bf16x8_s wq[S][4], xq[S][4];
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s) load(wq[s], xq[s], s);
+    for (int kb = 0; kb < KB; kb += S) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            load(wq[(s + S - 1) % S], xq[(s + S - 1) % S], kb + s + S - 1);
+            mma(wq[s], xq[s], (s & 1) ? acc2 : acc);
+        }
     }
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg)
@@ -433,17 +443,24 @@ __global__ __launch_bounds__(256) void gemm_pf_kernel(GemmArgs a) {
     }
 }
 
-static int gemm_prefill(const GemmArgs& a, int epi, hipStream_t st) {
-    if ((long)a.M * a.ldx * 2 >= 0x7fffffffL || (long)a.NG * a.KB * 1024 >= 0x7fffffffL) return -1;
-    const dim3 grid((unsigned)((a.NG + 7) / 8), (unsigned)((a.M + 127) / 128));
+template <int S>
+static int launch_pf(const GemmArgs& a, int epi, dim3 grid, hipStream_t st) {
     switch (epi) {
-        case EPI_BF16: hipLaunchKernelGGL(gemm_pf_kernel<EPI_BF16>, grid, dim3(256), 0, st, a); break;
-        case EPI_BIAS_BF16: hipLaunchKernelGGL(gemm_pf_kernel<EPI_BIAS_BF16>, grid, dim3(256), 0, st, a); break;
-        case EPI_BIAS_GELU: hipLaunchKernelGGL(gemm_pf_kernel<EPI_BIAS_GELU>, grid, dim3(256), 0, st, a); break;
-        case EPI_GEGLU: hipLaunchKernelGGL(gemm_pf_kernel<EPI_GEGLU>, grid, dim3(256), 0, st, a); break;
+        case EPI_BF16: hipLaunchKernelGGL((gemm_pf_kernel<EPI_BF16, S>), grid, dim3(256), 0, st, a); break;
+        case EPI_BIAS_BF16: hipLaunchKernelGGL((gemm_pf_kernel<EPI_BIAS_BF16, S>), grid, dim3(256), 0, st, a); break;
+        case EPI_BIAS_GELU: hipLaunchKernelGGL((gemm_pf_kernel<EPI_BIAS_GELU, S>), grid, dim3(256), 0, st, a); break;
+        case EPI_GEGLU: hipLaunchKernelGGL((gemm_pf_kernel<EPI_GEGLU, S>), grid, dim3(256), 0, st, a); break;
         default: return -4;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+static int gemm_prefill(const GemmArgs& a, int epi, hipStream_t st) {
+    if ((long)a.M * a.ldx * 2 >= 0x7fffffffL || (long)a.NG * a.KB * 1024 >= 0x7fffffffL) return -1;
+    const dim3 grid((unsigned)((a.NG + 7) / 8), (unsigned)((a.M + 127) / 128));
+    // ring depth: PF_STAGES k-steps when they divide KB (no partial ring turn), else 2
+    if (a.KB % PF_STAGES == 0) return launch_pf<PF_STAGES>(a, epi, grid, st);
+    return launch_pf<2>(a, epi, grid, st);
 }
 
 // Decode GEMM whose block stages the X rows of its K slice in LDS once and shares them
