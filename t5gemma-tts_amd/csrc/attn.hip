@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 constexpr int QSMAX = 4;   // q / appended-k/v projection slabs read by the decode kernel
 constexpr int DCH = 64;    // keys per decode chunk
 
-template <int D, int G>
+template <int D, int G, bool VFIRST>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     constexpr int LPK = D / 8;
     constexpr int KPW = 64 / LPK;
@@ -385,14 +385,19 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     // (zeros, no traffic) -- no branch
     const __amdgpu_buffer_rsrc_t krs = frag_rsrc(Kb, (uint32_t)a.kv_cap * D * 2u);
     const __amdgpu_buffer_rsrc_t vrs = frag_rsrc(Vb, (uint32_t)a.kv_cap * D * 2u);
+    // V is read only by single-chunk rows. VFIRST (launches whose rows are all one chunk:
+    // cross attention) requests it with K; otherwise it is requested after the scores, so
+    // NIT V registers are not held through the K stream: <= 128 VGPRs, four workgroups per
+    // CU, 1 024 chunk workgroups in one round (32 rows x 4 kv heads x 8 chunks)
     u32x4 kr[NIT], vr[NIT];
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
         const int j = c0 + i * KPB + wave * KPW + kg;
         const int off = j < c1 ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
         kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
-        vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, single ? off : (int)0x7ffffff0,
-                                                                              0, 0));
+        if constexpr (VFIRST)
+            vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  vrs, single ? off : (int)0x7ffffff0, 0, 0));
     }
     float q[G][8];
     if (a.Qpart) {
@@ -441,12 +446,13 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         }
     }
     if (n <= 0) return;
+    u32x4 vt = (u32x4){0u, 0u, 0u, 0u};   // the appended value, for the lane holding key t
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
         const int j = c0 + i * KPB + wave * KPW + kg;
         if (j >= c1) {
             kr[i] = (u32x4){0u, 0u, 0u, 0u};
-            vr[i] = (u32x4){0u, 0u, 0u, 0u};
+            if constexpr (VFIRST) vr[i] = (u32x4){0u, 0u, 0u, 0u};
         }
         if (has_t && j == t) {
             // key t: PM-RoPE of the new key (rope_store_kernel's arithmetic), then append
@@ -468,7 +474,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
                 vw[jj] = pack2(vo[0], vo[1]);
             }
             kr[i] = kw;
-            if (single) vr[i] = vw;
+            vt = vw;
+            if constexpr (VFIRST) vr[i] = vw;
             *(u32x4*)(const_cast<bf16_t*>(Kb) + (long)t * D + 8 * dl) = kw;
             *(u32x4*)(const_cast<bf16_t*>(Vb) + (long)t * D + 8 * dl) = vw;
         }
@@ -508,7 +515,17 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         return;
     }
     // single-chunk row: one aten kv block of `span` keys; every lane computes its key's p
-    // once (the tail's double exp included), the block sum then only chains adds
+    // once (the tail's double exp included), the block sum then only chains adds. Its V
+    // (the appended value from registers, not from the store above) is requested first.
+    if constexpr (!VFIRST) {
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int j = c0 + i * KPB + wave * KPW + kg;
+            const int off = (j < c1 && !(has_t && j == t)) ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
+            vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
+            if (has_t && j == t) vr[i] = vt;
+        }
+    }
     if (wave < G) {
         const int g = wave;
         const float s = lane < n ? sm[g][lane] : -INFINITY;
@@ -887,13 +904,14 @@ static int launch_decode(const AttnArgs& a_in, hipStream_t st) {
             a.head_split = 2;
             a.Hkv *= 2;
             a.G = 1;
-            hipLaunchKernelGGL((attn_decode_kernel<D, 1>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, 1u), dim3(256), 0, st,
-                               a);
+            hipLaunchKernelGGL((attn_decode_kernel<D, 1, true>), dim3((unsigned)a.Mq, (unsigned)a.Hkv, 1u), dim3(256),
+                               0, st, a);
             return hipGetLastError() == hipSuccess ? 0 : -2;
         }
     }
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
-    hipLaunchKernelGGL((attn_decode_kernel<D, G>), grid, dim3(256), 0, st, a);
+    if (a.nsplit == 1) hipLaunchKernelGGL((attn_decode_kernel<D, G, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_decode_kernel<D, G, false>), grid, dim3(256), 0, st, a);
     if (a.nsplit > 1) {
         // one round of workgroups: 32-wide slices (one workgroup per CU: 256 VGPRs) while
         // they fit, else 64-wide (two per CU)

@@ -585,10 +585,11 @@ static int head(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st) {
     const t5g_config& c = e->c;
     const int d = c.hidden;
     RC(gemm(xn_rows, d, B, e->w.head1, d, d, 1, e->w.head1_bias, e->dhh, d, EPI_BIAS_GELU, st));
-    if (B <= 16 && d == 2304) {
-        // 65,541-row head on the register-resident-X GEMV (47.6 vs 54.4 us at 8 rows,
-        // tools/probe_head.py)
-        DecGemmArgs g = dec_args(B, e->w.head2, e->V, d, e->logits, e->logits_ld, 8);
+    if (B <= 32 && d == 2304) {
+        // 65,541-row head on the register-resident-X GEMV (tools/probe_head_nw.py: 48.8 vs
+        // 56.3 us at 8 rows, 58.6 vs 103.1 at 32); above 16 rows only 4 waves' partial sums
+        // (17 units x 2 tiles x 4 waves x 1 KiB) fit LDS
+        DecGemmArgs g = dec_args(B, e->w.head2, e->V, d, e->logits, e->logits_ld, B <= 16 ? 8 : 4);
         g.X = e->dhh;
         g.ldx = d;
         g.un = 8;

@@ -164,20 +164,26 @@ def test_gemv_register_x_variant(epi, M):
     assert torch.equal(got, torch.cat(parts)), "register-X rows differ from the LDS-staged kernel"
 
 
-@pytest.mark.parametrize("nw,M", [(12, 8), (12, 1), (12, 16), (9, 8), (6, 5), (4, 8)])
-def test_gemv_register_x_wave_counts(nw, M):
-    """layout 1 at other wave counts (the decode gate/up runs 12 waves at K = 2304): vs the
-    fp32 reference, and batch-invariant (every row bitwise equal to the same row alone)."""
+@pytest.mark.parametrize("nw,M,epi", [(12, 8, 3), (12, 1, 3), (12, 16, 3), (9, 8, 3), (6, 5, 3), (4, 8, 3),
+                                      (4, 32, 1), (4, 21, 1), (8, 16, 1)])
+def test_gemv_register_x_wave_counts(nw, M, epi):
+    """layout 1 at other wave counts (the decode gate/up runs 12 waves at K = 2304; the
+    65 541-row head 8 waves up to 16 rows, 4 waves -- the partial-sum buffer's LDS limit --
+    up to 32): vs the fp32 reference, and batch-invariant (every row bitwise equal to the
+    same row alone)."""
     _need_gpu()
-    N, K = 18432, 2304
+    N, K = (18432, 2304) if epi == 3 else (65541, 2304)
     g = torch.Generator(device="cpu").manual_seed(nw * 31 + M)
     W = (torch.randn(N, K, generator=g) * 0.02).to(BF16)
     X = torch.randn(M, K, generator=g).to(BF16)
-    got, _, _, bias = _run(3, M, N, K, nw, 1, seed=5, X=X, W=W, layout=1)
-    ref = _epilogue(X.float() @ W.float().t(), 3, bias)
-    assert (got - ref).abs().max() <= 2 ** -6 * ref.abs().max()
+    got, _, _, bias = _run(epi, M, N, K, nw, 1, seed=5, X=X, W=W, layout=1)
+    ref = _epilogue(X.float() @ W.float().t(), epi, bias)
+    if epi == 3:
+        assert (got - ref).abs().max() <= 2 ** -6 * ref.abs().max()
+    else:
+        _close_bf16(got, ref, frac=0.97)
     for m in sorted({0, M // 2, M - 1}):
-        one = _run(3, 1, N, K, nw, 1, seed=5, X=X[m:m + 1].contiguous(), W=W, layout=1)[0]
+        one = _run(epi, 1, N, K, nw, 1, seed=5, X=X[m:m + 1].contiguous(), W=W, layout=1)[0]
         assert torch.equal(one[0], got[m]), f"row {m} depends on the batch at nw={nw}"
 
 

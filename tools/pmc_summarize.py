@@ -16,7 +16,7 @@ OPS = {
                 "algorithmic": 2 * 9216 * 2304 * 2 + 8 * 2304 * 2 + 8 * 9216 * 2,
                 "what": "decode gate/up GEGLU GEMV, M=8, N=18432, K=2304 (tools/pmc_gateup.py: 26 weight sets "
                         "rotated, 2.2 GB > 256 MiB Infinity Cache)"},
-    "attention": {"kernels": ["attn_decode_kernel<256, 2>", "attn_pvc_kernel<256, 2, 32>"],
+    "attention": {"kernels": ["attn_decode_kernel<256, 2, false>", "attn_pvc_kernel<256, 2, 32>"],
                   "algorithmic": None,
                   "what": "decode self attention (scores + P.V/combine launches), 8 rows x 8/4 heads x 256, L ~ 527 "
                           "(tools/pmc_attention.py: 26 KV caches, 436 MB > 256 MiB Infinity Cache)"},
