@@ -7,6 +7,7 @@
 // are staged through LDS once per block while the first weight fragments are in flight.
 // Optional split-K over blockIdx.y writes fp32 slabs (EPI_F32) for the consumer to sum.
 // The decode step runs its gate/up projection here (engine.hip decoder_pass).
+#include <algorithm>
 #include "common.h"
 #include "t5g_kernels.h"
 
@@ -362,46 +363,57 @@ size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int rg) {
     return (size_t)umax * a.nw * 64 * 16 + (size_t)a.M * (per * 32 + 8) * sizeof(bf16_t);
 }
 
-// the register-resident-X kernel for the shapes it is instantiated for (8 waves sharing
-// each unit's K stream, SPU = 9 k-steps per wave: K = 2304, no split) -- 0 if launched
-template <int NW, int MT, int EPI>
+// the register-resident-X kernel for the shapes it is instantiated for: PER k-steps per
+// K slice (72: K = 2304 unsplit; 36: the down projection's K = 9216 in 8 slices), SPU =
+// PER / NW per wave -- 0 if launched. Split-K launches put cu_count / splits blocks on each
+// slice, so every block streams several units against one register-held X slice.
+template <int NW, int MT, int EPI, int PER>
 static int launch_rx_nw(const DecGemmArgs& a, hipStream_t st) {
-    constexpr int SPU = 72 / NW;
+    static_assert(PER % NW == 0, "whole k-step batches per wave");
+    constexpr int SPU = PER / NW;
     auto* fn = gemv_rx_kernel<NW, MT, EPI, SPU>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GD_LDS_MAX);
         attr = true;
     }
-    const int grid = gd_grid(a, 1);
+    const int cap = a.max_grid > 0 ? a.max_grid : cu_count();
+    const int grid = a.splits > 1 ? std::max(1, std::min(a.NG, cap / a.splits)) : gd_grid(a, 1);
     const size_t shm = (size_t)((a.NG + grid - 1) / grid) * MT * NW * 64 * 16;
     if (shm > GD_LDS_MAX) return -1;
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid, 1u), dim3(NW * 64), shm, st, a);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid, (unsigned)a.splits), dim3(NW * 64), shm, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
-// a.nw picks the waves sharing each unit's K stream (72 k-steps split evenly; the decode
-// gate/up runs 12: 17.9 vs 18.5 us for 8 at 8 rows, tools/probe_rx_nw.py)
-template <int MT, int EPI>
+// a.nw picks the waves sharing each unit's K stream (the PER k-steps split evenly; the
+// decode gate/up runs 12: 17.9 vs 18.5 us for 8 at 8 rows, tools/probe_rx_nw.py)
+template <int MT, int EPI, int PER>
 static int launch_rx(const DecGemmArgs& a, hipStream_t st) {
     switch (a.nw) {
-        case 4: return launch_rx_nw<4, MT, EPI>(a, st);
-        case 6: return launch_rx_nw<6, MT, EPI>(a, st);
-        case 9: return launch_rx_nw<9, MT, EPI>(a, st);
-        case 12: return launch_rx_nw<12, MT, EPI>(a, st);
-        default: return launch_rx_nw<8, MT, EPI>(a, st);
+        case 4: return launch_rx_nw<4, MT, EPI, PER>(a, st);
+        case 6: return launch_rx_nw<6, MT, EPI, PER>(a, st);
+        case 9: return launch_rx_nw<9, MT, EPI, PER>(a, st);
+        case 12: return launch_rx_nw<12, MT, EPI, PER>(a, st);
+        default:
+            if constexpr (PER % 8 == 0) return launch_rx_nw<8, MT, EPI, PER>(a, st);
+            else return -1;
     }
 }
 
 int gemv_rx(const DecGemmArgs& a, int epi, hipStream_t st) {
-    if (a.M <= 0 || a.M > 32 || a.KB != 72 || a.K != 2304 || a.splits > 1 || a.NG % 4 || a.NG * 16 < a.N) return -1;
+    if (a.M <= 0 || a.M > 32 || a.K != a.KB * 32 || a.NG % 4 || a.NG * 16 < a.N) return -1;
+    if (a.splits < 1 || a.KB % a.splits) return -1;
+    const int per = a.KB / a.splits;
+    // unsplit K = 2304 (any epilogue), or fp32 slabs of 36-k-step slices (K = 9216 / 8)
+    if (!(per == 72 && a.splits == 1) && !(per == 36 && a.splits > 1 && epi == EPI_F32)) return -1;
     if (!a.X || a.ldx < a.K || a.ldx % 8) return -1;
     if ((epi == EPI_BIAS_BF16 || epi == EPI_BIAS_GELU) && !a.bias) return -1;
     const bool two = a.M > 16;
     switch (epi) {
-        case EPI_BF16: return two ? launch_rx<2, EPI_BF16>(a, st) : launch_rx<1, EPI_BF16>(a, st);
-        case EPI_BIAS_BF16: return two ? launch_rx<2, EPI_BIAS_BF16>(a, st) : launch_rx<1, EPI_BIAS_BF16>(a, st);
-        case EPI_BIAS_GELU: return two ? launch_rx<2, EPI_BIAS_GELU>(a, st) : launch_rx<1, EPI_BIAS_GELU>(a, st);
-        case EPI_GEGLU: return two ? launch_rx<2, EPI_GEGLU>(a, st) : launch_rx<1, EPI_GEGLU>(a, st);
+        case EPI_BF16: return two ? launch_rx<2, EPI_BF16, 72>(a, st) : launch_rx<1, EPI_BF16, 72>(a, st);
+        case EPI_BIAS_BF16: return two ? launch_rx<2, EPI_BIAS_BF16, 72>(a, st) : launch_rx<1, EPI_BIAS_BF16, 72>(a, st);
+        case EPI_BIAS_GELU: return two ? launch_rx<2, EPI_BIAS_GELU, 72>(a, st) : launch_rx<1, EPI_BIAS_GELU, 72>(a, st);
+        case EPI_GEGLU: return two ? launch_rx<2, EPI_GEGLU, 72>(a, st) : launch_rx<1, EPI_GEGLU, 72>(a, st);
+        case EPI_F32: return two ? launch_rx<2, EPI_F32, 36>(a, st) : launch_rx<1, EPI_F32, 36>(a, st);
         default: return -1;
     }
 }

@@ -187,6 +187,24 @@ def test_gemv_register_x_wave_counts(nw, M, epi):
         assert torch.equal(one[0], got[m]), f"row {m} depends on the batch at nw={nw}"
 
 
+@pytest.mark.parametrize("nw,M", [(12, 8), (12, 32), (12, 19), (4, 8), (9, 1)])
+def test_gemv_register_x_split_k(nw, M):
+    """layout 1 over 8 k-slices of K = 9216 (the decode down projection: fp32 slabs, 32
+    blocks per slice each streaming several units): slab sum vs the fp32 reference, and
+    batch-invariant."""
+    _need_gpu()
+    N, K, S = 2304, 9216, 8
+    g = torch.Generator(device="cpu").manual_seed(nw * 7 + M)
+    W = (torch.randn(N, K, generator=g) * 0.02).to(BF16)
+    X = torch.randn(M, K, generator=g).to(BF16)
+    got = _run(4, M, N, K, nw, S, seed=5, X=X, W=W, layout=1)[0]
+    ref = X.float() @ W.float().t()
+    assert (got - ref).abs().max() <= 1e-5 * ref.abs().max()
+    for m in sorted({0, M // 2, M - 1}):
+        one = _run(4, 1, N, K, nw, S, seed=5, X=X[m:m + 1].contiguous(), W=W, layout=1)[0]
+        assert torch.equal(one[0], got[m]), f"row {m} depends on the batch at nw={nw}"
+
+
 @pytest.mark.parametrize("M", [8, 3, 16])
 def test_resid_norm_vs_fp32(M):
     """The decode step's residual + RMSNorm kernel (t5g_resid_norm; norm.hip): against a
