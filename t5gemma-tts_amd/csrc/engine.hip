@@ -460,6 +460,22 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         n.normed_out = xn;
         return resid_norm(n, st);
     };
+    // attention output projection into the norm's fp32 slabs: at the 2b-2b width (K = 2048,
+    // 4 slices of 16 k-steps) on the register-resident-X GEMV for every batch size up to 32,
+    // so a row's sums never depend on the batch (tools/probe_proj_rx.py: 4.13 vs 4.23 us at
+    // 8 rows, 5.2 vs 6.8 at 32)
+    auto out_proj = [&](const bf16_t* x, const void* W) -> int {
+        if (decode && M <= 32 && d == 2304 && e->q_dim == 2048 && s_o == 4) {
+            DecGemmArgs g = dec_args(M, W, d, e->q_dim, e->part, d, 8);
+            g.X = x;
+            g.ldx = e->q_dim;
+            g.splits = s_o;
+            g.layout_rx = 1;
+            return gemv_dec(g, EPI_F32, st);
+        }
+        return gemm(x, e->q_dim, M, W, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
+                    s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode);
+    };
     auto rope_args = [&]() {
         RopeArgs r;
         memset(&r, 0, sizeof(r));
@@ -516,8 +532,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             RC(rope_store(r, st));
             RC(attn_packed(e, M, q, tok_row, tok_t, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1, win, att, st));
         }
-        RC(gemm(att, e->q_dim, M, L.o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
-                s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode));
+        RC(out_proj(att, L.o));
         RC(resid(s_o, L.norms[1], L.norms[2]));
         // --- PM cross attention (q rotated by the decoder progress, :149-165)
         if (decode && !eager) {
@@ -534,8 +549,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             RC(rope_store(r, st));
             RC(attn_packed(e, M, q, tok_row, tok_t, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, st));
         }
-        RC(gemm(att, e->q_dim, M, L.cross_o, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
-                s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode));
+        RC(out_proj(att, L.cross_o));
         RC(resid(s_o, L.norms[3], L.norms[4]));
         // --- GeGLU MLP (decode: the one-block-per-CU GEMV; register-resident X at the
         // 2b-2b width, up to 32 rows)
@@ -597,10 +611,11 @@ static int head(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st) {
     const int d = c.hidden;
     RC(gemm(xn_rows, d, B, e->w.head1, d, d, 1, e->w.head1_bias, e->dhh, d, EPI_BIAS_GELU, st));
     if (B <= 32 && d == 2304) {
-        // 65,541-row head on the register-resident-X GEMV (tools/probe_head_nw.py: 48.8 vs
-        // 56.3 us at 8 rows, 58.6 vs 103.1 at 32); above 16 rows only 4 waves' partial sums
-        // (17 units x 2 tiles x 4 waves x 1 KiB) fit LDS
-        DecGemmArgs g = dec_args(B, e->w.head2, e->V, d, e->logits, e->logits_ld, B <= 16 ? 8 : 4);
+        // 65,541-row head on the register-resident-X GEMV (tools/probe_head_nw.py: 50.3 vs
+        // 56.3 us at 8 rows, 58.6 vs 103.1 at 32). 4 waves at every batch size: above 16 rows
+        // only 4 waves' partial sums (17 units x 2 tiles x 4 waves x 1 KiB) fit LDS, and one
+        // wave count keeps a row's logits independent of the batch
+        DecGemmArgs g = dec_args(B, e->w.head2, e->V, d, e->logits, e->logits_ld, 4);
         g.X = e->dhh;
         g.ldx = d;
         g.un = 8;

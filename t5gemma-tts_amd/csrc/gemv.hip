@@ -364,7 +364,8 @@ size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int rg) {
 }
 
 // the register-resident-X kernel for the shapes it is instantiated for: PER k-steps per
-// K slice (72: K = 2304 unsplit; 36: the down projection's K = 9216 in 8 slices), SPU =
+// K slice (72: K = 2304 unsplit; 36: the down projection's K = 9216 in 8 slices; 8 / 16 /
+// 18 / 32: the attention projections' slices), SPU =
 // PER / NW per wave -- 0 if launched. Split-K launches put cu_count / splits blocks on each
 // slice, so every block streams several units against one register-held X slice.
 template <int NW, int MT, int EPI, int PER>
@@ -389,13 +390,22 @@ static int launch_rx_nw(const DecGemmArgs& a, hipStream_t st) {
 template <int MT, int EPI, int PER>
 static int launch_rx(const DecGemmArgs& a, hipStream_t st) {
     switch (a.nw) {
-        case 4: return launch_rx_nw<4, MT, EPI, PER>(a, st);
-        case 6: return launch_rx_nw<6, MT, EPI, PER>(a, st);
-        case 9: return launch_rx_nw<9, MT, EPI, PER>(a, st);
-        case 12: return launch_rx_nw<12, MT, EPI, PER>(a, st);
-        default:
-            if constexpr (PER % 8 == 0) return launch_rx_nw<8, MT, EPI, PER>(a, st);
-            else return -1;
+        case 4: if constexpr (PER % 4 == 0) return launch_rx_nw<4, MT, EPI, PER>(a, st); else return -1;
+        case 6: if constexpr (PER % 6 == 0) return launch_rx_nw<6, MT, EPI, PER>(a, st); else return -1;
+        case 9: if constexpr (PER % 9 == 0) return launch_rx_nw<9, MT, EPI, PER>(a, st); else return -1;
+        case 12: if constexpr (PER % 12 == 0) return launch_rx_nw<12, MT, EPI, PER>(a, st); else return -1;
+        default: if constexpr (PER % 8 == 0) return launch_rx_nw<8, MT, EPI, PER>(a, st); else return -1;
+    }
+}
+template <int MT>
+static int launch_rx_slabs(const DecGemmArgs& a, int per, hipStream_t st) {
+    switch (per) {
+        case 8: return launch_rx<MT, EPI_F32, 8>(a, st);
+        case 16: return launch_rx<MT, EPI_F32, 16>(a, st);
+        case 18: return launch_rx<MT, EPI_F32, 18>(a, st);
+        case 32: return launch_rx<MT, EPI_F32, 32>(a, st);
+        case 36: return launch_rx<MT, EPI_F32, 36>(a, st);
+        default: return -1;
     }
 }
 
@@ -403,8 +413,9 @@ int gemv_rx(const DecGemmArgs& a, int epi, hipStream_t st) {
     if (a.M <= 0 || a.M > 32 || a.K != a.KB * 32 || a.NG % 4 || a.NG * 16 < a.N) return -1;
     if (a.splits < 1 || a.KB % a.splits) return -1;
     const int per = a.KB / a.splits;
-    // unsplit K = 2304 (any epilogue), or fp32 slabs of 36-k-step slices (K = 9216 / 8)
-    if (!(per == 72 && a.splits == 1) && !(per == 36 && a.splits > 1 && epi == EPI_F32)) return -1;
+    // unsplit K = 2304 (any epilogue), or fp32 slabs of 8 / 16 / 18 / 32 / 36-k-step
+    // slices (the decode projections' split-K shapes)
+    if (!(per == 72 && a.splits == 1) && !(a.splits > 1 && epi == EPI_F32)) return -1;
     if (!a.X || a.ldx < a.K || a.ldx % 8) return -1;
     if ((epi == EPI_BIAS_BF16 || epi == EPI_BIAS_GELU) && !a.bias) return -1;
     const bool two = a.M > 16;
@@ -413,7 +424,7 @@ int gemv_rx(const DecGemmArgs& a, int epi, hipStream_t st) {
         case EPI_BIAS_BF16: return two ? launch_rx<2, EPI_BIAS_BF16, 72>(a, st) : launch_rx<1, EPI_BIAS_BF16, 72>(a, st);
         case EPI_BIAS_GELU: return two ? launch_rx<2, EPI_BIAS_GELU, 72>(a, st) : launch_rx<1, EPI_BIAS_GELU, 72>(a, st);
         case EPI_GEGLU: return two ? launch_rx<2, EPI_GEGLU, 72>(a, st) : launch_rx<1, EPI_GEGLU, 72>(a, st);
-        case EPI_F32: return two ? launch_rx<2, EPI_F32, 36>(a, st) : launch_rx<1, EPI_F32, 36>(a, st);
+        case EPI_F32: return two ? launch_rx_slabs<2>(a, per, st) : launch_rx_slabs<1>(a, per, st);
         default: return -1;
     }
 }

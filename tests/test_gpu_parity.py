@@ -430,6 +430,38 @@ def test_mid_width_teacher_forced():
     print(f"mid: free-running token-exact vs reference {n_exact}/{len(cases)}")
 
 
+def test_mid_width_batch32_rows_equal_single_rows():
+    """True 2b-2b widths (2+2 layers), where the decode step runs the register-resident-X
+    GEMVs (gate/up, down, o / cross-o, the 65 541-row head) and the 17..32-row GEMM: every
+    kernel choice keeps a row's sums independent of the batch, so rows of a 32-row batch
+    equal the same utterances run alone and in a batch of 8 (tokens and logits bitwise)."""
+    _need_gpu()
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import SamplingParams, Utterance
+    from t5gemma_tts_amd.weights import synthetic_weights
+    meta, _ = _load("golden_mid")
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    eng = _engine(cfg, sd, max_batch=32, max_text=64, max_audio=128, max_gen=48)
+    rng = np.random.default_rng(5)
+    utts = []
+    for b in range(32):
+        x = rng.integers(3, 4000, size=int(rng.integers(4, 40))).tolist()   # mid: 4 096 text ids
+        tp = int(rng.integers(0, 40))
+        y = rng.integers(0, 65536, size=tp).tolist() + ([cfg.y_sep_token] if tp else [])
+        utts.append(Utterance(x=x, y=y, tgt_y_len=len(y) + int(rng.integers(8, 24))))
+    p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
+    seeds = list(range(200, 232))
+    batch = eng.generate(utts, p, seeds=seeds, parity=True, record_logits=True)
+    for rows in ([0], [31], list(range(8, 16))):
+        part = eng.generate([utts[b] for b in rows], p, seeds=[seeds[b] for b in rows], parity=True,
+                            record_logits=True)
+        for i, b in enumerate(rows):
+            assert part["gen"][i].tolist() == batch["gen"][b].tolist(), b
+            for t in range(min(len(part["logits"]), len(part["gen"][i]))):   # the row's own steps
+                assert torch.equal(part["logits"][t][i], batch["logits"][t][b]), (b, t)
+
+
 def test_sampler_kernel_vs_reference_golden():
     """On-device sampler on the reference's sampler golden cases (V = 65541)."""
     _need_gpu()
