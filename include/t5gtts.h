@@ -206,11 +206,13 @@ int t5g_time_gemm(const void* X_dev, int32_t ldx, int32_t M, const void* const* 
                   float* avg_us);
 int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, float* avg_us);
 
-/* Decode-step GEMV (csrc/gemv.hip; M <= 16 rows): Y = X . W^T on a packed W with
- * epilogue epi (as t5g_gemm: 0 bf16, 1 +bias bf16, 3 GeGLU(tanh), 4 fp32 split-K slabs),
- * X rows staged through LDS, at most one workgroup per CU -- the kernel the decode step
- * runs its gate/up projection on ([tf] T5GemmaMLP :81-97). Fields marked "reserved" must
- * be 0 / NULL (the fused-prologue variants measured slower in round 1 were removed). */
+/* Decode-step GEMV (csrc/gemv.hip): Y = X . W^T on a packed W with epilogue epi (as
+ * t5g_gemm: 0 bf16, 1 +bias bf16, 3 GeGLU(tanh), 4 fp32 split-K slabs), at most one
+ * workgroup per CU per k-slice -- the kernels the decode step runs its gate/up and down
+ * projections ([tf] T5GemmaMLP :81-97), attention output projections ([tf] :264-304,
+ * PMCrossAttention :167-253) and 65 541-row head (predict_layer :469-478) on. Fields
+ * marked "reserved" must be 0 / NULL (the fused-prologue variants measured slower in
+ * round 1 were removed). */
 typedef struct {
     int32_t M, K, N;
     int32_t epi, pro, nw;     /* pro: reserved (0); nw: waves per block -- layout 0: 4 / 8 / 16
@@ -233,7 +235,9 @@ typedef struct {
     int32_t max_grid;         /* tuning: blocks per launch cap, 0 = one per CU */
     int32_t splits;           /* split-K (epi 4): fp32 slabs [splits][M][ldy]; 0/1 = none */
     int32_t layout;           /* 0: the LDS-staged-X GEMV (M <= 16); 1: the register-resident-X
-                                 GEMV (M <= 32, K = 2304, no split); W packed P16 either way */
+                                 GEMV (M <= 32; K / 32 k-steps per slice = 72 unsplit, or epi 4
+                                 with 8 / 16 / 18 / 32 / 36 per slice, nw dividing it); W packed
+                                 P16 either way; -1 for any other shape */
 } t5g_gemv_args;
 int t5g_gemv(const t5g_gemv_args* args, void* stream);
 /* The decode step's residual + RMSNorm pair on caller buffers (norm.hip, [tf] T5GemmaRMSNorm
