@@ -336,6 +336,9 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     const int c0 = lo + sp * DCH;
     const int c1 = min(hi, c0 + DCH);
     const int n = c1 - c0;
+    // chunks past the row (the grid covers the cache capacity) leave before any request:
+    // they publish nothing, and the block holding t always has keys
+    if (n <= 0) return;
     // the block whose keys include t appends the step's own key/value (a.append)
     const bool has_t = a.append && a.Qpart && t >= c0 && t < c1;
     // head_split > 1 (single-chunk rows, no append: cross attention): blockIdx.y is a q
