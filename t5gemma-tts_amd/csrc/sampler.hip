@@ -565,6 +565,12 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
 // st_sc1 / ld_sc1 (common.h): the fast path's cross-block candidate hand-off
 
 constexpr int FT = 256;
+// The candidate hand-off below (sc1 write-through stores, a drained vmcnt, one relaxed
+// agent-scope ticket add, sc1 loads by the last block) is the gfx950 form of the CDNA
+// guide's G16 pattern; another target's cache / counter model would need acquire-release.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "sampler_fast_kernel's cross-block hand-off is written for gfx950"
+#endif
 __device__ __forceinline__ bool lane_ok(int t) { return t < FS_NB; }
 constexpr int FEPT = 24;   // V <= FS_NB * FT * FEPT = 98304
 
