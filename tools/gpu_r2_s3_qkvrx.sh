@@ -1,4 +1,5 @@
-# Probe: qkv projection on the split-K register-X GEMV (T5G_QKV_RX=1) vs the tiled GEMM:
+# Probe (recorded in profiles/r02_probe_qkv_rx.txt): qkv projection on the split-K register-X GEMV
+# (T5G_QKV_RX=1, a switch removed from engine.hip after this run) vs the tiled GEMM.
 # C3 and C5 benches and the C3 step timeline for both.
 source tools/gpu_run.sh
 export TMPDIR=/tmp
