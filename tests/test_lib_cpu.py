@@ -69,3 +69,25 @@ def test_host_sampler_matches_reference_golden():
         assert rc == 0
         assert tok.value == c["token"], c
         assert out.cur_num_gen == 101 and out.prev_token == c["token"]
+
+
+@pytest.mark.parametrize("layout,M,K,splits,epi,nw", [
+    (1, 33, 2304, 1, 3, 12),    # register-X: at most 32 rows
+    (1, 8, 2304, 2, 3, 12),     # split K only into fp32 slabs
+    (1, 8, 2048, 1, 4, 8),      # unsplit slices must be 72 k-steps
+    (1, 8, 9216, 8, 4, 8),      # 36-k-step slices: nw must divide 36
+    (1, 8, 9216, 3, 4, 12),     # 96-k-step slices: not instantiated
+    (1, 8, 2304, 5, 4, 4),      # 72 k-steps do not split in 5
+    (0, 17, 2304, 1, 3, 8),     # LDS-staged X: at most 16 rows
+    (2, 8, 2304, 1, 3, 8),      # no third layout
+])
+def test_gemv_rejects_unsupported_shapes(layout, M, K, splits, epi, nw):
+    """t5g_gemv validates on the host and returns an error code before any launch for the
+    shapes its kernels are not built for (csrc/gemv.hip gemv_rx / gemv_dec)."""
+    from t5gemma_tts_amd import _lib
+    L = _lib.lib()
+    a = _lib.GemvArgs()
+    a.M, a.K, a.N, a.epi, a.pro, a.nw, a.un = M, K, 2304, epi, 0, nw, 8
+    a.X, a.ldx, a.Y, a.ldy, a.splits, a.layout, a.max_grid = 16, K, 16, 2304, splits, layout, 0
+    a.W = 16   # never dereferenced: every case is rejected before a launch
+    assert L.t5g_gemv(C.byref(a), None) < 0
