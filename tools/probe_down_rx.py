@@ -17,7 +17,8 @@ def main():
     L = _lib.lib()
     dev = torch.device("cuda:0")
     st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    N, K, S = 2304, 9216, 8
+    N, K = 2304, 9216
+    S = int(os.environ.get("PROBE_SPLITS", "8"))
     n_w = max(2, -(-600_000_000 // (N * K * 2)))
     g = torch.Generator(device=dev).manual_seed(7)
     Ws = []
@@ -37,8 +38,8 @@ def main():
                                    C.c_void_p(Y.data_ptr()), N, 4, 200, st, C.byref(us)), "gemm")
         _lib.check(L.t5g_gemm(C.c_void_p(X.data_ptr()), K, M, C.c_void_p(Ws[0].data_ptr()), N, K, S, None,
                               C.c_void_p(Y.data_ptr()), N, 4, st), "gemm1")
-        row = {"op": "down", "M": M, "gemm_us": round(us.value, 2)}
-        for nw in (4, 6, 9, 12):
+        row = {"op": "down", "splits": S, "M": M, "gemm_us": round(us.value, 2)}
+        for nw in ((4, 6, 9, 12) if S == 8 else (4, 6, 8, 9, 12)):
             for mg in (0, 512):
                 a = _lib.GemvArgs()
                 a.M, a.K, a.N, a.epi, a.pro, a.nw, a.un = M, K, N, 4, 0, nw, 8
