@@ -235,3 +235,22 @@ def test_resid_norm_vs_fp32(M):
         ulp = ref.float().abs().clamp(min=2.0 ** -20) * 2 ** -7
         assert (diff <= 2 * ulp).all(), diff.max()
         assert (diff == 0).float().mean() > 0.95
+
+
+@pytest.mark.parametrize("epi,K,splits,nw,M,caps", [(3, 2304, 1, 12, 8, (200, 100)),
+                                                    (4, 9216, 8, 12, 32, (96 * 8, 40 * 8)),
+                                                    (4, 2048, 4, 8, 8, (96 * 4, 40 * 4)),
+                                                    (1, 2304, 1, 4, 24, (241, 230))])
+def test_gemv_register_x_grid_invariant(epi, K, splits, nw, M, caps):
+    """The register-X GEMV's results do not depend on how many blocks share the units (a
+    unit's sums are one block's fixed wave order): bitwise equal at the default grid (one
+    block per CU per slice) and at capped grids, e.g. a partitioned GPU with fewer CUs."""
+    _need_gpu()
+    N = 18432 if epi == 3 else (65541 if epi == 1 else 2304)
+    g = torch.Generator(device="cpu").manual_seed(K + splits + M)
+    W = (torch.randn(N, K, generator=g) * 0.02).to(BF16)
+    X = torch.randn(M, K, generator=g).to(BF16)
+    base = _run(epi, M, N, K, nw, splits, seed=9, X=X, W=W, layout=1)[0]
+    for cap in caps:   # units per block stay within the partial-sum buffer's LDS
+        got = _run(epi, M, N, K, nw, splits, seed=9, X=X, W=W, layout=1, max_grid=cap)[0]
+        assert torch.equal(got, base), f"max_grid {cap}"
