@@ -1,4 +1,5 @@
 # Probe: prefill GEMM register ring depth S = 2 / 4 / 6 / 8 (one library per depth).
+# (tools/bin is listed in .gpurunignore since this ran: drop that line to run it again)
 source tools/gpu_run.sh
 export TMPDIR=/tmp
 for S in 2 4 6 8; do
