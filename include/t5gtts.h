@@ -273,6 +273,37 @@ int64_t t5g_attention_decode_work_bytes(int32_t B, int32_t n_heads, int32_t n_kv
                                         int32_t cap);
 int t5g_attention_decode(const t5g_attn_decode_args* args, void* stream);
 
+/* --- parity mode (csrc/exact.hip) ------------------------------------------------
+ * Switch an engine to the exact-order kernels: every Linear, RMSNorm mean, q.k / P.V of
+ * attention and GELU computed in the accumulation order of the reference's own CPU run
+ * (torch 2.10 CPU bf16: oneDNN AMX F.linear, aten SDPA + oneDNN gemv / gemm, aten AVX2
+ * sum; measured on the machine the golden vectors come from), so that
+ * logits -- and with the reference's noise stream, token ids -- are the reference's bit
+ * for bit. Replaces the bf16 linears of modeling_t5gemma_voice.py:469-478 / [tf]
+ * modeling_t5gemma.py:81-97, 264-304, PMCrossAttention :167-253 and the RMSNorm of [tf]
+ * :61-78 inside t5g_encode / t5g_prefill / t5g_decode. gelu_lut: bf16 -> bf16 nn.GELU()
+ * (erf) of the reference host, 65 536 entries indexed by the input bits (NULL: the
+ * exact-erf form, equal except on 24 inputs in [-4.4, -3.1]); threads: the reference
+ * host's torch thread count (8, the only measured K-split table; others -> EUNSUPPORTED).
+ * enable = 0 returns to the fast kernels. Per-utterance token counts (text, prompt + 1)
+ * must not exceed 512 in parity mode (the measured table). Synchronous. */
+int t5g_engine_set_exact(t5g_engine* e, int32_t enable, const uint16_t* gelu_lut, int32_t threads);
+/* Single exact-order Linear on caller buffers (parity tests): Y = X . W^T on a packed W in
+ * the reference's order (32-element E/O chunk chains, chunk sums folded; K split into
+ * parts of kb32 * 32 elements, kb32 = 0: no split; bias last). epi as t5g_gemm
+ * (0 bf16, 1 +bias bf16, 2 +bias GELU(erf) via gelu_lut, 3 GeGLU(tanh), 4 fp32 unrounded). */
+int t5g_exact_linear(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K,
+                     int32_t kb32, const void* bias_dev, const void* gelu_lut_dev, void* Y_dev, int32_t ldy,
+                     int32_t epi, void* stream);
+/* Single exact-order SDPA call on caller buffers (parity tests): one reference call per row b
+ * with q_len[b] queries (q rows packed, q_row / q_pos per query) over kv_len[b] keys of a
+ * [B][n_kv_heads][cap][head_dim] cache, torch 2.10 CPU flash-attention numerics incl. its
+ * GEMM selection (gemv / unpacked / packed, threads = the reference thread count). */
+int t5g_exact_attention(const void* q_dev, int32_t Mq, const int32_t* q_row_dev, const int32_t* q_pos_dev,
+                        const int32_t* q_len_dev, const void* k_cache_dev, const void* v_cache_dev, int32_t cap,
+                        const int32_t* kv_len_dev, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
+                        int32_t causal, int32_t window, float scale, int32_t threads, void* out_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -118,7 +118,33 @@ SIGNATURES = {
     "t5g_time_gemv": (C.c_int, [C.POINTER(GemvArgs), C.POINTER(_P), _I, _I, _P, C.POINTER(_F)]),
     "t5g_attention_decode_work_bytes": (_L, [_I, _I, _I, _I, _I]),
     "t5g_attention_decode": (C.c_int, [C.POINTER(AttnDecodeArgs), _P]),
+    "t5g_engine_set_exact": (C.c_int, [_P, _I, _P, _I]),
+    "t5g_exact_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
+    "t5g_exact_attention": (C.c_int, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
 }
+
+# parity mode: the reference host's bf16 nn.GELU() (erf) table (tools/cpu_order/make_gelu_table.py)
+GELU_ERF_TABLE = os.path.join(_PKG, "data", "gelu_erf_bf16.bin")
+_gelu_tab = None
+
+
+def gelu_erf_table():
+    """(ctypes uint16 array of 65 536 entries) the reference host's GELU on every bf16 input."""
+    global _gelu_tab
+    if _gelu_tab is None:
+        if not os.path.exists(GELU_ERF_TABLE):
+            raise RuntimeError(f"parity-mode GELU table missing: {GELU_ERF_TABLE}")
+        raw = open(GELU_ERF_TABLE, "rb").read()
+        if len(raw) != 65536 * 2:
+            raise RuntimeError(f"{GELU_ERF_TABLE}: {len(raw)} bytes, expected 131072")
+        _gelu_tab = (C.c_uint16 * 65536).from_buffer_copy(raw)
+    return _gelu_tab
+
+
+# the K-split table of the reference host's F.linear was measured for this many threads
+# and per-utterance token counts up to EXACT_MAX_TOKENS (csrc/ref_ksplit.h)
+EXACT_THREADS = 8
+EXACT_MAX_TOKENS = 512
 
 _lib = None
 

@@ -16,10 +16,14 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "lib", "libt5gtts.so")
-SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "xc2.hip", "xc2enc.hip", "whisper.hip", "host_sampler.cpp"]
-HEADERS = ["common.h", "t5g_kernels.h", "xc2_common.h"]
+SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "exact.hip", "xc2.hip", "xc2enc.hip", "whisper.hip", "host_sampler.cpp"]
+HEADERS = ["common.h", "t5g_kernels.h", "xc2_common.h", "exact_math.h", "ref_ksplit.h"]
 ARCH = os.environ.get("T5G_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+# -ffp-contract=off: HIP's default (fast-honor-pragmas) fuses a*b+c into one fma even
+# through __fmul_rn / __fsub_rn, which changes roundings the reference's CPU kernels keep
+# separate (e.g. aten's fast exp: x*log2e is rounded before floor / subtract). Every fma
+# the kernels want is written explicitly (fmaf, MFMA).
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result", "-ffp-contract=off",
          "-I", os.path.join(REPO, "include")]
 
 

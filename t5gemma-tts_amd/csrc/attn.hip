@@ -13,6 +13,7 @@
 // O / sum rounded once); ``eager`` mirrors eager_attention_forward (bf16 scores,
 // tanh softcap, bf16-rounded normalised probabilities).
 #include "common.h"
+#include "exact_math.h"
 #include "t5g_kernels.h"
 
 namespace t5g {
@@ -63,8 +64,8 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
             sn = a.rope_tab[(long)row * D + H2 + i];
         } else {
             const float ang = a.inv_freq[i] * a.pos[m];
-            c = rbf(cosf(ang));
-            sn = rbf(sinf(ang));
+            c = rbf(a.exact_trig ? t5g_exact::rope_cos(ang) : cosf(ang));
+            sn = rbf(a.exact_trig ? t5g_exact::rope_sin(ang) : sinf(ang));
         }
         o1 = rbf(rbf(x1 * c) + rbf(-x2 * sn));
         o2 = rbf(rbf(x2 * c) + rbf(x1 * sn));

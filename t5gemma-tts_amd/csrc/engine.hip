@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/t5gtts.h"
+#include "ref_ksplit.h"
 #include "t5g_kernels.h"
 
 using namespace t5g;
@@ -89,6 +90,11 @@ struct t5g_engine {
     int graph_B = -1;
     hipStream_t graph_stream = nullptr;
     hipStream_t cap_stream = nullptr;
+    // parity mode (t5g_engine_set_exact): every sum in the reference host's CPU order
+    bool exact = false;
+    int exact_threads = REF_KSPLIT_THREADS;
+    uint16_t* ksplit_dev = nullptr;     // ref_ksplit.h tables [REF_KSPLIT_NSHAPES][REF_KSPLIT_MAX_M]
+    uint16_t* gelu_lut_dev = nullptr;   // [65536] bf16 -> bf16 nn.GELU() of the reference host
 };
 
 template <typename T>
@@ -288,6 +294,285 @@ static int attn_packed(t5g_engine* e, int ntok, const bf16_t* q, const int* tok_
     return attention(a, st);
 }
 
+// ---------------------------------------------------------------------------
+// Parity mode: the same phases on the exact-order kernels (exact.hip, norm.hip EXACT),
+// unfused, with every tensor rounded where the reference's bf16 tensor ops round it.
+static const uint16_t* ksplit_tab(const t5g_engine* e, int N, int K) {
+    if (!e->ksplit_dev) return nullptr;
+    for (int i = 0; i < REF_KSPLIT_NSHAPES; ++i)
+        if (ref_ksplit_shapes[i].N == N && ref_ksplit_shapes[i].K == K) return e->ksplit_dev + (long)i * REF_KSPLIT_MAX_M;
+    return nullptr;   // shapes never split by the reference host (K <= 256 in the probes)
+}
+
+// nref_a / nref_b: the reference Linear's output width for packed columns < / >= nsplit_col
+// (q | k,v share one packed matrix here but are separate F.linear calls there)
+static int xlin(t5g_engine* e, const bf16_t* X, int ldx, int M, const void* W, int N, int K, const void* bias,
+                void* Y, int ldy, int epi, const int* tok_row, const int* row_len, int nref_a, int nref_b,
+                int nsplit_col, hipStream_t st) {
+    ExactLinArgs a;
+    memset(&a, 0, sizeof(a));
+    a.X = X;
+    a.ldx = ldx;
+    a.M = M;
+    a.W = (const bf16_t*)W;
+    a.N = N;
+    a.NG = ng_pad(N);
+    a.KB = K / 32;
+    a.bias = (const bf16_t*)bias;
+    a.Y = Y;
+    a.ldy = ldy;
+    a.tok_row = tok_row;
+    a.row_len = row_len;
+    a.kb_a = ksplit_tab(e, nref_a, K);
+    a.kb_b = nref_b ? ksplit_tab(e, nref_b, K) : nullptr;
+    a.nsplit_col = nsplit_col;
+    a.kb_len = REF_KSPLIT_MAX_M;
+    a.gelu_lut = e->gelu_lut_dev;
+    return exact_linear(a, epi, st);
+}
+
+static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const int* q_pos, const int* q_len,
+                 const bf16_t* K, const bf16_t* Vc, int cap, const int* kv_len, int causal, int window, bf16_t* O,
+                 hipStream_t st) {
+    const t5g_config& c = e->c;
+    ExactAttnArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Q = Q;
+    a.ldq = e->q_dim;
+    a.Mq = Mq;
+    a.q_row = q_row;
+    a.q_pos = q_pos;
+    a.q_len = q_len;
+    a.K = K;
+    a.V = Vc;
+    a.kv_hstride = (long)cap * c.head_dim;
+    a.kv_bstride = a.kv_hstride * c.n_kv_heads;
+    a.kv_len = kv_len;
+    a.Hq = c.n_heads;
+    a.Hkv = c.n_kv_heads;
+    a.D = c.head_dim;
+    a.causal = causal;
+    a.window = window;
+    a.scale = c.attn_scale;
+    a.threads = e->exact_threads;
+    a.O = O;
+    a.ldo = e->q_dim;
+    return exact_attention(a, st);
+}
+
+static NormArgs xnorm_args(int M, int d, float eps) {
+    NormArgs n;
+    memset(&n, 0, sizeof(n));
+    n.M = M;
+    n.d = d;
+    n.eps = eps;
+    n.exact = 1;
+    return n;
+}
+
+static RopeArgs xrope_args(int M, int D, const float* pos, const float* inv_freq, const int* tok_row, const int* tok_t,
+                           const int* kv_len) {
+    RopeArgs r;
+    memset(&r, 0, sizeof(r));
+    r.M = M;
+    r.D = D;
+    r.pos = pos;
+    r.inv_freq = inv_freq;
+    r.tok_row = tok_row;
+    r.tok_t = tok_t;
+    r.kv_len = kv_len;
+    r.exact_trig = 1;
+    return r;
+}
+
+static int encode_exact(t5g_engine* e, int ntok, const int32_t* ids, const int32_t* tok_row, const int32_t* tok_t,
+                        const float* pos, hipStream_t st) {
+    const t5g_config& c = e->c;
+    const int d = c.hidden, f = c.intermediate, D = c.head_dim;
+    const int* rl = e->enc_len;   // the reference encodes one utterance: M = its text length
+    for (int l = 0; l < c.n_enc_layers; ++l) {
+        const t5g_layer_weights& L = e->enc[l];
+        NormArgs n = xnorm_args(ntok, d, c.rms_eps);
+        if (l == 0) {
+            n.ids = ids;
+            n.table = (const bf16_t*)e->w.enc_embed;
+            n.n_table = c.text_vocab;
+            n.scale = c.normalizer;
+        } else {
+            n.delta = e->tmp;
+            n.post_w = (const bf16_t*)e->enc[l - 1].norms[5];
+            n.resid = e->h;
+        }
+        n.pre_w = (const bf16_t*)L.norms[0];
+        n.resid_out = e->h;
+        n.normed_out = e->xn;
+        RC(resid_norm(n, st));
+        RC(xlin(e, e->xn, d, ntok, L.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, EPI_BF16, tok_row, rl, e->q_dim,
+                e->kv_dim, e->q_dim, st));
+        RopeArgs r = xrope_args(ntok, D, pos, e->w.inv_freq, tok_row, tok_t, nullptr);
+        r.X = e->qkv;
+        r.ldx = e->qkv_dim;
+        r.nq = c.n_heads;
+        r.nk = r.nv = c.n_kv_heads;
+        r.rope_q = r.rope_k = 1;
+        r.Qout = e->q;
+        r.ldq = e->q_dim;
+        r.Kc = e->enc_k;
+        r.Vc = e->enc_v;
+        r.c_hstride = (long)c.max_text * D;
+        r.c_bstride = r.c_hstride * c.n_kv_heads;
+        RC(rope_store(r, st));
+        RC(xattn(e, e->q, ntok, tok_row, tok_t, rl, e->enc_k, e->enc_v, c.max_text, rl, 0,
+                 c.enc_sliding[l] ? c.sliding_window : 0, e->att, st));
+        RC(xlin(e, e->att, e->q_dim, ntok, L.o, d, e->q_dim, nullptr, e->tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+        n = xnorm_args(ntok, d, c.rms_eps);
+        n.delta = e->tmp;
+        n.post_w = (const bf16_t*)L.norms[1];
+        n.resid = e->h;
+        n.pre_w = (const bf16_t*)L.norms[4];
+        n.resid_out = e->h;
+        n.normed_out = e->xn;
+        RC(resid_norm(n, st));
+        RC(xlin(e, e->xn, d, ntok, L.gate_up, 2 * f, d, nullptr, e->act, f, EPI_GEGLU, tok_row, rl, f, 0, 0, st));
+        RC(xlin(e, e->act, f, ntok, L.down, d, f, nullptr, e->tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+    }
+    NormArgs n = xnorm_args(ntok, d, c.rms_eps);
+    n.delta = e->tmp;
+    n.post_w = (const bf16_t*)e->enc[c.n_enc_layers - 1].norms[5];
+    n.resid = e->h;
+    n.pre_w = (const bf16_t*)e->w.enc_final_norm;
+    n.resid_out = e->h;
+    n.normed_out = e->mem;
+    RC(resid_norm(n, st));
+    for (int l = 0; l < c.n_dec_layers; ++l) {
+        RC(xlin(e, e->mem, d, ntok, e->dec[l].cross_kv, 2 * e->kv_dim, d, nullptr, e->qkv, 2 * e->kv_dim, EPI_BF16,
+                tok_row, rl, e->kv_dim, e->kv_dim, e->kv_dim, st));
+        RopeArgs r = xrope_args(ntok, D, pos, e->w.inv_freq, tok_row, tok_t, nullptr);
+        r.X = e->qkv;
+        r.ldx = 2 * e->kv_dim;
+        r.nk = r.nv = c.n_kv_heads;
+        r.rope_k = 1;
+        r.Kc = e->ck[l];
+        r.Vc = e->cv[l];
+        r.c_hstride = (long)c.max_text * D;
+        r.c_bstride = r.c_hstride * c.n_kv_heads;
+        RC(rope_store(r, st));
+    }
+    return T5G_OK;
+}
+
+// decode: M = B rows fed by the sampler buffers (the reference's M = 1 per call);
+// prefill: M packed tokens, the reference's M = the row's token count (kv_len)
+static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* tok_row, const int* tok_t,
+                              const float* pos, bool decode, hipStream_t st) {
+    const t5g_config& c = e->c;
+    const int d = c.hidden, f = c.intermediate, D = c.head_dim;
+    bf16_t* h = decode ? e->dh : e->h;
+    bf16_t* xn = decode ? e->dxn : e->xn;
+    bf16_t* q = decode ? e->dq : e->q;
+    bf16_t* att = decode ? e->datt : e->att;
+    bf16_t* act = decode ? e->dact : e->act;
+    bf16_t* tmp = e->tmp;
+    const int* rl = decode ? nullptr : e->kv_len;
+    const int* qlen = decode ? nullptr : e->kv_len;
+    auto norm = [&](const void* post_w, const void* pre_w) -> int {
+        NormArgs n = xnorm_args(M, d, c.rms_eps);
+        n.delta = tmp;
+        n.post_w = (const bf16_t*)post_w;
+        n.resid = h;
+        n.pre_w = (const bf16_t*)pre_w;
+        n.resid_out = h;
+        n.normed_out = xn;
+        return resid_norm(n, st);
+    };
+    for (int l = 0; l < c.n_dec_layers; ++l) {
+        const t5g_layer_weights& L = e->dec[l];
+        if (l == 0) {
+            NormArgs n = xnorm_args(M, d, c.rms_eps);
+            n.ids = ids;
+            n.table = (const bf16_t*)e->w.audio_embed;
+            n.n_table = c.n_audio_tokens;
+            n.scale = c.normalizer;
+            n.pre_w = (const bf16_t*)L.norms[0];
+            n.resid_out = h;
+            n.normed_out = xn;
+            RC(resid_norm(n, st));
+        }
+        // self attention
+        RC(xlin(e, xn, d, M, L.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, EPI_BF16, tok_row, rl, e->q_dim,
+                e->kv_dim, e->q_dim, st));
+        RopeArgs r = xrope_args(M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
+        r.X = e->qkv;
+        r.ldx = e->qkv_dim;
+        r.nq = c.n_heads;
+        r.nk = r.nv = c.n_kv_heads;
+        r.rope_q = r.rope_k = 1;
+        r.Qout = q;
+        r.ldq = e->q_dim;
+        r.Kc = e->sk[l];
+        r.Vc = e->sv[l];
+        r.c_hstride = (long)c.max_audio * D;
+        r.c_bstride = r.c_hstride * c.n_kv_heads;
+        RC(rope_store(r, st));
+        RC(xattn(e, q, M, tok_row, tok_t, qlen, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1,
+                 c.dec_sliding[l] ? c.sliding_window : 0, att, st));
+        RC(xlin(e, att, e->q_dim, M, L.o, d, e->q_dim, nullptr, tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+        RC(norm(L.norms[1], L.norms[2]));
+        // PM cross attention
+        RC(xlin(e, xn, d, M, L.cross_q, e->q_dim, d, nullptr, q, e->q_dim, EPI_BF16, tok_row, rl, e->q_dim, 0, 0, st));
+        r = xrope_args(M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
+        r.X = q;
+        r.ldx = e->q_dim;
+        r.nq = c.n_heads;
+        r.rope_q = 1;
+        r.Qout = q;
+        r.ldq = e->q_dim;
+        RC(rope_store(r, st));
+        RC(xattn(e, q, M, tok_row, tok_t, qlen, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, st));
+        RC(xlin(e, att, e->q_dim, M, L.cross_o, d, e->q_dim, nullptr, tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+        RC(norm(L.norms[3], L.norms[4]));
+        // GeGLU MLP
+        RC(xlin(e, xn, d, M, L.gate_up, 2 * f, d, nullptr, act, f, EPI_GEGLU, tok_row, rl, f, 0, 0, st));
+        RC(xlin(e, act, f, M, L.down, d, f, nullptr, tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+        const bool last = l == c.n_dec_layers - 1;
+        RC(norm(L.norms[5], last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]));
+    }
+    return T5G_OK;
+}
+
+static int head_exact(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st) {
+    const t5g_config& c = e->c;
+    const int d = c.hidden;
+    RC(xlin(e, xn_rows, d, B, e->w.head1, d, d, e->w.head1_bias, e->dhh, d, EPI_BIAS_GELU, nullptr, nullptr, d, 0, 0,
+            st));
+    RC(xlin(e, e->dhh, d, B, e->w.head2, e->V, d, e->w.head2_bias, e->logits, e->logits_ld, EPI_BIAS_BF16, nullptr,
+            nullptr, e->V, 0, 0, st));
+    return T5G_OK;
+}
+
+extern "C" int t5g_engine_set_exact(t5g_engine* e, int32_t enable, const uint16_t* gelu_lut, int32_t threads) {
+    if (!e) return T5G_EINVAL;
+    if (!enable) {
+        if (e->exact) drop_graphs(e);
+        e->exact = false;
+        return T5G_OK;
+    }
+    if (threads != REF_KSPLIT_THREADS) return T5G_EUNSUPPORTED;   // the only measured K-split table
+    if (e->c.softcap > 0.f) return T5G_EUNSUPPORTED;   // eager attention (softcap): not restated
+    if (!e->ksplit_dev) {
+        RC(alloc(e, &e->ksplit_dev, (int64_t)REF_KSPLIT_NSHAPES * REF_KSPLIT_MAX_M));
+        HIPCHK(hipMemcpy(e->ksplit_dev, ref_ksplit_kb32, sizeof(ref_ksplit_kb32), hipMemcpyHostToDevice));
+    }
+    if (gelu_lut) {
+        if (!e->gelu_lut_dev) RC(alloc(e, &e->gelu_lut_dev, 65536));
+        HIPCHK(hipMemcpy(e->gelu_lut_dev, gelu_lut, 65536 * sizeof(uint16_t), hipMemcpyHostToDevice));
+    }
+    e->exact_threads = threads;
+    if (!e->exact) drop_graphs(e);
+    e->exact = true;
+    return T5G_OK;
+}
+
 extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t* ids, const int32_t* tok_row,
                           const int32_t* tok_t, const float* pos, const int32_t* text_len, void* stream) {
     if (!e || B <= 0 || ntok <= 0) return T5G_EINVAL;
@@ -296,6 +581,7 @@ extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t*
     hipStream_t st = (hipStream_t)stream;
     const int d = c.hidden, f = c.intermediate, D = c.head_dim;
     HIPCHK(hipMemcpyAsync(e->enc_len, text_len, B * sizeof(int), hipMemcpyDeviceToDevice, st));
+    if (e->exact) return encode_exact(e, ntok, ids, tok_row, tok_t, pos, st);
     for (int l = 0; l < c.n_enc_layers; ++l) {
         const t5g_layer_weights& L = e->enc[l];
         NormArgs n = norm_args(ntok, d, c.rms_eps);
@@ -600,7 +886,12 @@ static DecGemmArgs dec_args(int M, const void* W, int N, int K, void* Y, int ldy
 
 // one decoder step + predict head for the e->B rows fed by the sampler buffers
 static int head(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st);
+static int head_exact(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st);
 static int decode_forward(t5g_engine* e, hipStream_t st) {
+    if (e->exact) {
+        RC(decoder_pass_exact(e, e->B, e->next_token, nullptr, nullptr, e->next_pos, true, st));
+        return head_exact(e, e->dxn, e->B, st);
+    }
     int rc = decoder_pass(e, e->B, e->next_token, nullptr, nullptr, e->next_pos, true, st);
     if (rc) return rc;
     return head(e, e->dxn, e->B, st);
@@ -638,7 +929,8 @@ extern "C" int t5g_prefill(t5g_engine* e, int32_t B, int32_t ntok, const int32_t
     e->B = B;
     HIPCHK(hipMemcpyAsync(e->kv_len, kv_len, B * sizeof(int), hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemcpyAsync(e->last_rows, last_index, B * sizeof(int), hipMemcpyDeviceToDevice, st));
-    int rc = decoder_pass(e, ntok, ids, tok_row, tok_t, pos, false, st);
+    int rc = e->exact ? decoder_pass_exact(e, ntok, ids, tok_row, tok_t, pos, false, st)
+                      : decoder_pass(e, ntok, ids, tok_row, tok_t, pos, false, st);
     if (rc) return rc;
     // the last decoder_pass norm wrote final-normed hidden of every token into xn;
     // gather each row's last token
@@ -648,7 +940,7 @@ extern "C" int t5g_prefill(t5g_engine* e, int32_t B, int32_t ntok, const int32_t
     n.out_rows = e->last_rows;
     n.resid_out = e->dxn;
     RC(resid_norm(n, st));
-    return head(e, e->dxn, B, st);
+    return e->exact ? head_exact(e, e->dxn, B, st) : head(e, e->dxn, B, st);
 }
 
 extern "C" int t5g_sampler_setup(t5g_engine* e, int32_t B, const t5g_sampler_row* rows, const t5g_sampler_state* init,
@@ -991,5 +1283,67 @@ extern "C" int t5g_time_gemv(const t5g_gemv_args* g, const void* const* Wp_list,
     *avg_us = ms * 1000.f / iters;
     hipEventDestroy(e0);
     hipEventDestroy(e1);
+    return T5G_OK;
+}
+
+extern "C" int t5g_exact_linear(const void* X, int32_t ldx, int32_t M, const void* Wp, int32_t N, int32_t K,
+                                int32_t kb32, const void* bias, const void* gelu_lut, void* Y, int32_t ldy, int32_t epi,
+                                void* stream) {
+    if (!X || !Wp || !Y || M <= 0 || N <= 0 || K <= 0 || K % 32 || kb32 < 0) return T5G_EINVAL;
+    static thread_local uint16_t* kb_dev = nullptr;   // a one-entry split table
+    if (!kb_dev && hipMalloc(&kb_dev, sizeof(uint16_t)) != hipSuccess) return T5G_EHIP;
+    const uint16_t kb = (uint16_t)kb32;
+    if (kb32 > 0) HIPCHK(hipMemcpyAsync(kb_dev, &kb, sizeof(kb), hipMemcpyHostToDevice, (hipStream_t)stream));
+    ExactLinArgs a;
+    memset(&a, 0, sizeof(a));
+    a.X = (const bf16_t*)X;
+    a.ldx = ldx;
+    a.M = M;
+    a.W = (const bf16_t*)Wp;
+    a.N = N;
+    a.NG = ng_pad(N);
+    a.KB = K / 32;
+    a.bias = (const bf16_t*)bias;
+    a.Y = Y;
+    a.ldy = ldy;
+    a.kb_a = kb32 > 0 ? kb_dev : nullptr;
+    a.kb_len = 1;
+    a.gelu_lut = (const uint16_t*)gelu_lut;
+    RC(exact_linear(a, epi, (hipStream_t)stream));
+    if (kb32 > 0) HIPCHK(hipStreamSynchronize((hipStream_t)stream));   // kb is a host temporary
+    return T5G_OK;
+}
+
+extern "C" int t5g_exact_attention(const void* q, int32_t Mq, const int32_t* q_row, const int32_t* q_pos,
+                                   const int32_t* q_len, const void* k_cache, const void* v_cache, int32_t cap,
+                                   const int32_t* kv_len, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
+                                   int32_t causal, int32_t window, float scale, int32_t threads, void* out,
+                                   void* stream) {
+    if (!q || !k_cache || !v_cache || !kv_len || !out || Mq <= 0 || cap <= 0 || n_kv_heads <= 0 ||
+        n_heads % n_kv_heads || head_dim <= 0 || threads <= 0)
+        return T5G_EINVAL;
+    ExactAttnArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Q = (const bf16_t*)q;
+    a.ldq = n_heads * head_dim;
+    a.Mq = Mq;
+    a.q_row = q_row;
+    a.q_pos = q_pos;
+    a.q_len = q_len;
+    a.K = (const bf16_t*)k_cache;
+    a.V = (const bf16_t*)v_cache;
+    a.kv_hstride = (long)cap * head_dim;
+    a.kv_bstride = a.kv_hstride * n_kv_heads;
+    a.kv_len = kv_len;
+    a.Hq = n_heads;
+    a.Hkv = n_kv_heads;
+    a.D = head_dim;
+    a.causal = causal;
+    a.window = window;
+    a.scale = scale;
+    a.threads = threads;
+    a.O = (bf16_t*)out;
+    a.ldo = a.ldq;
+    RC(exact_attention(a, (hipStream_t)stream));
     return T5G_OK;
 }

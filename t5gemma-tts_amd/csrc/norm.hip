@@ -13,6 +13,7 @@
 //   out = pre_w ? bf16((h * (1/sqrt(mean(h^2)+eps))) * (1 + pre_w))   -> normed_out
 // Sums reduce in a fixed order, so results are run-to-run deterministic.
 #include "common.h"
+#include "exact_math.h"
 #include "t5g_kernels.h"
 
 namespace t5g {
@@ -48,11 +49,67 @@ __device__ __forceinline__ float block_sum_once(float v, float* red) {
     return s;
 }
 
-__device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, u32x4 w8, float eps, float* red) {
-    float ss = 0.f;
+// Sum of squares in the order of torch 2.10's CPU float sum over a contiguous row
+// (exact / parity mode). aten SumKernel.cpp cascade_sum -> vectorized_inner_sum, AVX2
+// kernel (the AVX-512 stub is not registered): the row is a sequence of 8-float vectors
+// (thread c holds vector c); row_sum interleaves 4 vector accumulators (vector c ->
+// accumulator c % 4, row c / 4); multi_row_sum folds each accumulator's rows in a
+// cascade of 4 levels of 16 rows; accumulators 1..3 are added to 0, vectors past the last
+// whole row of 4 go to accumulator 0 first; finally the 8 lanes are summed in order.
+// Verified bit for bit against torch on random rows (tools/cpu_order).
+__device__ __forceinline__ float ref_sumsq(const float (&v)[8], bool active, int nvec, float* sq) {
+    const int c = threadIdx.x;
+    if (active) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
-    float tot = block_sum_once(active ? ss : 0.f, red);
+        for (int j = 0; j < 8; ++j) sq[c * 8 + j] = __fmul_rn(v[j], v[j]);
+    }
+    __syncthreads();
+    if (c < 32) {
+        const int k = c >> 3, j = c & 7;
+        const int size_ilp = nvec / 4;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int i = 0;
+        while (i + 16 <= size_ilp) {
+            for (int q = 0; q < 16; ++q, ++i) a0 = __fadd_rn(a0, sq[(i * 4 + k) * 8 + j]);
+            a1 = __fadd_rn(a1, a0);
+            a0 = 0.f;
+            if (i & 0xF0) continue;
+            a2 = __fadd_rn(a2, a1);
+            a1 = 0.f;
+            if (i & 0xF00) continue;
+            a3 = __fadd_rn(a3, a2);
+            a2 = 0.f;
+        }
+        for (; i < size_ilp; ++i) a0 = __fadd_rn(a0, sq[(i * 4 + k) * 8 + j]);
+        a0 = __fadd_rn(__fadd_rn(__fadd_rn(a0, a1), a2), a3);
+        if (k == 0)
+            for (int t = size_ilp * 4; t < nvec; ++t) a0 = __fadd_rn(a0, sq[t * 8 + j]);
+        sq[nvec * 8 + c] = a0;
+    }
+    __syncthreads();
+    float lanes[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        lanes[j] = __fadd_rn(__fadd_rn(__fadd_rn(sq[nvec * 8 + j], sq[nvec * 8 + 8 + j]), sq[nvec * 8 + 16 + j]),
+                             sq[nvec * 8 + 24 + j]);
+    float tot = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tot = __fadd_rn(tot, lanes[j]);
+    __syncthreads();   // sq is reused by the launch's second RMSNorm
+    return tot;
+}
+
+template <bool EXACT>
+__device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, u32x4 w8, float eps, float* red, float* sq) {
+    float tot;
+    if constexpr (EXACT) {
+        tot = ref_sumsq(v, active, d / 8, sq);
+    } else {
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+        tot = block_sum_once(active ? ss : 0.f, red);
+    }
     float r = 1.0f / sqrtf(tot / (float)d + eps);
     if (!active) return;
     float wf[8];
@@ -66,17 +123,18 @@ __device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, u32x4 w8
 // and idle threads read the last chunk. A load guarded by a branch makes the
 // compiler wait for every load in flight at the branch join (vmcnt(0)), which
 // serialised two memory round trips here.
-template <int NS, int SRC>   // NS: split-K slabs of the part path; SRC: 0 delta, 1 ids, 2 part
+template <int NS, int SRC, bool EXACT = false>   // NS: split-K slabs of the part path; SRC: 0 delta, 1 ids, 2 part
 __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_post, int has_resid, int has_pre) {
     __shared__ float red[2][32];   // one per RMSNorm of the launch
+    __shared__ float sq[EXACT ? 8 * 1024 + 32 : 1];   // exact mode: squares + accumulator lanes
     T5G_TS(0);
     const int mi = blockIdx.x;
     if (a.rope_tab) {   // the decode step's per-row cos/sin table (used by every layer's attention)
         const int H2 = a.rope_D / 2;
         for (int i = threadIdx.x; i < H2; i += blockDim.x) {
             const float ang = a.rope_inv_freq[i] * a.rope_pos[mi];
-            a.rope_tab[(long)mi * a.rope_D + i] = rbf(cosf(ang));
-            a.rope_tab[(long)mi * a.rope_D + H2 + i] = rbf(sinf(ang));
+            a.rope_tab[(long)mi * a.rope_D + i] = rbf(EXACT ? t5g_exact::rope_cos(ang) : cosf(ang));
+            a.rope_tab[(long)mi * a.rope_D + H2 + i] = rbf(EXACT ? t5g_exact::rope_sin(ang) : sinf(ang));
         }
     }
     const int m = a.out_rows ? a.out_rows[mi] : mi;
@@ -116,7 +174,7 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
     } else {
         unpack8(*(const u32x4*)(a.delta + (long)m * d + 8 * cc), v);
     }
-    if (has_post) rms8(v, active, d, w_post, a.eps, red[0]);
+    if (has_post) rms8<EXACT>(v, active, d, w_post, a.eps, red[0], sq);
     T5G_TS(1);
     if (has_resid) {
         float r8[8];
@@ -127,7 +185,7 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
     const long orow = a.out_rows ? (long)mi : (long)m;
     if (a.resid_out && active) *(u32x4*)(a.resid_out + orow * d + 8 * c) = pack8(v);
     if (has_pre) {
-        rms8(v, active, d, w_pre, a.eps, red[1]);
+        rms8<EXACT>(v, active, d, w_pre, a.eps, red[1], sq);
         if (active) *(u32x4*)(a.normed_out + orow * d + 8 * c) = pack8(v);
     }
     T5G_TS(2);
@@ -155,7 +213,12 @@ int resid_norm(const NormArgs& a_in, hipStream_t st) {
     const dim3 g((unsigned)a.M), b(threads);
 #define T5G_NORM(NS_, SRC_) \
     hipLaunchKernelGGL((resid_norm_kernel<NS_, SRC_>), g, b, 0, st, a, has_post, has_resid, has_pre)
-    if (src == 0) T5G_NORM(0, 0);
+    if (a.exact) {
+        // parity mode: the reference's CPU sum order (part slabs are not used there)
+        if (src == 2 || a.d > 8 * 1024) return -1;
+        if (src == 0) hipLaunchKernelGGL((resid_norm_kernel<0, 0, true>), g, b, 0, st, a, has_post, has_resid, has_pre);
+        else hipLaunchKernelGGL((resid_norm_kernel<0, 1, true>), g, b, 0, st, a, has_post, has_resid, has_pre);
+    } else if (src == 0) T5G_NORM(0, 0);
     else if (src == 1) T5G_NORM(0, 1);
     else switch (a.nsplit) {
         case 1: T5G_NORM(1, 2); break;

@@ -159,7 +159,9 @@ __device__ __forceinline__ uint32_t philox(uint32_t c0, uint32_t c1, uint32_t c2
 // streams get different seeds from the host).
 __device__ __forceinline__ float draw_q(const SamplerArgs& a, const SamplerRow& pr, const SamplerState& st, int b,
                                         int i) {
-    if (a.noise) return bf2f(a.noise[((long)b * a.noise_steps + st.cur_num_gen) * a.V + i]);
+    // parity mode: the step's reference draws (steps past the uploaded ones -- never reached
+    // when the host sizes the stream to the row budget + 1 -- reuse the last, in bounds)
+    if (a.noise) return bf2f(a.noise[((long)b * a.noise_steps + min(st.cur_num_gen, a.noise_steps - 1)) * a.V + i]);
     (void)b;
     const uint32_t u = philox((uint32_t)i, (uint32_t)st.cur_num_gen, 0u, pr.seed_lo, pr.seed_hi);
     const float uf = ((float)(u >> 8) + 1.0f) * (1.0f / 16777216.0f);
@@ -526,7 +528,8 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
             if (v > -INFINITY) ls += expf(v - m);
         }
         const float inv = 1.0f / block_sum(ls, redv);
-        const bf16_t* nz = a.noise ? a.noise + ((long)b * a.noise_steps + st.cur_num_gen) * V : nullptr;
+        const bf16_t* nz =
+            a.noise ? a.noise + ((long)b * a.noise_steps + min(st.cur_num_gen, a.noise_steps - 1)) * V : nullptr;
         float bv = -1.f;
         int bi = 0x7fffffff;
 #pragma unroll

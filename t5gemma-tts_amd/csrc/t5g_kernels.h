@@ -68,6 +68,7 @@ struct NormArgs {
     const float* rope_inv_freq;
     float* rope_tab;         // [M][rope_D]
     int rope_D;
+    int exact;               // parity mode: the reference's CPU sum order (delta / ids sources)
 };
 int resid_norm(const NormArgs& a, hipStream_t st);
 
@@ -91,6 +92,7 @@ struct RopeArgs {
     bf16_t* Vc;
     long c_bstride, c_hstride;
     const float* rope_tab;   // optional [rows][D]: bf16-rounded cos (D/2) | sin (D/2) per row
+    int exact_trig;          // parity mode: cos / sin as the reference host rounds them (exact_math.h)
 };
 int rope_store(const RopeArgs& a, hipStream_t st);
 // (the decode step's per-row table tab[r][i] = bf16(cos(inv_freq[i] * pos[r])),
@@ -132,6 +134,46 @@ struct AttnArgs {
 int attention(const AttnArgs& a, hipStream_t st);
 // decode-shaped (64-key chunks over blockIdx.z + one P.V / combine launch, sdpa numerics)
 int attention_decode(const AttnArgs& a, hipStream_t st);
+
+// ---- exact-order (parity mode) kernels, exact.hip ------------------------------------
+struct ExactLinArgs {
+    const bf16_t* X;          // [M][ldx] bf16
+    int ldx, M;
+    const bf16_t* W;          // packed P16
+    int N, NG, KB;            // real output rows, padded row groups (multiple of 4), K / 32
+    const bf16_t* bias;
+    void* Y;                  // fp32 / bf16 [M][ldy] (GEGLU: bf16 [M][N/2])
+    int ldy;
+    // the reference call's row count of each X row: row_len[tok_row[m]] (tok_row null:
+    // row_len[m]; row_len null: 1) selects the K split kb_a[M_ref - 1] (columns >= nsplit_col:
+    // kb_b) in 32-element chunks; null tables: no split
+    const int* tok_row;
+    const int* row_len;
+    const uint16_t* kb_a;
+    const uint16_t* kb_b;
+    int nsplit_col, kb_len;
+    const uint16_t* gelu_lut; // EPI_BIAS_GELU: bf16 -> bf16 nn.GELU() table (null: exact_math.h)
+};
+int exact_linear(const ExactLinArgs& a, int epi, hipStream_t st);
+
+struct ExactAttnArgs {
+    const bf16_t* Q;          // [Mq][ldq] RoPE'd queries
+    int ldq, Mq;
+    const int* q_row;         // [Mq] batch row (null: query index)
+    const int* q_pos;         // [Mq] query index within its row's call (null: Tq - 1)
+    const int* q_len;         // [B] queries of each row's reference call (null: 1)
+    const bf16_t* K;          // cache [B][Hkv][cap][D]
+    const bf16_t* V;
+    long kv_bstride, kv_hstride;
+    const int* kv_len;        // [B] keys of each row's call
+    int Hq, Hkv, D;
+    int causal, window;       // window > 0: sliding-window layer (explicit mask once keys >= window)
+    float scale;
+    int threads;              // the reference host's torch thread count (aten need_pack)
+    bf16_t* O;
+    int ldo;
+};
+int exact_attention(const ExactAttnArgs& a, hipStream_t st);
 
 // ---- sampler -------------------------------------------------------------------
 struct SamplerRow {           // per-utterance parameters (device)

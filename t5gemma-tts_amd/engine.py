@@ -245,19 +245,40 @@ class T5GemmaTTSEngine:
         return t[:, :self.V]
 
     # ------------------------------------------------------------------
+    def set_exact(self, enable: bool) -> None:
+        """Switch the engine to the exact-order kernels (csrc/exact.hip: every sum in the
+        reference host's CPU order) or back to the fast kernels."""
+        if bool(enable) == getattr(self, "_exact", False):
+            return
+        tab = _lib.gelu_erf_table() if enable else None
+        _lib.check(self.L.t5g_engine_set_exact(self.h, 1 if enable else 0, tab, _lib.EXACT_THREADS), "set_exact")
+        self._exact = bool(enable)
+
     def generate(self, utts: Sequence[Utterance], params: Union[SamplingParams, Sequence[SamplingParams]],
                  seeds: Optional[Sequence[int]] = None, parity: bool = False, use_graph: bool = True,
                  chunk: int = 32, record_logits: bool = False,
-                 generators: Optional[Sequence[torch.Generator]] = None):
-        """Run inference_tts on a batch. ``parity=True`` uses the reference's CPU RNG
-        stream and resolves tie-ambiguous top-p steps on the host -- token-exact
-        reproduction mode (slow: one host sync per step). The stream of row i is
-        ``torch.manual_seed(seeds[i])`` or, with ``generators``, the continuation of
-        ``generators[i]`` (e.g. ``torch.default_generator`` after ``seed_everything``),
-        which is then advanced by exactly the draws the reference would have made.
+                 generators: Optional[Sequence[torch.Generator]] = None, exact: Optional[bool] = None):
+        """Run inference_tts on a batch. ``parity=True`` is the reference-reproduction mode:
+        the exact-order kernels (logits bit-identical to the reference host's CPU run), the
+        reference's CPU RNG stream, and host resolution of tie-ambiguous top-p steps (one
+        host sync per step). The stream of row i is ``torch.manual_seed(seeds[i])`` or, with
+        ``generators``, the continuation of ``generators[i]`` (e.g. ``torch.default_generator``
+        after ``seed_everything``), which is then advanced by exactly the draws the reference
+        would have made. ``exact`` (default: = parity) selects the kernel set on its own.
         Returns dict(res=[...], gen=[...], steps, ambiguous)."""
         if generators is not None and not parity:
             raise ValueError("generators= drives the reference RNG stream: parity=True only")
+        if exact is None:
+            # the exact-order kernels restate the sdpa attention path; eager (softcap)
+            # configurations keep the fast kernels under parity=True
+            exact = parity and self.cfg.backbone.softcap == 0.0
+        if exact:
+            for u in utts:
+                n_y = len(u.y) + 1
+                if len(u.x) > _lib.EXACT_MAX_TOKENS or n_y > _lib.EXACT_MAX_TOKENS:
+                    raise ValueError(f"parity mode: text {len(u.x)} / prompt {n_y} tokens exceed the measured "
+                                     f"reference K-split table ({_lib.EXACT_MAX_TOKENS})")
+        self.set_exact(exact)
         stream = _stream(self.device)
         ctx = self._prepare(utts, params, generators if generators is not None else seeds, parity, stream)
         if parity:
@@ -369,7 +390,9 @@ class T5GemmaTTSEngine:
         d_alen, d_last = torch.tensor(alen, **i32), torch.tensor(last, **i32)
         noise = None
         if parity:
-            noise = torch.stack([reference_noise(s, max_steps, self.V) for s in seeds[:B]]).to(dev)
+            # one stream step per sampler call: up to the row budget, plus the step at which a
+            # cap (time budget or, without tgt_y_lens, the cache capacity) forces EOS
+            noise = torch.stack([reference_noise(s, max_steps + 1, self.V) for s in seeds[:B]]).to(dev)
         L = self.L
         # the host tensors above were filled on torch's current stream: order them first
         torch.cuda.current_stream(dev).synchronize()
@@ -380,7 +403,7 @@ class T5GemmaTTSEngine:
         tk = (C.c_int32 * max(1, len(topk_list)))(*topk_list)
         sl = (C.c_int32 * max(1, len(silence)))(*silence)
         _lib.check(L.t5g_sampler_setup(self.h, B, rows, states, tk, len(topk_list), sl, len(silence),
-                                       _ptr(noise), max_steps if parity else 0, stream), "sampler_setup")
+                                       _ptr(noise), max_steps + 1 if parity else 0, stream), "sampler_setup")
         return {"B": B, "rows": rows, "tk": tk, "sl": sl, "noise": noise, "y_rows": y_rows,
                 "max_steps": max_steps, "steps": 0, "ambiguous_fixed": 0, "rec": None,
                 "cur": (_lib.SamplerState * B)(), "keep": (d_ids, d_trow, d_tt, d_tpos, d_tlen, d_aid, d_arow, d_at,

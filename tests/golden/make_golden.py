@@ -266,6 +266,41 @@ def gen_full_golden(RT, out="golden_full", seed=13, n_cases=2, steps=16):
     np.savez_compressed(os.path.join(HERE, f"{out}.npz"), **arrays)
 
 
+def gen_long_golden(RT, out="golden_long", seed=13, n_cases=2):
+    """The C3 bench workload at full depth and full length: the first ``n_cases`` rows of
+    bench.py's synthetic batch (T_x 60, T_p 151, tgt_y_lens = T_p + 500, default
+    extra_cutoff 5 -> up to 751 tokens, L up to 903), EOS accepted as in the reference.
+    Stores top-64 logits + a sha of every full logit row per step."""
+    import hashlib
+    sys.path.insert(0, REPO)
+    from bench import make_batch
+    cfg = named_config("2b2b", extra_cutoff=5.0)
+    with tempfile.TemporaryDirectory(dir=os.environ.get("GOLDEN_TMP", "/tmp")) as td:
+        m, sd = build_reference_model(RT, cfg, seed, td, lowmem=True)
+        cases = []
+        for i, (x, y, tgt) in enumerate(make_batch(cfg, n_cases, seed=20251226)):
+            cases.append(dict(x=[int(v) for v in x], y=[int(v) for v in y], tgt=int(tgt), seed=int(3000 + i),
+                              top_k=30, top_p=0.9, min_p=0.0, temperature=0.8, stop_repetition=3,
+                              silence_tokens=[]))
+        arrays = {}
+        for ci, c in enumerate(cases):
+            res, gen, logs, dt = run_case(RT, m, cfg, c)
+            c["res"], c["gen"] = res, gen
+            c["ref_seconds"] = round(dt, 4)
+            c["n_steps"] = int(logs.shape[0])
+            top = torch.topk(logs.float(), 64, dim=-1)
+            arrays[f"top_vals_{ci}"] = bf16_bits(top.values.to(torch.bfloat16))
+            arrays[f"top_idx_{ci}"] = top.indices.numpy().astype(np.int32)
+            c["logit_sha"] = [hashlib.sha256(bf16_bits(r).tobytes()).hexdigest()[:16] for r in logs]
+            print(f"[long] case {ci}: T_x={len(c['x'])} T_p={len(c['y'])} gen={len(gen)} ({dt:.2f}s)", flush=True)
+        digest = state_dict_digest(sd)
+    meta = {"config": "2b2b", "config_kw": {"extra_cutoff": 5.0}, "weight_seed": seed, "weight_sha256": digest,
+            "torch": torch.__version__, "threads": torch.get_num_threads(), "cases": cases}
+    with open(os.path.join(HERE, f"{out}.json"), "w") as f:
+        json.dump(meta, f)
+    np.savez_compressed(os.path.join(HERE, f"{out}.npz"), **arrays)
+
+
 def gen_sampler_golden(RU, out="golden_sampler", V=65541, n=48):
     """Per-step sampler cases at the real vocab: reference topk_sampling +
     torch.multinomial under torch.manual_seed(seed). Logits regenerable from
@@ -322,6 +357,8 @@ if __name__ == "__main__":
         gen_model_golden(RT, "tiny", {"sliding_window": 8}, seed=9, n_cases=4, out="golden_tiny_window")
     if "full" in todo:
         gen_full_golden(RT)
+    if "long" in todo:
+        gen_long_golden(RT)
     if "mid" in todo:
         gen_model_golden(RT, "mid", {}, seed=11, n_cases=2, out="golden_mid", store_logits="top",
                          max_tx=40, tgt_frames=(4, 8))
