@@ -1,0 +1,174 @@
+"""CPU tests of the reference-host accumulation-order restatement (oracle/cpu_order.py) and
+of the exact-mode elementwise functions (csrc/exact_math.h, data/gelu_erf_bf16.bin).
+
+* Against torch itself: only meaningful on the reference host (the build container the
+  golden vectors were made on: torch 2.10 CPU with oneDNN AMX); skipped elsewhere.
+* Against the reference's golden vectors: machine-independent (numpy arithmetic)."""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import GOLDEN, REPO
+
+BF16 = torch.bfloat16
+
+
+def _reference_host():
+    try:
+        flags = open("/proc/cpuinfo").read()
+    except OSError:
+        return False
+    return "amx_bf16" in flags and torch.__version__.startswith("2.10")
+
+
+ref_host = pytest.mark.skipif(not _reference_host(), reason="torch comparison needs the reference host (AMX, torch 2.10)")
+
+
+def _hdr(shape, g):
+    v = torch.randn(shape, generator=g) * torch.exp2(torch.randint(-10, 11, shape, generator=g).float())
+    big = torch.rand(shape, generator=g) < 4.0 / shape[-1]
+    return torch.where(big, torch.randn(shape, generator=g) * 2.0 ** 14, v).to(BF16)
+
+
+@ref_host
+@pytest.mark.parametrize("n", [2304, 128, 64, 9216, 100, 8])
+def test_sum_last_matches_torch(n):
+    from oracle import cpu_order
+    torch.set_num_threads(8)
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(16, n, generator=g) * torch.exp2(torch.randint(-12, 13, (16, n), generator=g).float())
+    assert np.array_equal(cpu_order.sum_last(x.numpy()), x.sum(-1).numpy())
+    assert np.array_equal((cpu_order.sum_last((x * x).numpy()) / np.float32(n)).astype(np.float32),
+                          x.pow(2).mean(-1).numpy())
+
+
+@ref_host
+@pytest.mark.parametrize("M,N,K", [(1, 2048, 2304), (1, 2304, 9216), (60, 2304, 9216), (152, 2304, 9216),
+                                   (60, 1024, 2304), (7, 128, 256), (1, 2304, 2048)])
+def test_linear_order_matches_torch(M, N, K):
+    """The E/O chunk model with the measured K split == torch's F.linear, on a sample of
+    output columns of order-revealing data."""
+    from oracle import cpu_order
+    torch.set_num_threads(8)
+    g = torch.Generator().manual_seed(M + N + K)
+    x = _hdr((M, K), g)
+    cols = torch.randperm(N, generator=g)[:64]
+    w = torch.zeros(N, K, dtype=BF16)
+    w[cols] = _hdr((64, K), g)
+    ref = F.linear(x, w)[:, cols]
+    kb = cpu_order.ksplit(N, K, M)
+    got = torch.from_numpy(cpu_order.linear_f32(x.float().numpy(), w[cols].float().numpy(), kb)).to(BF16)
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+
+
+@ref_host
+@pytest.mark.parametrize("Tq,Tk,causal", [(1, 903, False), (1, 60, False), (60, 60, False), (152, 152, True),
+                                          (152, 60, False), (33, 33, True), (300, 300, True)])
+def test_sdpa_order_matches_torch(Tq, Tk, causal):
+    from oracle import cpu_order
+    torch.set_num_threads(8)
+    g = torch.Generator().manual_seed(Tq * 7 + Tk)
+    q = torch.randn(1, 8, Tq, 256, generator=g).to(BF16)
+    k = torch.randn(1, 4, Tk, 256, generator=g).to(BF16)
+    v = torch.randn(1, 4, Tk, 256, generator=g).to(BF16)
+    ref = F.scaled_dot_product_attention(q, k, v, scale=1 / 16, is_causal=causal and Tq > 1, enable_gqa=True)[0]
+    got = cpu_order.sdpa(q[0], k[0].repeat_interleave(2, 0), v[0].repeat_interleave(2, 0), 1 / 16,
+                         is_causal=causal, Hq=8)
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+
+
+@pytest.mark.parametrize("name", ["golden_tiny", "golden_tiny_window"])
+def test_cpu_order_oracle_reproduces_reference_goldens(name):
+    """With every Linear / RMSNorm / SDPA restated (no oneDNN, no aten reductions), the
+    oracle reproduces the reference's runs bit for bit: tokens and every logit row."""
+    import oracle.t5g_oracle as O
+    from oracle import cpu_order
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.weights import synthetic_weights
+    meta = json.load(open(os.path.join(GOLDEN, name + ".json")))
+    arrs = dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    cpu_order.install(O)
+    try:
+        orc = O.T5GemmaTTSOracle(cfg, sd)
+        for ci, c in enumerate(meta["cases"]):
+            p = O.SamplerParams(top_k=c["top_k"], top_p=c["top_p"], min_p=c["min_p"], temperature=c["temperature"],
+                                stop_repetition=c["stop_repetition"], silence_tokens=tuple(c["silence_tokens"]))
+            out = orc.generate(c["x"], c["y"], c["tgt"], p, seed=c["seed"], record_logits=True)
+            assert out["gen"].view(-1).tolist() == c["gen"], ci
+            assert np.array_equal(out["logits"].contiguous().view(torch.int16).numpy(), arrs[f"logits_{ci}"]), ci
+    finally:
+        cpu_order.uninstall(O)
+
+
+# ------------------------------------------------------------------- exact_math.h
+_SHIM = r"""
+#define T5G_HD
+#include "exact_math.h"
+extern "C" void eval_all(unsigned short* tanh_out, unsigned short* erf_out) {
+    for (int i = 0; i < 65536; ++i) {
+        unsigned int u = (unsigned int)i << 16; float x; __builtin_memcpy(&x, &u, 4);
+        float a = t5g_exact::gelu_tanh(x), b = t5g_exact::gelu_erf(x);
+        unsigned int ua, ub; __builtin_memcpy(&ua, &a, 4); __builtin_memcpy(&ub, &b, 4);
+        // RNE to bf16 (NaN kept NaN)
+        tanh_out[i] = (ua & 0x7fffffff) > 0x7f800000 ? (unsigned short)((ua >> 16) | 0x40)
+                                                     : (unsigned short)((ua + 0x7fff + ((ua >> 16) & 1)) >> 16);
+        erf_out[i] = (ub & 0x7fffffff) > 0x7f800000 ? (unsigned short)((ub >> 16) | 0x40)
+                                                    : (unsigned short)((ub + 0x7fff + ((ub >> 16) & 1)) >> 16);
+    }
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def exact_math_lib(tmp_path_factory):
+    d = tmp_path_factory.mktemp("exact_math")
+    src = d / "shim.cpp"
+    src.write_text(_SHIM)
+    so = d / "shim.so"
+    inc = os.path.join(REPO, "t5gemma-tts_amd", "csrc")
+    r = subprocess.run(["g++", "-O2", "-ffp-contract=off", "-shared", "-fPIC", "-I", inc, str(src), "-o", str(so)],
+                       capture_output=True, text=True)
+    if r.returncode:
+        pytest.skip(f"g++ unavailable: {r.stderr[-300:]}")
+    lib = C.CDLL(str(so))
+    t = np.zeros(65536, np.uint16)
+    e = np.zeros(65536, np.uint16)
+    lib.eval_all(t.ctypes.data_as(C.c_void_p), e.ctypes.data_as(C.c_void_p))
+    return t, e
+
+
+def _finite_mask():
+    x = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(BF16).float()
+    return torch.isfinite(x).numpy()
+
+
+def test_gelu_tanh_matches_torch_every_bf16(exact_math_lib):
+    """gelu_tanh of exact_math.h == torch's CPU gelu(approximate='tanh') on every finite bf16."""
+    tanh_out, _ = exact_math_lib
+    x = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(BF16)
+    ref = F.gelu(x, approximate="tanh").view(torch.int16).numpy().astype(np.uint16)
+    ok = _finite_mask()
+    assert np.array_equal(tanh_out[ok], ref[ok]), int((tanh_out[ok] != ref[ok]).sum())
+
+
+def test_gelu_erf_table_and_exact_form(exact_math_lib):
+    """The shipped GELU(erf) table is torch's CPU nn.GELU() of the reference host; the
+    exact-erf fallback differs from it only on the 24 documented inputs in [-5.4, -3.1]."""
+    _, erf_out = exact_math_lib
+    tab = np.fromfile(os.path.join(REPO, "t5gemma-tts_amd", "data", "gelu_erf_bf16.bin"), dtype="<u2")
+    assert tab.shape == (65536,)
+    ok = _finite_mask()
+    diff = np.nonzero(ok & (erf_out != tab))[0]
+    xs = torch.from_numpy(diff.astype(np.int32)).to(torch.int16).view(BF16).float()
+    assert len(diff) == 24 and bool(((xs >= -5.4) & (xs <= -3.1)).all()), xs.tolist()
+    if _reference_host():
+        x = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(BF16)
+        assert np.array_equal(F.gelu(x).view(torch.int16).numpy().astype(np.uint16)[ok], tab[ok])

@@ -219,7 +219,7 @@ def _oparams(c):
 # free-running token-exact cases each golden set must keep (measured on MI355X, see
 # profiles/r02_parity_rates.json); every other case must diverge only at an explained
 # sampling-boundary flip (see _explain_divergence)
-MIN_EXACT = {"golden_tiny": 9, "golden_tiny_eager": 4, "golden_tiny_window": 4}
+MIN_EXACT = {"golden_tiny": 12, "golden_tiny_eager": 4, "golden_tiny_window": 4}
 
 
 def _topk_agree(g, r, k, tol):

@@ -89,3 +89,27 @@ def test_oracle_matches_reference_mid():
         bits = _bits(out["logits"])
         shas = [hashlib.sha256(r.astype(np.int16).tobytes()).hexdigest()[:16] for r in bits]
         assert shas == c["logit_sha"], ci
+
+
+def test_oracle_matches_reference_full_depth():
+    """Full 26+26-layer 2b-2b at the C3 shapes (T_x 60, T_p 151), 16 steps per case: token
+    ids and every step's full logit-row sha equal the reference's own run (same host,
+    same thread count as the fixture)."""
+    import hashlib
+    name = "golden_full"
+    if not os.path.exists(os.path.join(GOLDEN, name + ".json")):
+        pytest.skip("fixture not generated")
+    meta, arrs = _load(name)
+    torch.set_num_threads(meta["threads"])
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    assert state_dict_digest(sd) == meta["weight_sha256"]
+    orc = T5GemmaTTSOracle(cfg, sd)
+    for ci, c in enumerate(meta["cases"]):
+        out = orc.generate(c["x"], c["y"], c["tgt"], _params(c), seed=c["seed"], record_logits=True)
+        assert out["gen"].view(-1).tolist() == c["gen"], ci
+        bits = _bits(out["logits"])
+        shas = [hashlib.sha256(r.astype(np.int16).tobytes()).hexdigest()[:16] for r in bits]
+        assert shas == c["logit_sha"], ci
+        top = torch.topk(out["logits"].float(), 64, dim=-1)
+        assert np.array_equal(top.indices.numpy().astype(np.int32), arrs[f"top_idx_{ci}"]), ci
