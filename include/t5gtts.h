@@ -273,6 +273,11 @@ int64_t t5g_attention_decode_work_bytes(int32_t B, int32_t n_heads, int32_t n_kv
                                         int32_t cap);
 int t5g_attention_decode(const t5g_attn_decode_args* args, void* stream);
 
+/* Sampler launch shape: 0 (default) the 16-slice multi-block kernel, falling back per row to
+ * the single-block kernel when a row's top-k / survivor set exceeds it; 1 the single-block
+ * kernel only. Both pick the same tokens (tests/test_gpu_sampler.py). */
+int t5g_engine_set_sampler_path(t5g_engine* e, int32_t single_block);
+
 /* --- parity mode (csrc/exact.hip) ------------------------------------------------
  * Switch an engine to the exact-order kernels: every Linear, RMSNorm mean, q.k / P.V of
  * attention and GELU computed in the accumulation order of the reference's own CPU run
@@ -283,7 +288,7 @@ int t5g_attention_decode(const t5g_attn_decode_args* args, void* stream);
  * modeling_t5gemma.py:81-97, 264-304, PMCrossAttention :167-253 and the RMSNorm of [tf]
  * :61-78 inside t5g_encode / t5g_prefill / t5g_decode. gelu_lut: bf16 -> bf16 nn.GELU()
  * (erf) of the reference host, 65 536 entries indexed by the input bits (NULL: the
- * exact-erf form, equal except on 24 inputs in [-4.4, -3.1]); threads: the reference
+ * exact-erf form, equal except on 24 inputs in [-5.4, -3.1]); threads: the reference
  * host's torch thread count (8, the only measured K-split table; others -> EUNSUPPORTED).
  * enable = 0 returns to the fast kernels. Per-utterance token counts (text, prompt + 1)
  * must not exceed 512 in parity mode (the measured table). Synchronous. */

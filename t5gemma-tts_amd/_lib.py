@@ -119,6 +119,7 @@ SIGNATURES = {
     "t5g_attention_decode_work_bytes": (_L, [_I, _I, _I, _I, _I]),
     "t5g_attention_decode": (C.c_int, [C.POINTER(AttnDecodeArgs), _P]),
     "t5g_engine_set_exact": (C.c_int, [_P, _I, _P, _I]),
+    "t5g_engine_set_sampler_path": (C.c_int, [_P, _I]),
     "t5g_exact_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
     "t5g_exact_attention": (C.c_int, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
 }

@@ -99,9 +99,12 @@ def run_inference(reference_speech=None, target_text="こんにちは、私はAI
                   repeat_prompt=0, stop_repetition=3, sample_batch_size=1, seed=1, output_dir="./generated_tts",
                   cut_off_sec=100, dump_tokens=False, lang=None, codec_dir=None, tokenizer_dir=None, synthetic=None,
                   codec="44k", device="cuda:0", whisper_model="large-v3-turbo", model=None, audio_tokenizer=None,
-                  text_tokenizer=None, asr_model=None):
+                  text_tokenizer=None, asr_model=None, parity=True):
     """inference_commandline_hf.py:72-242. ``model`` / ``audio_tokenizer`` /
     ``text_tokenizer`` / ``asr_model`` may be passed pre-built (then nothing is loaded).
+    ``parity`` (default True, ``--parity False`` on the command line): reproduce the
+    reference's tokens bit for bit (exact-order kernels, reference RNG stream, one host sync
+    per step); False runs the fast graph-replayed path with on-device noise.
     Returns the path of the written wav."""
     from .audio import audio_info, write_wav
     from .pipeline import inference_one_sample, parse_silence_tokens
@@ -169,7 +172,8 @@ def run_inference(reference_speech=None, target_text="こんにちは、私はAI
                                lang=lang_code, device=device, decode_config=decode_config,
                                prompt_end_frame=prompt_end_frame, target_generation_length=target_generation_length,
                                prefix_transcript=prefix_transcript, multi_trial=multi_trial,
-                               repeat_prompt=repeat_prompt, return_frames=dump_tokens, prompt_sample_rate=prompt_sr)
+                               repeat_prompt=repeat_prompt, return_frames=dump_tokens, prompt_sample_rate=prompt_sr,
+                               parity=parity)
     if dump_tokens:
         concat_audio, gen_audio, concat_frames, gen_frames = res
     else:

@@ -74,7 +74,7 @@ struct t5g_engine {
     int* fs_ami;
     unsigned* fs_ticket;
     int* fs_slow;
-    bool fast_sampler = true;   // T5G_SAMPLER_FAST=0 at creation: single-block sampler only
+    bool fast_sampler = true;   // false: single-block sampler only (t5g_engine_set_sampler_path)
     // decode split-K factors (measured on MI355X): qkv 2, o / cross-q /
     // cross-o 4, down 8 k-slices; gate/up on the one-block-per-CU GEMV
     static constexpr int s_qkv = 2, s_o = 4, s_down = 8;
@@ -220,10 +220,6 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->fs_ami, (int64_t)B * FS_NB);
     rc |= alloc(e, &e->fs_ticket, B);
     rc |= alloc(e, &e->fs_slow, B);
-    {
-        const char* fsv = getenv("T5G_SAMPLER_FAST");
-        e->fast_sampler = !(fsv && fsv[0] == '0');
-    }
     if (rc) {
         t5g_engine_destroy(e);
         return T5G_ENOMEM;
@@ -573,6 +569,14 @@ extern "C" int t5g_engine_set_exact(t5g_engine* e, int32_t enable, const uint16_
     return T5G_OK;
 }
 
+extern "C" int t5g_engine_set_sampler_path(t5g_engine* e, int32_t single_block) {
+    if (!e) return T5G_EINVAL;
+    const bool fast = single_block == 0;
+    if (fast != e->fast_sampler) drop_graphs(e);   // the sampler launch is baked into the graphs
+    e->fast_sampler = fast;
+    return T5G_OK;
+}
+
 extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t* ids, const int32_t* tok_row,
                           const int32_t* tok_t, const float* pos, const int32_t* text_len, void* stream) {
     if (!e || B <= 0 || ntok <= 0) return T5G_EINVAL;
@@ -757,7 +761,10 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             g.ldx = e->q_dim;
             g.splits = s_o;
             g.layout_rx = 1;
-            return gemv_dec(g, EPI_F32, st);
+            // -1: the register-X GEMV's per-block LDS does not fit this device's CU count
+            // (e.g. a CPX partition): the tiled split-K GEMM below
+            const int rc = gemv_dec(g, EPI_F32, st);
+            if (rc != -1) return rc;
         }
         return gemm(x, e->q_dim, M, W, d, e->q_dim, s_o, nullptr, s_o > 1 ? (void*)e->part : (void*)tmp, d,
                     s_o > 1 ? EPI_F32 : EPI_BF16, st, !decode);
@@ -845,7 +852,9 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             g.ldx = d;
             g.un = 8;
             g.layout_rx = d == 2304;
-            RC(gemv_dec(g, EPI_GEGLU, st));
+            const int rc = gemv_dec(g, EPI_GEGLU, st);
+            if (rc == -1) RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st, !decode));
+            else RC(rc);
         } else {
             RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st, !decode));
         }
@@ -857,7 +866,9 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             g.ldx = f;
             g.splits = s_down;
             g.layout_rx = 1;
-            RC(gemv_dec(g, EPI_F32, st));
+            const int rc = gemv_dec(g, EPI_F32, st);
+            if (rc == -1) RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, e->part, d, EPI_F32, st, false));
+            else RC(rc);
         } else {
             RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, s_down > 1 ? (void*)e->part : (void*)tmp, d,
                     s_down > 1 ? EPI_F32 : EPI_BF16, st, !decode));
@@ -912,7 +923,10 @@ static int head(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st) {
         g.un = 8;
         g.layout_rx = 1;
         g.bias = (const bf16_t*)e->w.head2_bias;
-        RC(gemv_dec(g, EPI_BIAS_BF16, st));
+        const int rc = gemv_dec(g, EPI_BIAS_BF16, st);
+        if (rc == -1)
+            RC(gemm(e->dhh, d, B, e->w.head2, e->V, d, 1, e->w.head2_bias, e->logits, e->logits_ld, EPI_BIAS_BF16, st));
+        else RC(rc);
     } else {
         RC(gemm(e->dhh, d, B, e->w.head2, e->V, d, 1, e->w.head2_bias, e->logits, e->logits_ld, EPI_BIAS_BF16, st));
     }

@@ -394,7 +394,8 @@ static int launch_rx(const DecGemmArgs& a, hipStream_t st) {
         case 6: if constexpr (PER % 6 == 0) return launch_rx_nw<6, MT, EPI, PER>(a, st); else return -1;
         case 9: if constexpr (PER % 9 == 0) return launch_rx_nw<9, MT, EPI, PER>(a, st); else return -1;
         case 12: if constexpr (PER % 12 == 0) return launch_rx_nw<12, MT, EPI, PER>(a, st); else return -1;
-        default: if constexpr (PER % 8 == 0) return launch_rx_nw<8, MT, EPI, PER>(a, st); else return -1;
+        case 8: if constexpr (PER % 8 == 0) return launch_rx_nw<8, MT, EPI, PER>(a, st); else return -1;
+        default: return -1;   // a wave split the kernel is not built for (a different sum order)
     }
 }
 template <int MT>

@@ -9,8 +9,9 @@ SURVEY 8(a) rows covered here:
   and the codec call on the concatenated / generated frames (:359-366).
 
 Text normalisation and duration estimation are text.py; the prompt audio is encoded by
-the codec's XCodec2 encoder (codec_enc.py) when ``audio_fn`` is a path. Whisper
-transcription is not part of this build (callers pass the reference transcript).
+the codec's XCodec2 encoder (codec_enc.py) when ``audio_fn`` is a path. A missing
+reference transcript is produced by the Whisper recognizer (whisper_asr.py) in cli.py,
+as the reference CLI does (inference_commandline_hf.py:144-150).
 
 ``inference_batch`` is the batched form the reference lacks (its batch is asserted to
 1, :288): many utterances through one engine call and one batched codec decode.

@@ -6,7 +6,7 @@
   same reference noise draw -- except rows the kernel itself flags ambiguous (a tie
   group straddling the top-p cut), which parity mode resolves on the host.
 * With production (Philox) noise, the fast path and the single-block kernel
-  (T5G_SAMPLER_FAST=0) must pick the same tokens.
+  (t5g_engine_set_sampler_path(e, 1)) must pick the same tokens.
 """
 import ctypes as C
 import os
@@ -111,11 +111,9 @@ def test_device_sampler_equals_host_reference(mode):
 def test_fast_path_equals_single_block_kernel_philox():
     B = 8
     eng_fast = _engine(B)
-    os.environ["T5G_SAMPLER_FAST"] = "0"
-    try:
-        eng_slow = _engine(B)
-    finally:
-        del os.environ["T5G_SAMPLER_FAST"]
+    eng_slow = _engine(B)
+    from t5gemma_tts_amd import _lib
+    _lib.check(_lib.lib().t5g_engine_set_sampler_path(eng_slow.h, 1), "set_sampler_path")
     g = torch.Generator().manual_seed(11)
     diff = total = 0
     for it in range(8):

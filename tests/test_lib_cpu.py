@@ -80,6 +80,8 @@ def test_host_sampler_matches_reference_golden():
     (1, 8, 2304, 5, 4, 4),      # 72 k-steps do not split in 5
     (0, 17, 2304, 1, 3, 8),     # LDS-staged X: at most 16 rows
     (2, 8, 2304, 1, 3, 8),      # no third layout
+    (1, 8, 2304, 1, 3, 16),     # register-X wave counts: 4 / 6 / 8 / 9 / 12 only
+    (1, 8, 2304, 1, 3, 5),
 ])
 def test_gemv_rejects_unsupported_shapes(layout, M, K, splits, epi, nw):
     """t5g_gemv validates on the host and returns an error code before any launch for the
