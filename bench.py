@@ -1,17 +1,24 @@
 """Throughput benchmark: T5Gemma-TTS-2b-2b generate() on MI355X.
 
-Default workload (BASELINE.json metric, configs[2], C3): bf16, batch 8 voice-cloning
-utterances per GPU -- T_x = 60 text tokens (28 transcript + x_sep + 31 target),
-T_p = 151 prompt frames (150 codes + y_sep), tgt_y_lens = T_p + 500 (10 s),
-top-k 30 / top-p 0.9 / T 0.8, throughput mode (EOS never accepted before the
-time budget) so every row emits exactly 751 tokens (incl. EOS).
-A "step" = one full generate() (encoder + prefill + AR loop + on-device stop
-rules) over the batch. Weights: seeded random at the exact 2b-2b shapes (no
-checkpoint download); data: synthetic.
+Workloads (BASELINE.json configs; ``--workload``, default c3 = the headline metric):
+* c3 (configs[2], default): bf16, batch 8 voice-cloning utterances per GPU -- T_x = 60 text
+  tokens (28 transcript + x_sep + 31 target), T_p = 151 prompt frames (150 codes + y_sep),
+  tgt_y_lens = T_p + 500 (10 s), top-k 30 / top-p 0.9 / T 0.8, throughput mode (EOS never
+  accepted before the time budget) so every row emits exactly 751 tokens.
+* c2 (configs[1]): batch 1, T_x 32, no prompt, 10 s target (751 tokens).
+* c4 (configs[3]): T_x 36 (a 128-character text), no prompt, 10 s, 8 utterances per GPU
+  -- ``--gpus 8`` is the 64-utterance node batch.
+* c5 (configs[4], also ``--e2e``): batch 32 per GPU, the c3 rows, generate() plus the
+  batched XCodec2 decode of every row at 882 samples per token (Anime-XCodec2-44.1kHz-v2
+  rate) inside the timed region; reports the real-time factor.
+A "step" = one full generate() (encoder + prefill + AR loop + on-device stop rules) over
+the batch. Weights: seeded random at the exact 2b-2b shapes (no checkpoint download);
+data: synthetic.
 
-``--e2e`` (configs[4], C5): batch 32 per GPU, 10 s target, generate() plus the batched
-XCodec2 decode of every row at 882 samples per token (Anime-XCodec2-44.1kHz-v2 rate)
-inside the timed region; reports the real-time factor.
+``--parity``: time the drop-in default path instead (``inference_tts`` /
+``inference_one_sample`` run ``parity=True``: exact-order kernels, the reference's CPU RNG
+stream, one host sync per step, EOS accepted as in the reference), and print the
+reference's own ``[Speed]`` line (inference_tts_utils.py:308-321) for it.
 
 Multi-GPU: ``--gpus N`` launches N ranks itself (one process per GPU via
 torch.distributed.run, before any GPU call) unless it already runs under a launcher
@@ -32,31 +39,49 @@ sys.path.insert(0, REPO)
 
 import numpy as np  # noqa: E402
 
-T_X, T_P, DUR_FRAMES = 60, 151, 500
+DUR_FRAMES = 500
+# name -> (utterances per GPU, T_x, T_p incl. y_sep (0: no prompt), e2e, BASELINE configs index)
+WORKLOADS = {
+    "c2": (1, 32, 0, False, 1),
+    "c3": (8, 60, 151, False, 2),
+    "c4": (8, 36, 0, False, 3),
+    "c5": (32, 60, 151, True, 4),
+}
+T_X, T_P = 60, 151          # c3 (kept for tools that import them)
 B_PER_GPU = 8
 B_PER_GPU_E2E = 32
-CPU_SAMPLE_TOKENS = 160
+CPU_SAMPLE_STEPS = 8        # decode steps timed at each sampled cache length
+CPU_SAMPLE_LENS = (450, 750, 900)
 
 
-def make_batch(cfg, n: int, seed: int):
+def make_batch(cfg, n: int, seed: int, T_x: int = T_X, T_p: int = T_P):
+    """n synthetic utterances: text ids (x_sep after the 28-id transcript when there is a
+    prompt), T_p - 1 prompt codes + y_sep (none when T_p = 0), tgt_y_lens = T_p + 500."""
     rng = np.random.default_rng(seed)
     rows = []
     for _ in range(n):
-        x = rng.integers(3, cfg.backbone.text_vocab_size - 1, size=T_X)
-        x[28] = cfg.x_sep_token
-        y = rng.integers(0, cfg.audio_vocab_size, size=T_P - 1).tolist() + [cfg.y_sep_token]
-        rows.append((x.tolist(), y, T_P + DUR_FRAMES))
+        x = rng.integers(3, cfg.backbone.text_vocab_size - 1, size=T_x)
+        if T_p:
+            x[28] = cfg.x_sep_token
+            y = rng.integers(0, cfg.audio_vocab_size, size=T_p - 1).tolist() + [cfg.y_sep_token]
+        else:
+            y = []
+        rows.append((x.tolist(), y, T_p + DUR_FRAMES))
     return rows
 
 
-def cpu_baseline(cfg, sd_gpu, utt, n_tokens: int = CPU_SAMPLE_TOKENS):
-    """Time the CPU oracle (the reference's algorithm restated in PyTorch CPU ops, pinned
-    bitwise to the reference's golden vectors) over a complete, measured generate() of
-    one utterance of the same workload: encoder + prefill + ``n_tokens`` AR steps, batch 1
-    as the reference. Nothing is extrapolated; the rate is tokens / wall time like the
-    reference's own [Speed] line (inference_tts_utils.py:289, 308-321)."""
+def cpu_baseline(cfg, sd_gpu, utt, n_budget: int):
+    """The CPU oracle (the reference's algorithm in PyTorch CPU ops, pinned bitwise to the
+    reference's golden vectors) on one utterance of the workload, batch 1 as the reference.
+    Bounded sample of the whole generate(): encoder + prefill and CPU_SAMPLE_STEPS decode
+    steps right after it are timed on the utterance itself; the per-step time further into
+    the row (larger self-attention cache) is timed at CPU_SAMPLE_LENS keys, each on the same
+    utterance with its prompt extended to that length (prefill untimed). A least-squares
+    line through the step times over the cache length gives the time of all ``n_budget``
+    steps; rate = n_budget / (prefill + steps), the reference's [Speed] definition
+    (inference_tts_utils.py:308-321)."""
     import torch
-    from oracle.t5g_oracle import SamplerParams, T5GemmaTTSOracle
+    from oracle.t5g_oracle import SamplerParams, T5GemmaTTSOracle, draw_noise, sample_helper
     threads = int(os.environ.get("OMP_NUM_THREADS", torch.get_num_threads()))
     torch.set_num_threads(threads)
     sd = {k: v.cpu() for k, v in sd_gpu.items()}
@@ -64,14 +89,46 @@ def cpu_baseline(cfg, sd_gpu, utt, n_tokens: int = CPU_SAMPLE_TOKENS):
     x, y, tgt = utt
     p = SamplerParams(top_k=30, top_p=0.9, temperature=0.8, eos_disabled=True)
     t0 = time.perf_counter()
-    out = orc.generate(x, y, tgt, p, seed=1, max_steps=n_tokens)
-    dt = time.perf_counter() - t0
-    n = int(out["gen"].numel())
-    return {"value": round(n / dt, 3), "unit": "audio tokens/s", "cores": threads, "kind": "port",
-            "sample": f"1 utterance of this workload (T_x {T_X}, T_p {T_P}), complete generate(): encoder + "
-                      f"prefill + {n} AR steps (self-attention keys {T_P + 1}..{T_P + n}) in {dt:.1f} s, "
-                      f"batch 1 (reference semantics); the reference itself measured 7.04 tok/s on 8 cores "
-                      f"(SURVEY 6)"}
+    ctx = orc.prepare(x, y, tgt)
+    t_pre = time.perf_counter() - t0
+    rng = np.random.default_rng(5)
+    pts = []
+    L0 = len(y) + 1
+
+    gen = torch.Generator().manual_seed(1)
+
+    def time_steps(c):
+        # one AR step as generate() runs it: head, sample_helper (+ its noise draw), embed +
+        # decoder step
+        st = c["state"]
+        t1 = time.perf_counter()
+        for _ in range(CPU_SAMPLE_STEPS):
+            logits = orc.step_logits(c)
+            tok, _ = sample_helper(logits, p, st, draw_noise(gen, logits.shape[-1]), eos=cfg.eog_inference,
+                                   encodec_sr=cfg.encodec_sr, extra_cutoff=cfg.extra_cutoff)
+            st.cur_num_gen += 1
+            st.current_length += 1
+            orc.advance(c, tok)
+        return (time.perf_counter() - t1) / CPU_SAMPLE_STEPS
+
+    pts.append((L0, time_steps(ctx)))
+    for L in CPU_SAMPLE_LENS:
+        # the same text, a prompt of L - 2 codes + y_sep: the step then attends over L keys
+        yl = rng.integers(0, cfg.audio_vocab_size, size=L - 2).tolist() + [cfg.y_sep_token]
+        c = orc.prepare(x, yl, len(yl) + DUR_FRAMES)
+        pts.append((len(yl) + 1, time_steps(c)))
+    Ls = np.array([q[0] for q in pts], float)
+    ts = np.array([q[1] for q in pts], float)
+    b, a = np.polyfit(Ls, ts, 1)
+    steps = a * n_budget + b * sum(L0 + i for i in range(n_budget))
+    total = t_pre + steps
+    return {"value": round(n_budget / total, 3), "unit": "audio tokens/s", "cores": threads, "kind": "port",
+            "sample": f"1 utterance of this workload (T_x {len(x)}, T_p {len(y)}), batch 1 (reference semantics): "
+                      f"encoder + prefill {t_pre:.1f} s timed; decode step times at cache lengths "
+                      + ", ".join(f"{int(l)}: {t * 1e3:.0f} ms" for l, t in pts)
+                      + f" ({CPU_SAMPLE_STEPS} steps each), fitted linearly over all {n_budget} steps "
+                      f"(L {L0}..{L0 + n_budget - 1}): {steps:.1f} s; the reference itself measured 7.04 tok/s "
+                      f"on 8 cores in the build container (SURVEY 6)"}
 
 
 def main():
@@ -80,7 +137,12 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--batch", type=int, default=0, help="utterances per GPU (default 8, --e2e 32)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
+                    help="BASELINE config: c2 / c3 (default) / c4 / c5 (= --e2e)")
+    ap.add_argument("--parity", action="store_true",
+                    help="time the drop-in default path (parity=True: exact-order kernels, reference RNG, "
+                         "one host sync per step, EOS accepted) and print the reference's [Speed] line")
+    ap.add_argument("--batch", type=int, default=0, help="utterances per GPU (default: the workload's)")
     ap.add_argument("--natural-eos", action="store_true",
                     help="accept EOS when sampled (SURVEY 8(d)'s second run) instead of throughput mode")
     ap.add_argument("--e2e", action="store_true", help="C5: generate + XCodec2 decode in the timed region")
@@ -88,6 +150,10 @@ def main():
                     help="nccl (= RCCL, default) or gloo (CPU collectives; lets N ranks share one GPU "
                          "to rehearse the sharded path)")
     args = ap.parse_args()
+    if args.e2e:
+        args.workload = "c5"
+    wl_b, wl_tx, wl_tp, wl_e2e, wl_cfg = WORKLOADS[args.workload]
+    args.e2e = wl_e2e
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU, started before this process touches the GPU
@@ -122,12 +188,12 @@ def main():
     from t5gemma_tts_amd.weights import synthetic_weights
 
     cfg = config_2b2b()
-    B = args.batch or (B_PER_GPU_E2E if args.e2e else B_PER_GPU)
+    B = args.batch or wl_b
     torch.manual_seed(1234)
     sd = synthetic_weights(cfg, seed=1234, device=str(dev))
     n_tok_row = DUR_FRAMES + int(cfg.extra_budget) + 1
     eng = T5GemmaTTSEngine(cfg, sd, device=str(dev), max_batch=B, max_text=64,
-                           max_audio=T_P + 1 + n_tok_row + 8, max_gen=n_tok_row + 4)
+                           max_audio=wl_tp + 1 + n_tok_row + 8, max_gen=n_tok_row + 4)
     codec = None
     if args.e2e:
         from t5gemma_tts_amd.codec import XCodec2Decoder, codec_44k, synthetic_codec_weights
@@ -141,17 +207,26 @@ def main():
     G = B * world
     rows = costs = None
     if rank == 0:
-        rows = [[len(x), tgt] + x + y for x, y, tgt in make_batch(cfg, G, seed=20251226)]
+        rows = [[len(x), tgt] + x + y for x, y, tgt in make_batch(cfg, G, seed=20251226, T_x=wl_tx, T_p=wl_tp)]
         costs = [r[1] for r in rows]
     params = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3,
-                            eos_disabled=not args.natural_eos)
+                            eos_disabled=not (args.natural_eos or args.parity))
+    speed_lines = []
     gen_tokens = [0]
     audio_frames = [0]
 
     def generate(shard, i):
         utts = [Utterance(x=r[2:2 + r[0]], y=r[2 + r[0]:], tgt_y_len=r[1]) for r in shard]
-        out = eng.generate(utts, params, seeds=[1000 * i + rank * B + b for b in range(len(utts))], chunk=64)
-        gen_tokens[0] += sum(len(g) for g in out["gen"])
+        t_call = time.perf_counter()
+        out = eng.generate(utts, params, seeds=[1000 * i + rank * B + b for b in range(len(utts))], chunk=64,
+                           parity=args.parity)
+        n_gen = sum(len(g) for g in out["gen"])
+        gen_tokens[0] += n_gen
+        if args.parity:
+            # the reference's own report (inference_tts_utils.py:308-321)
+            dt_call = time.perf_counter() - t_call
+            speed_lines.append(f"[Speed] {n_gen / dt_call:.2f} tokens/s | RTF: {n_gen / 50.0 / dt_call:.2f}x | "
+                               f"Generated {n_gen} tokens in {dt_call:.2f}s")
         if codec is not None:
             # strip EOS (inference_tts_utils.py:323-354) and decode every row in one launch
             frames = [g[g != cfg.eog_inference] for g in out["gen"]]
@@ -197,7 +272,7 @@ def main():
 
     # ---- roofline of the dominant kernel: decode GeGLU gate/up GEMV (largest weight stream)
     roof = None
-    if rank == 0 and not args.e2e:
+    if rank == 0 and not args.e2e and not args.parity:
         import ctypes as C
         from t5gemma_tts_amd import _lib
         L = _lib.lib()
@@ -227,7 +302,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.e2e:
         r0 = rows[0]
-        cpu = cpu_baseline(cfg, sd, (r0[2:2 + r0[0]], r0[2 + r0[0]:], r0[1]))
+        cpu = cpu_baseline(cfg, sd, (r0[2:2 + r0[0]], r0[2 + r0[0]:], r0[1]), n_tok_row)
 
     if rank == 0:
         ms = dt_max / args.steps * 1e3
@@ -243,26 +318,35 @@ def main():
                 "config": {"workload": f"C5 end-to-end: 2b-2b bf16, {B} utterances/GPU, T_x 60, T_p 151, 10 s "
                                        f"target (751 tokens/utterance), generate + XCodec2 decode at {hop} "
                                        f"samples/token in the timed region",
-                           "global_batch": B * world, "seq_len": T_P + 1 + n_tok_row,
+                           "global_batch": B * world, "seq_len": wl_tp + 1 + n_tok_row,
                            "parallelism": f"dp{world} (utterance shards)"},
                 "audio_tokens_per_s": round(value, 2), "wall_s_per_audio_s": round(dt_max / audio_s, 5),
                 "samples_per_s": round(frames_all * hop / dt_max, 1),
             }
         else:
+            prompt = f"T_p {wl_tp} (voice clone)" if wl_tp else "no prompt"
+            desc = {"c2": "C2 single utterance", "c3": "C3 voice-clone", "c4": "C4 text-only"}[args.workload]
+            mode = ("parity mode (drop-in default: exact-order kernels, reference RNG stream, host sync per "
+                    "step, EOS accepted)" if args.parity else
+                    "top-k 30/top-p 0.9/T 0.8" + (", EOS accepted when sampled" if args.natural_eos else ""))
             line = {
-                "metric": "XCodec2 audio tokens/sec (whole node) + RTF, T5Gemma-TTS-2b-2b bs=8",
+                "metric": "XCodec2 audio tokens/sec (whole node) + RTF, T5Gemma-TTS-2b-2b bs=8"
+                          if args.workload == "c3" and not args.parity else
+                          f"XCodec2 audio tokens/sec (whole node) + RTF, T5Gemma-TTS-2b-2b, BASELINE configs[{wl_cfg}]"
+                          + (" parity mode" if args.parity else ""),
                 "value": round(value, 2), "unit": "audio tokens/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "bf16",
                 "data": "synthetic (seeded random 2b-2b weights, random text/prompt codes)",
-                "config": {"workload": f"C3 voice-clone: 2b-2b bf16, {B} utterances/GPU, T_x 60, T_p 151, "
-                                       "10 s target (751 tokens/utterance), top-k 30/top-p 0.9/T 0.8"
-                                       + (", EOS accepted when sampled" if args.natural_eos else ""),
-                           "global_batch": B * world, "seq_len": T_P + 1 + n_tok_row,
+                "config": {"workload": f"{desc}: 2b-2b bf16, {B} utterances/GPU, T_x {wl_tx}, {prompt}, "
+                                       f"10 s target (751 tokens/utterance), {mode}",
+                           "global_batch": B * world, "seq_len": wl_tp + 1 + n_tok_row,
                            "parallelism": f"dp{world} (utterance shards)"},
                 "rtf_audio_s_per_wall_s": round(value / 50.0, 3),
                 "roofline": roof, "cpu_baseline": cpu,
             }
+            if speed_lines:
+                line["reference_speed_lines"] = speed_lines[-args.steps:]
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

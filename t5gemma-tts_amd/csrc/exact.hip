@@ -153,12 +153,9 @@ __global__ __launch_bounds__(NW * 64) void exact_linear_kernel(ExactLinArgs a) {
     }
 }
 
-int exact_linear(const ExactLinArgs& a, int epi, hipStream_t st) {
-    if (a.M <= 0) return 0;
-    if (!a.X || !a.W || !a.Y || a.N <= 0 || a.KB <= 0 || a.NG % 4) return -1;
-    if ((epi == EPI_BIAS_BF16 || epi == EPI_BIAS_GELU) && !a.bias) return -1;
-    if (epi == EPI_GEGLU && a.N % 16) return -1;
-    constexpr int RT = 8, NW = 8;
+template <int RT>
+static int launch_exact_linear(const ExactLinArgs& a, int epi, hipStream_t st) {
+    constexpr int NW = 8;
     const dim3 grid((unsigned)(a.NG / 4), (unsigned)((a.M + RT - 1) / RT)), blk(NW * 64);
     switch (epi) {
         case EPI_F32: hipLaunchKernelGGL((exact_linear_kernel<RT, NW, EPI_F32>), grid, blk, 0, st, a); break;
@@ -169,6 +166,18 @@ int exact_linear(const ExactLinArgs& a, int epi, hipStream_t st) {
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int exact_linear(const ExactLinArgs& a, int epi, hipStream_t st) {
+    if (a.M <= 0) return 0;
+    if (!a.X || !a.W || !a.Y || a.N <= 0 || a.KB <= 0 || a.NG % 4) return -1;
+    if ((epi == EPI_BIAS_BF16 || epi == EPI_BIAS_GELU) && !a.bias) return -1;
+    if (epi == EPI_GEGLU && a.N % 16) return -1;
+    // rows per tile: the batch of a decode step (1..8 rows) without idle rows; 8 beyond
+    if (a.M <= 1) return launch_exact_linear<1>(a, epi, st);
+    if (a.M <= 2) return launch_exact_linear<2>(a, epi, st);
+    if (a.M <= 4) return launch_exact_linear<4>(a, epi, st);
+    return launch_exact_linear<8>(a, epi, st);
 }
 
 // ---------------------------------------------------------------------------------
