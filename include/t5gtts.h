@@ -171,10 +171,12 @@ int t5g_write_state(t5g_engine* e, const t5g_sampler_state* state, int32_t row, 
                     int32_t token, void* stream);
 
 /* Parity-mode pieces of one AR iteration: sample only (flags readable), then
- * the decoder step + head only. t5g_read_flags: bit0 = ambiguous top-p tie cut,
- * bit1 = argmax was EOS (synchronous). */
+ * the decoder step + head only (replayed from a graph captured on first use per
+ * batch size). t5g_read_flags: bit0 = ambiguous top-p tie cut, bit1 = argmax was
+ * EOS (synchronous); t5g_read_step: the row states and the flags in one sync. */
 int t5g_step_only(t5g_engine* e, void* stream);
 int t5g_read_flags(t5g_engine* e, int32_t* flags_out, int32_t B, void* stream);
+int t5g_read_step(t5g_engine* e, t5g_sampler_state* state_out, int32_t* flags_out, int32_t B, void* stream);
 /* Host re-run of one sampler step with torch.sort's exact std::sort tie order
  * (resolves ambiguous steps; see csrc/host_sampler.cpp). Pure host function.
  * max_gen / max_len: the engine's generated-token and self-attention cache capacity
@@ -231,7 +233,8 @@ typedef struct {
     const void* pre_w;        /* reserved */
     void* h_out;              /* reserved */
     void* x_out;              /* reserved */
-    int32_t un;               /* tuning: fragments in flight per wave (8 / 16), 0 = default */
+    int32_t un;               /* tuning: fragments in flight per wave (8 / 16), 0 = default; layout 1:
+                                 -1 = every unit's weights requested before the first MFMA */
     int32_t max_grid;         /* tuning: blocks per launch cap, 0 = one per CU */
     int32_t splits;           /* split-K (epi 4): fp32 slabs [splits][M][ldy]; 0/1 = none */
     int32_t layout;           /* 0: the LDS-staged-X GEMV (M <= 16); 1: the register-resident-X

@@ -105,6 +105,7 @@ SIGNATURES = {
     "t5g_write_state": (C.c_int, [_P, C.POINTER(SamplerState), _I, _I, _I, _P]),
     "t5g_step_only": (C.c_int, [_P, _P]),
     "t5g_read_flags": (C.c_int, [_P, _P, _I, _P]),
+    "t5g_read_step": (C.c_int, [_P, _P, _P, _I, _P]),
     "t5g_host_sample": (C.c_int, [_P, _I, C.POINTER(SamplerRow), _P, _P, C.POINTER(SamplerState), _P, _I, _I,
                                   _F, _I, _F, _I, _I, C.POINTER(SamplerState), C.POINTER(_I)]),
     "t5g_logits_ptr": (_P, [_P, C.POINTER(_I)]),

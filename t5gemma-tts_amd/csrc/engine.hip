@@ -88,6 +88,10 @@ struct t5g_engine {
     hipGraph_t graph = nullptr, graph_n = nullptr;
     hipGraphExec_t gexec = nullptr, gexec_n = nullptr;
     int graph_B = -1;
+    // graph of one decoder step + head without the sampler (t5g_step_only: parity mode)
+    hipGraph_t graph_fwd = nullptr;
+    hipGraphExec_t gexec_fwd = nullptr;
+    int graph_fwd_B = -1;
     hipStream_t graph_stream = nullptr;
     hipStream_t cap_stream = nullptr;
     // parity mode (t5g_engine_set_exact): every sum in the reference host's CPU order
@@ -125,8 +129,10 @@ static void drop_graphs(t5g_engine* e) {
     if (e->gexec_n) hipGraphExecDestroy(e->gexec_n);
     if (e->graph) hipGraphDestroy(e->graph);
     if (e->graph_n) hipGraphDestroy(e->graph_n);
-    e->gexec = e->gexec_n = nullptr;
-    e->graph = e->graph_n = nullptr;
+    if (e->gexec_fwd) hipGraphExecDestroy(e->gexec_fwd);
+    if (e->graph_fwd) hipGraphDestroy(e->graph_fwd);
+    e->gexec = e->gexec_n = e->gexec_fwd = nullptr;
+    e->graph = e->graph_n = e->graph_fwd = nullptr;
 }
 
 extern "C" int t5g_engine_destroy(t5g_engine* e) {
@@ -850,7 +856,9 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             DecGemmArgs g = dec_args(M, L.gate_up, 2 * f, d, act, f, d == 2304 ? 12 : 8);
             g.X = xn;
             g.ldx = d;
-            g.un = 8;
+            // register-X at 2b-2b width: every unit's weights requested up front (18.84 ->
+            // 18.39 us at 8 rows, 24.2 -> 23.9 at 32, bitwise equal: tools/probe_rx_all.py)
+            g.un = d == 2304 ? -1 : 8;
             g.layout_rx = d == 2304;
             const int rc = gemv_dec(g, EPI_GEGLU, st);
             if (rc == -1) RC(gemm(xn, d, M, L.gate_up, 2 * f, d, 1, nullptr, act, f, EPI_GEGLU, st, !decode));
@@ -1104,13 +1112,50 @@ extern "C" int t5g_write_state(t5g_engine* e, const t5g_sampler_state* s, int32_
 
 extern "C" int t5g_step_only(t5g_engine* e, void* stream) {
     if (!e || e->B <= 0) return T5G_EINVAL;
-    return decode_forward(e, (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    // replayed from a graph: the step reads its tokens / positions / lengths from device
+    // memory, so one capture per batch size serves every step (~250 launches in parity mode)
+    if (!e->gexec_fwd || e->graph_fwd_B != e->B) {
+        if (e->gexec_fwd) hipGraphExecDestroy(e->gexec_fwd);
+        if (e->graph_fwd) hipGraphDestroy(e->graph_fwd);
+        e->gexec_fwd = nullptr;
+        e->graph_fwd = nullptr;
+        if (!e->cap_stream) HIPCHK(hipStreamCreateWithFlags(&e->cap_stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamBeginCapture(e->cap_stream, hipStreamCaptureModeThreadLocal));
+        const int rc = decode_forward(e, e->cap_stream);
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(e->cap_stream, &g);
+        if (rc || ec != hipSuccess) {
+            if (g) hipGraphDestroy(g);
+            return rc ? rc : T5G_EHIP;
+        }
+        hipGraphExec_t x = nullptr;
+        if (hipGraphInstantiate(&x, g, nullptr, nullptr, 0) != hipSuccess) {
+            hipGraphDestroy(g);
+            return T5G_EHIP;
+        }
+        e->graph_fwd = g;
+        e->gexec_fwd = x;
+        e->graph_fwd_B = e->B;
+    }
+    HIPCHK(hipGraphLaunch(e->gexec_fwd, st));
+    return T5G_OK;
 }
 
 extern "C" int t5g_read_flags(t5g_engine* e, int32_t* out, int32_t B, void* stream) {
     if (!e || !out || B <= 0 || B > e->c.max_batch) return T5G_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipMemcpyAsync(out, e->flags, B * sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return T5G_OK;
+}
+
+extern "C" int t5g_read_step(t5g_engine* e, t5g_sampler_state* state_out, int32_t* flags_out, int32_t B,
+                             void* stream) {
+    if (!e || !state_out || !flags_out || B <= 0 || B > e->c.max_batch) return T5G_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(state_out, e->state, B * sizeof(SamplerState), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(flags_out, e->flags, B * sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return T5G_OK;
 }

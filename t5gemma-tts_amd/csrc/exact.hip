@@ -57,77 +57,10 @@ extern "C" int t5g_dbg_set_exact(void* p) {
 // the scalar cache: its address is wave-uniform) and stores the chunk sums in LDS; after
 // the barrier wave r folds row r's chunk sums of the stage, in chunk order. Two LDS
 // buffers let stage s+1's chunks be computed while stage s is folded.
-template <int RT, int NW, int EPI>
-__global__ __launch_bounds__(NW * 64) void exact_linear_kernel(ExactLinArgs a) {
-    static_assert(RT <= NW, "every folded row needs a wave");
-    __shared__ float cs[2][RT][NW][64];
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int g = blockIdx.x * 4 + (lane >> 4);
-    const int r16 = lane & 15;
-    const int n = blockIdx.x * 64 + lane;       // packed output row
-    const int m0 = blockIdx.y * RT;
-    const int KB = a.KB;
-    const bf16_t* wg = a.W + (long)g * KB * 512;
-    // fold state of row m0 + w (waves < RT)
-    float tot = 0.f, part = 0.f;
-    int kbc = KB;
-    if (w < RT) {
-        const int m = min(m0 + w, a.M - 1);
-        const int mu = a.row_len ? a.row_len[a.tok_row ? a.tok_row[m] : m] : 1;
-        const uint16_t* tab = (a.kb_b && n >= a.nsplit_col) ? a.kb_b : a.kb_a;
-        if (tab) kbc = tab[min(max(mu, 1), a.kb_len) - 1];
-        if (kbc <= 0) kbc = KB;
-    }
-    const int nst = (KB + NW - 1) / NW;
-    for (int s = 0; s < nst; ++s) {
-        const int kb = s * NW + w;
-        if (kb < KB) {
-            u32x4 wv[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) wv[j] = *(const u32x4*)(wg + ((long)kb * 64 + j * 16 + r16) * 8);
-            float wf[32];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    wf[8 * j + 2 * q] = bf_lo(wv[j][q]);
-                    wf[8 * j + 2 * q + 1] = bf_hi(wv[j][q]);
-                }
-#pragma unroll
-            for (int r = 0; r < RT; ++r) {
-                const int m = min(m0 + r, a.M - 1);
-                const uint32_t* xr = (const uint32_t*)(a.X + (long)m * a.ldx + kb * 32);
-                float e = 0.f, o = 0.f;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const uint32_t xw = xr[i];
-                    e = fmaf(bf_lo(xw), wf[2 * i], e);
-                    o = fmaf(bf_hi(xw), wf[2 * i + 1], o);
-                }
-                cs[s & 1][r][w][lane] = __fadd_rn(e, o);
-            }
-        }
-        __syncthreads();
-        if (w < RT) {
-#pragma unroll
-            for (int i = 0; i < NW; ++i) {
-                const int kb2 = s * NW + i;
-                if (kb2 < KB) {
-                    const float c = cs[s & 1][w][i][lane];
-                    if (kb2 % kbc == 0) {
-                        if (kb2 > 0) tot = __fadd_rn(tot, part);
-                        part = __fadd_rn(0.f, c);
-                    } else {
-                        part = __fadd_rn(part, c);
-                    }
-                }
-            }
-        }
-    }
-    if (w >= RT) return;
-    const int m = m0 + w;
-    const float y = KB > kbc ? __fadd_rn(tot, part) : part;
+// Epilogue of output (row m, packed column n = g*16 + r16); y = the folded fp32 sum.
+// Called by whole waves (GEGLU pairs lanes r16 and r16 + 8).
+template <int EPI>
+__device__ __forceinline__ void exact_lin_store(const ExactLinArgs& a, int m, int g, int r16, int n, float y) {
     if constexpr (EPI == EPI_GEGLU) {
         // rows g*16 + 0..7 gate, + 8..15 up of features g*8 + 0..7 (engine.py interleave)
         const float other = xlane<8>(y);
@@ -153,6 +86,104 @@ __global__ __launch_bounds__(NW * 64) void exact_linear_kernel(ExactLinArgs a) {
     }
 }
 
+// The K-split chunk size (32-element chunks per part) of row m for packed column n.
+__device__ __forceinline__ int exact_lin_kbc(const ExactLinArgs& a, int m, int n) {
+    const int mu = a.row_len ? a.row_len[a.tok_row ? a.tok_row[m] : m] : 1;
+    const uint16_t* tab = (a.kb_b && n >= a.nsplit_col) ? a.kb_b : a.kb_a;
+    int kbc = tab ? tab[min(max(mu, 1), a.kb_len) - 1] : a.KB;
+    return kbc <= 0 ? a.KB : kbc;
+}
+
+// One 32-element chunk sum (even chain + odd chain) of X row xr against the lane's
+// unpacked weight chunk wf.
+__device__ __forceinline__ float exact_chunk(const uint32_t* xr, const float* wf) {
+    float e = 0.f, o = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t xw = xr[i];
+        e = fmaf(bf_lo(xw), wf[2 * i], e);
+        o = fmaf(bf_hi(xw), wf[2 * i + 1], o);
+    }
+    return __fadd_rn(e, o);
+}
+
+// exact_chunk with X's chunk read through vector loads (lanes of a wave on different chunks)
+__device__ __forceinline__ float exact_chunk_v(const u32x4* xr4, const float* wf) {
+    u32x4 xv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = xr4[j];
+    float e = 0.f, o = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t xw = xv[i >> 2][i & 3];
+        e = fmaf(bf_lo(xw), wf[2 * i], e);
+        o = fmaf(bf_hi(xw), wf[2 * i + 1], o);
+    }
+    return __fadd_rn(e, o);
+}
+
+__device__ __forceinline__ void exact_load_chunk(const bf16_t* wg, int kb, int r16, float* wf) {
+    u32x4 wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wv[j] = *(const u32x4*)(wg + ((long)kb * 64 + j * 16 + r16) * 8);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            wf[8 * j + 2 * q] = bf_lo(wv[j][q]);
+            wf[8 * j + 2 * q + 1] = bf_hi(wv[j][q]);
+        }
+}
+
+template <int RT, int NW, int EPI>
+__global__ __launch_bounds__(NW * 64) void exact_linear_kernel(ExactLinArgs a) {
+    static_assert(RT <= NW, "every folded row needs a wave");
+    __shared__ float cs[2][RT][NW][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = blockIdx.x * 4 + (lane >> 4);
+    const int r16 = lane & 15;
+    const int n = blockIdx.x * 64 + lane;       // packed output row
+    const int m0 = blockIdx.y * RT;
+    const int KB = a.KB;
+    const bf16_t* wg = a.W + (long)g * KB * 512;
+    // fold state of row m0 + w (waves < RT)
+    float tot = 0.f, part = 0.f;
+    int kbc = KB;
+    if (w < RT) kbc = exact_lin_kbc(a, min(m0 + w, a.M - 1), n);
+    const int nst = (KB + NW - 1) / NW;
+    for (int s = 0; s < nst; ++s) {
+        const int kb = s * NW + w;
+        if (kb < KB) {
+            float wf[32];
+            exact_load_chunk(wg, kb, r16, wf);
+#pragma unroll
+            for (int r = 0; r < RT; ++r) {
+                const int m = min(m0 + r, a.M - 1);
+                cs[s & 1][r][w][lane] = exact_chunk((const uint32_t*)(a.X + (long)m * a.ldx + kb * 32), wf);
+            }
+        }
+        __syncthreads();
+        if (w < RT) {
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int kb2 = s * NW + i;
+                if (kb2 < KB) {
+                    const float c = cs[s & 1][w][i][lane];
+                    if (kb2 % kbc == 0) {
+                        if (kb2 > 0) tot = __fadd_rn(tot, part);
+                        part = __fadd_rn(0.f, c);
+                    } else {
+                        part = __fadd_rn(part, c);
+                    }
+                }
+            }
+        }
+    }
+    if (w >= RT) return;
+    exact_lin_store<EPI>(a, m0 + w, g, r16, n, KB > kbc ? __fadd_rn(tot, part) : part);
+}
+
 template <int RT>
 static int launch_exact_linear(const ExactLinArgs& a, int epi, hipStream_t st) {
     constexpr int NW = 8;
@@ -168,12 +199,107 @@ static int launch_exact_linear(const ExactLinArgs& a, int epi, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+
+// Decode-size launches (M <= 8 rows): one workgroup per 16-row group g of W (16 output
+// columns; 64-column tiles would leave most of the chip idle), 16 waves. A stage covers
+// 64 chunks: wave w computes chunks 4w + (lane >> 4) for column lane & 15 and RT rows of
+// X; after the barrier thread (row tid >> 4, column tid & 15) folds the stage's chunk sums
+// of its row in chunk order -- the same order and arithmetic as exact_linear_kernel.
+template <int RT, int EPI>
+__global__ __launch_bounds__(1024) void exact_linear_g16_kernel(ExactLinArgs a) {
+    constexpr int SC = 64, SP = SC + 4;   // chunks per stage; padded LDS row (16-byte aligned)
+    __shared__ __attribute__((aligned(16))) float cs[2][RT][16][SP];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int g = blockIdx.x, r16 = lane & 15, q = lane >> 4;
+    const int KB = a.KB;
+    const bf16_t* wg = a.W + (long)g * KB * 512;
+    const int fr = tid >> 4, fc = tid & 15;   // fold row / column (threads < RT * 16)
+    const bool folder = tid < RT * 16;
+    float tot = 0.f, part = 0.f;
+    int kbc = KB;
+    if (folder) kbc = exact_lin_kbc(a, min(fr, a.M - 1), g * 16 + fc);
+    int nb = 0;   // next K part boundary (chunk index)
+    const int nst = (KB + SC - 1) / SC;
+    // this lane's weight chunk of the current stage, loaded one stage ahead
+    u32x4 wv[4];
+    auto load = [&](int kb) {
+        if (kb < KB) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wv[j] = *(const u32x4*)(wg + ((long)kb * 64 + j * 16 + r16) * 8);
+        }
+    };
+    load(w * 4 + q);
+    for (int s = 0; s < nst; ++s) {
+        const int kb = s * SC + w * 4 + q;
+        if (kb < KB) {
+            float wf[32];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    wf[8 * j + 2 * i] = bf_lo(wv[j][i]);
+                    wf[8 * j + 2 * i + 1] = bf_hi(wv[j][i]);
+                }
+#pragma unroll
+            for (int r = 0; r < RT; ++r) {
+                const int m = min(r, a.M - 1);
+                cs[s & 1][r][r16][w * 4 + q] = exact_chunk_v((const u32x4*)(a.X + (long)m * a.ldx + kb * 32), wf);
+            }
+        }
+        load(kb + SC);
+        __syncthreads();
+        if (folder) {
+            const int kn = min(SC, KB - s * SC);
+            float c[SC];
+#pragma unroll
+            for (int i = 0; i < SC; i += 4) *(float4*)&c[i] = *(const float4*)&cs[s & 1][fr][fc][i];
+#pragma unroll
+            for (int i = 0; i < SC; ++i) {
+                const int kb2 = s * SC + i;
+                if (i < kn) {
+                    if (kb2 == nb) {   // a K part starts (multiples of kbc)
+                        if (kb2 > 0) tot = __fadd_rn(tot, part);
+                        part = __fadd_rn(0.f, c[i]);
+                        nb += kbc;
+                    } else {
+                        part = __fadd_rn(part, c[i]);
+                    }
+                }
+            }
+        }
+    }
+    if (w * 64 >= RT * 16) return;   // whole waves: GEGLU pairs lanes fc and fc ^ 8
+    exact_lin_store<EPI>(a, fr, g, fc, g * 16 + fc, KB > kbc ? __fadd_rn(tot, part) : part);
+}
+
+template <int RT>
+static int launch_exact_linear_g16(const ExactLinArgs& a, int epi, hipStream_t st) {
+    const dim3 grid((unsigned)a.NG), blk(1024);
+    switch (epi) {
+        case EPI_F32: hipLaunchKernelGGL((exact_linear_g16_kernel<RT, EPI_F32>), grid, blk, 0, st, a); break;
+        case EPI_BF16: hipLaunchKernelGGL((exact_linear_g16_kernel<RT, EPI_BF16>), grid, blk, 0, st, a); break;
+        case EPI_BIAS_BF16: hipLaunchKernelGGL((exact_linear_g16_kernel<RT, EPI_BIAS_BF16>), grid, blk, 0, st, a); break;
+        case EPI_BIAS_GELU: hipLaunchKernelGGL((exact_linear_g16_kernel<RT, EPI_BIAS_GELU>), grid, blk, 0, st, a); break;
+        case EPI_GEGLU: hipLaunchKernelGGL((exact_linear_g16_kernel<RT, EPI_GEGLU>), grid, blk, 0, st, a); break;
+        default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int exact_linear(const ExactLinArgs& a, int epi, hipStream_t st) {
     if (a.M <= 0) return 0;
     if (!a.X || !a.W || !a.Y || a.N <= 0 || a.KB <= 0 || a.NG % 4) return -1;
     if ((epi == EPI_BIAS_BF16 || epi == EPI_BIAS_GELU) && !a.bias) return -1;
     if (epi == EPI_GEGLU && a.N % 16) return -1;
     // rows per tile: the batch of a decode step (1..8 rows) without idle rows; 8 beyond
+    // decode rows whose 64-column tiles cannot fill the chip: 16-column workgroups
+    if (a.M <= 8 && a.NG / 4 < 256) switch (a.M) {
+        case 1: return launch_exact_linear_g16<1>(a, epi, st);
+        case 2: return launch_exact_linear_g16<2>(a, epi, st);
+        case 3: case 4: return launch_exact_linear_g16<4>(a, epi, st);
+        case 5: case 6: case 7: case 8: return launch_exact_linear_g16<8>(a, epi, st);
+        default: break;
+    }
     if (a.M <= 1) return launch_exact_linear<1>(a, epi, st);
     if (a.M <= 2) return launch_exact_linear<2>(a, epi, st);
     if (a.M <= 4) return launch_exact_linear<4>(a, epi, st);
@@ -181,9 +307,9 @@ int exact_linear(const ExactLinArgs& a, int epi, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------
-// SDPA. One workgroup per (query token, query head), 256 threads. Keys of one 512-key
-// block at a time: scores (thread per key), softmax pieces (wave 0), P.V (thread per
-// output dim).
+// SDPA. One workgroup per (query token, query head, 32-dim output slice), 256 threads.
+// Keys of one 512-key block at a time: scores (thread per key, repeated by every slice),
+// softmax pieces (wave 0), P.V (8 threads per output dim on chunk sums, one folds).
 constexpr int XA_BLOCK = 512;
 constexpr int XA_MAXD = 256;
 
@@ -207,11 +333,16 @@ __device__ __forceinline__ bool xa_need_pack(int Tq, int Tk, int Hq, int D, int 
     return gemm / pack_size >= 4.0;
 }
 
+constexpr int XA_DS = 32;               // output dims per workgroup (blockIdx.z slices)
+constexpr int XA_PARTS = 256 / XA_DS;   // threads per dim in P.V
+
 __global__ __launch_bounds__(256) void exact_attn_kernel(ExactAttnArgs a) {
     __shared__ float qs_[XA_MAXD];
     __shared__ float sp[XA_BLOCK + 16];   // scores, then bf16-rounded p of the block
+    __shared__ float csum[XA_BLOCK / 2 * XA_DS];   // P.V chunk sums [chunk][dim] (chunks >= 2 keys)
     __shared__ float bsum;
     const int qi = blockIdx.x, h = blockIdx.y;
+    const int d0 = blockIdx.z * XA_DS;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int D = a.D;
     const int row = a.q_row ? a.q_row[qi] : qi;
@@ -327,45 +458,71 @@ __global__ __launch_bounds__(256) void exact_attn_kernel(ExactAttnArgs a) {
             XA_DBG(1, bs + kk, sp[kk]);
         }
         __syncthreads();
-        // ---- P.V onto the rescaled output
-        if (tid < D) {
-            const bf16_t* vc = Vb + (long)bs * D + tid;
-            float acc = bs == 0 ? 0.f : __fmul_rn(dst, et);
-            if (gemv) {
-                for (int g0 = 0; g0 < blen; g0 += 8) {
+        // ---- P.V onto the rescaled output. This workgroup owns XA_DS output dims; each
+        // dim's keys are cut into the GEMM's chunks (gemv: groups of 8 keys; else E/O
+        // chunks of ch keys), XA_PARTS threads per dim compute chunk sums in parallel, then
+        // the dim's owner folds them in chunk order onto the rescaled output.
+        {
+            const int dl = tid % XA_DS, part = tid / XA_DS;
+            const int d = d0 + dl;
+            const int ch = gemv ? 8 : (pack ? xa_even_div_chunk(blen) : 32);
+            const int nch = (blen + ch - 1) / ch;
+            const bf16_t* vc = Vb + (long)bs * D + d;
+            for (int c = part; d < D && c < nch; c += XA_PARTS) {
+                const int c0 = c * ch, cn = min(ch, blen - c0);
+                float cs;
+                if (gemv) {   // pairs (odd key first), one chain per 8-key group
+                    float vv[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) vv[j] = j < cn ? bf2f(vc[(long)(c0 + j) * D]) : 0.f;
                     float tmp = 0.f;
-                    for (int j = g0; j < min(g0 + 8, blen); j += 2) {
-                        if (j + 1 < blen) tmp = fmaf(sp[j + 1], bf2f(vc[(long)(j + 1) * D]), tmp);
-                        tmp = fmaf(sp[j], bf2f(vc[(long)j * D]), tmp);
+#pragma unroll
+                    for (int j = 0; j < 8; j += 2) {
+                        if (j < cn) {
+                            if (j + 1 < cn) tmp = fmaf(sp[c0 + j + 1], vv[j + 1], tmp);
+                            tmp = fmaf(sp[c0 + j], vv[j], tmp);
+                        }
                     }
-                    acc = __fadd_rn(acc, tmp);
-                }
-            } else {
-                const int ch = pack ? xa_even_div_chunk(blen) : 32;
-                for (int c0 = 0; c0 < blen; c0 += ch) {
-                    const int cn = min(ch, blen - c0);
+                    cs = tmp;
+                } else {      // E/O chains of the chunk
                     float e = 0.f, o = 0.f;
-                    for (int j = 0; j < cn; j += 2) {
-                        e = fmaf(sp[c0 + j], bf2f(vc[(long)(c0 + j) * D]), e);
-                        if (j + 1 < cn) o = fmaf(sp[c0 + j + 1], bf2f(vc[(long)(c0 + j + 1) * D]), o);
+                    for (int j0 = 0; j0 < cn; j0 += 8) {
+                        float vv[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) vv[j] = j0 + j < cn ? bf2f(vc[(long)(c0 + j0 + j) * D]) : 0.f;
+#pragma unroll
+                        for (int j = 0; j < 8; j += 2) {
+                            if (j0 + j < cn) e = fmaf(sp[c0 + j0 + j], vv[j], e);
+                            if (j0 + j + 1 < cn) o = fmaf(sp[c0 + j0 + j + 1], vv[j + 1], o);
+                        }
                     }
-                    const float cs = __fadd_rn(e, o);
-                    acc = (bs == 0 && c0 == 0) ? cs : __fadd_rn(acc, cs);
+                    cs = __fadd_rn(e, o);
                 }
+                csum[c * XA_DS + dl] = cs;
             }
-            dst = acc;
+            __syncthreads();
+            if (part == 0 && d < D) {
+                float acc = bs == 0 ? 0.f : __fmul_rn(dst, et);
+                for (int c = 0; c < nch; ++c) {
+                    const float cs = csum[c * XA_DS + dl];
+                    acc = (!gemv && bs == 0 && c == 0) ? cs : __fadd_rn(acc, cs);
+                }
+                dst = acc;
+            }
         }
         m = mn;
         __syncthreads();
     }
-    if (tid < D) a.O[(long)qi * a.ldo + h * D + tid] = f2bf(__fmul_rn(dst, __fdiv_rn(1.0f, l)));
+    if (tid < XA_DS && d0 + tid < D)
+        a.O[(long)qi * a.ldo + h * D + d0 + tid] = f2bf(__fmul_rn(dst, __fdiv_rn(1.0f, l)));
 }
 
 int exact_attention(const ExactAttnArgs& a, hipStream_t st) {
     if (a.Mq <= 0) return 0;
     if (!a.Q || !a.K || !a.V || !a.kv_len || !a.O || a.D > XA_MAXD || a.D % 32 || a.Hq % a.Hkv || a.threads <= 0)
         return -1;
-    hipLaunchKernelGGL(exact_attn_kernel, dim3((unsigned)a.Mq, (unsigned)a.Hq), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(exact_attn_kernel, dim3((unsigned)a.Mq, (unsigned)a.Hq, (unsigned)((a.D + XA_DS - 1) / XA_DS)),
+                       dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

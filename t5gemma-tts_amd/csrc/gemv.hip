@@ -203,7 +203,10 @@ __global__ __launch_bounds__(NW * 64) void gemv_dec_kernel(DecGemmArgs a) {
 // double-buffered per unit: unit i + 1's fragments are in flight while unit i multiplies.
 // Per-row results are bitwise those of gemv_dec_kernel (same k-step order per wave, same
 // fixed-order wave reduction).
-template <int NW, int MT, int EPI, int SPU>
+// UMAX > 0: every unit's weight batch is requested before the first multiply (up to UMAX
+// units per block held in registers) instead of one unit ahead -- the block's whole weight
+// stream is in flight from the start.
+template <int NW, int MT, int EPI, int SPU, int UMAX = 0>
 __global__ __launch_bounds__(NW * 64) void gemv_rx_kernel(DecGemmArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     f32x4* red = (f32x4*)smem;   // [umax][MT][NW][64]
@@ -226,7 +229,13 @@ __global__ __launch_bounds__(NW * 64) void gemv_rx_kernel(DecGemmArgs a) {
         }
     };
     bf16x8_s wa[SPU], wb[SPU];
-    wbatch(0, wa);
+    bf16x8_s wall[UMAX > 0 ? UMAX : 1][SPU];
+    if constexpr (UMAX > 0) {
+#pragma unroll
+        for (int i = 0; i < UMAX; ++i) wbatch(i, wall[i]);
+    } else {
+        wbatch(0, wa);
+    }
     // this wave's X fragments (rows >= M and k-steps past the slice are zero)
     bf16x8_s xf[MT][SPU];
     const bf16x8_s z8 = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -250,11 +259,16 @@ __global__ __launch_bounds__(NW * 64) void gemv_rx_kernel(DecGemmArgs a) {
             if (i < nu) red[((i * MT + t) * NW + wave) * 64 + lane] = acc;
         }
     };
-    for (int i = 0; i < nu; i += 2) {
-        wbatch(i + 1, wb);
-        mul(i, wa);
-        wbatch(i + 2, wa);
-        mul(i + 1, wb);
+    if constexpr (UMAX > 0) {
+#pragma unroll
+        for (int i = 0; i < UMAX; ++i) mul(i, wall[i]);   // units past nu: zero batches, results dropped
+    } else {
+        for (int i = 0; i < nu; i += 2) {
+            wbatch(i + 1, wb);
+            mul(i, wa);
+            wbatch(i + 2, wa);
+            mul(i + 1, wb);
+        }
     }
     __syncthreads();
 
@@ -372,16 +386,24 @@ template <int NW, int MT, int EPI, int PER>
 static int launch_rx_nw(const DecGemmArgs& a, hipStream_t st) {
     static_assert(PER % NW == 0, "whole k-step batches per wave");
     constexpr int SPU = PER / NW;
-    auto* fn = gemv_rx_kernel<NW, MT, EPI, SPU>;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GD_LDS_MAX);
-        attr = true;
-    }
     const int cap = a.max_grid > 0 ? a.max_grid : cu_count();
     const int grid = a.splits > 1 ? std::max(1, std::min(a.NG, cap / a.splits)) : gd_grid(a, 1);
-    const size_t shm = (size_t)((a.NG + grid - 1) / grid) * MT * NW * 64 * 16;
+    const int umax = (a.NG + grid - 1) / grid;
+    const size_t shm = (size_t)umax * MT * NW * 64 * 16;
     if (shm > GD_LDS_MAX) return -1;
+    // un = -1 (tuning): the whole per-block weight stream requested up front, for blocks of
+    // <= 5 units whose batches fit the register budget (SPU * 5 fragments per wave)
+    bool all = false;
+    auto* fn = gemv_rx_kernel<NW, MT, EPI, SPU, 0>;
+    if constexpr (MT == 1 && SPU <= 6) {
+        all = a.un == -1 && umax <= 5;
+        if (all) fn = gemv_rx_kernel<NW, MT, EPI, SPU, 5>;
+    }
+    static bool attr[2] = {false, false};
+    if (!attr[all]) {
+        (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GD_LDS_MAX);
+        attr[all] = true;
+    }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid, (unsigned)a.splits), dim3(NW * 64), shm, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -434,30 +434,33 @@ class T5GemmaTTSEngine:
         cur = ctx["cur"]
         _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
         flags = (C.c_int32 * B)()
+        nxt = (_lib.SamplerState * B)()
         while not all(cur[b].done for b in range(B)):
             if rec is not None:
                 rec.append(self.logits(B).clone())
-            pre = (_lib.SamplerState * B)()
-            C.memmove(pre, cur, C.sizeof(cur))
             _lib.check(L.t5g_sample_only(self.h, B, C.c_void_p(self._logits_ptr), self.logits_ld, stream), "sample")
-            _lib.check(L.t5g_read_flags(self.h, flags, B, stream), "read_flags")
+            _lib.check(L.t5g_read_step(self.h, nxt, flags, B, stream), "read_step")
+            fixed = False
             for b in range(B):
-                if pre[b].done or not (flags[b] & 1):
+                if cur[b].done or not (flags[b] & 1):
                     continue
                 lg = self.logits(B)[b].contiguous().cpu()
-                nz = noise[b, pre[b].cur_num_gen].contiguous().cpu()
+                nz = noise[b, cur[b].cur_num_gen].contiguous().cpu()
                 out_st = _lib.SamplerState()
                 tok = C.c_int32()
                 _lib.check(L.t5g_host_sample(
-                    _ptr(lg), self.V, C.byref(rows[b]), tk, sl, C.byref(pre[b]), _ptr(nz), eos,
+                    _ptr(lg), self.V, C.byref(rows[b]), tk, sl, C.byref(cur[b]), _ptr(nz), eos,
                     self._cfg.eos_guard, self._cfg.budget_extra, self._cfg.text_guard,
                     self._cfg.progress_scale, self.max_gen, self.max_audio, C.byref(out_st), C.byref(tok)),
                     "host_sample")
-                out_st.ambiguous_steps = pre[b].ambiguous_steps + 1
-                _lib.check(L.t5g_write_state(self.h, C.byref(out_st), b, pre[b].cur_num_gen, tok.value,
+                out_st.ambiguous_steps = cur[b].ambiguous_steps + 1
+                _lib.check(L.t5g_write_state(self.h, C.byref(out_st), b, cur[b].cur_num_gen, tok.value,
                                              stream), "write_state")
                 ctx["ambiguous_fixed"] += 1
-            _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
+                fixed = True
+            if fixed:
+                _lib.check(L.t5g_read_state(self.h, nxt, B, stream), "read_state")
+            C.memmove(cur, nxt, C.sizeof(cur))
             ctx["steps"] += 1
             if not all(cur[b].done for b in range(B)):
                 _lib.check(L.t5g_step_only(self.h, stream), "step")

@@ -55,6 +55,8 @@ def _hdr(shape, g):
     (1, 2048, 2304, 0, 0), (8, 4096, 2304, 0, 4), (3, 2304, 9216, 4608, 0), (60, 2304, 9216, 3072, 4),
     (152, 2304, 9216, 2304, 0), (8, 2304, 2048, 0, 0), (5, 2304, 2304, 0, 1), (4, 2304, 2304, 0, 2),
     (8, 18432, 2304, 0, 3), (2, 65541, 2304, 0, 1), (17, 300, 128, 0, 0), (9, 256, 128, 0, 3),
+    # split-K launches (<= 8 rows, < 256 row tiles): K parts, bias, GEGLU, a ragged last tile
+    (8, 2304, 9216, 2304, 3), (7, 1024, 9216, 3072, 1), (1, 1028, 2304, 0, 1), (6, 2304, 9216, 4608, 4),
 ])
 def test_exact_linear_bitwise_vs_cpu_order(M, N, K, kb, epi):
     """t5g_exact_linear == oracle.cpu_order.linear (the reference host's F.linear order)."""
