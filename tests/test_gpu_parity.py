@@ -525,23 +525,27 @@ def test_sampler_kernel_vs_reference_golden():
     assert ok == len(meta["cases"])
 
 
-def test_generate_without_target_length():
+@pytest.mark.parametrize("max_audio,max_gen", [(96, 40), (40, 96)])
+def test_generate_without_target_length(max_audio, max_gen):
     """tgt_y_lens=None (the reference accepts it, modeling_t5gemma_voice.py:624-660: no time
     budget, decoder progress over a 2 s lookahead) on a default-sized engine: generation
     stops at EOS or at the engine's capacity, and every step the reference sampler would
-    also have taken is teacher-forced exact (this path used to raise)."""
+    also have taken is teacher-forced exact (this path used to raise). The second
+    case makes the cache capacity (max_audio - prompt) the cap, so the forced-EOS step samples
+    at cur_num_gen == budget: the parity noise buffer holds budget + 1 steps."""
     _need_gpu()
     from t5gemma_tts_amd.config import named_config
     from t5gemma_tts_amd.engine import Utterance
     from t5gemma_tts_amd.weights import synthetic_weights
     cfg = named_config("tiny")
     sd = synthetic_weights(cfg, 7)
-    eng = _engine(cfg, sd, max_batch=2, max_text=32, max_audio=96, max_gen=40)
+    eng = _engine(cfg, sd, max_batch=2, max_text=32, max_audio=max_audio, max_gen=max_gen)
+    cap = min(max_gen, max_audio - 3)
     c = {"top_k": 30, "top_p": 0.9, "min_p": 0.0, "temperature": 0.8, "stop_repetition": 3, "silence_tokens": []}
     u = Utterance(x=[5, 17, 301, 44, 9], y=[3, 60, cfg.y_sep_token], tgt_y_len=None)
     out = eng.generate([u], _params(c), seeds=[11], parity=True, record_logits=True)
     g = out["gen"][0].tolist()
-    assert 1 <= len(g) <= 40
-    if g[-1] == cfg.eog_inference and len(g) == 40:   # capacity stop: the last EOS is the engine's
+    assert 1 <= len(g) <= cap + 1
+    if g[-1] == cfg.eog_inference and len(g) >= cap:   # capacity stop: the last EOS is the engine's
         out = {"gen": [out["gen"][0][:-1]], "logits": out["logits"][:-1]}
     teacher_forced_check(cfg, sd, u, _oparams(c), 11, out, rtol=0.02)

@@ -12,7 +12,7 @@ import os
 import sys
 
 OPS = {
-    "gate_up": {"kernels": ["gemv_rx_kernel<12, 1, 3, 6>"],
+    "gate_up": {"kernels": ["gemv_rx_kernel<12, 1, 3, 6"],
                 "algorithmic": 2 * 9216 * 2304 * 2 + 8 * 2304 * 2 + 8 * 9216 * 2,
                 "what": "decode gate/up GEGLU GEMV, M=8, N=18432, K=2304 (tools/pmc_gateup.py: 26 weight sets "
                         "rotated, 2.2 GB > 256 MiB Infinity Cache)"},
