@@ -146,6 +146,8 @@ def main():
     ap.add_argument("--natural-eos", action="store_true",
                     help="accept EOS when sampled (SURVEY 8(d)'s second run) instead of throughput mode")
     ap.add_argument("--e2e", action="store_true", help="C5: generate + XCodec2 decode in the timed region")
+    ap.add_argument("--no-fused", action="store_true",
+                    help="decode MLP half as three launches instead of the persistent fused launch (A/B)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo (CPU collectives; lets N ranks share one GPU "
                          "to rehearse the sharded path)")
@@ -194,6 +196,8 @@ def main():
     n_tok_row = DUR_FRAMES + int(cfg.extra_budget) + 1
     eng = T5GemmaTTSEngine(cfg, sd, device=str(dev), max_batch=B, max_text=64,
                            max_audio=wl_tp + 1 + n_tok_row + 8, max_gen=n_tok_row + 4)
+    if args.no_fused:
+        eng.set_fused(False)
     codec = None
     if args.e2e:
         from t5gemma_tts_amd.codec import XCodec2Decoder, codec_44k, synthetic_codec_weights
@@ -270,30 +274,38 @@ def main():
         tokens_all, frames_all, dt_max = float(tokens), float(audio_frames[0]), dt
     value = tokens_all / dt_max
 
-    # ---- roofline of the dominant kernel: decode GeGLU gate/up GEMV (largest weight stream)
+    # ---- roofline of the dominant kernel: the fused decode-MLP launch (norm + gate/up +
+    # down, 127 MB of weights per layer), or the gate/up GEMV when the MLP runs unfused
     roof = None
     if rank == 0 and not args.e2e and not args.parity:
         import ctypes as C
         from t5gemma_tts_amd import _lib
         L = _lib.lib()
         d, f = cfg.backbone.hidden_size, cfg.backbone.intermediate_size
-        # rotate over every decoder layer's gate/up weights (2.2 GB >> 256 MiB Infinity
-        # Cache) so each launch streams its weights from HBM, as inside a decode step
-        X = torch.randn(B, d, device=dev).to(torch.bfloat16)
-        Y = torch.empty(B, f, dtype=torch.bfloat16, device=dev)
         st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        us_gu = _lib.time_gate_up(X.data_ptr(), d, B, [lw.gate_up for lw in eng._dec], 2 * f, d, Y.data_ptr(),
-                                  208, st)
-        alg_bytes = 2 * f * d * 2 + B * d * 2 + B * f * 2
-        achieved = alg_bytes / (us_gu * 1e-6) / 1e9
+        if not args.no_fused:
+            us = C.c_float()
+            # 208 launches rotated over the 26 layers' weights (3.3 GB >> 256 MiB Infinity
+            # Cache): every launch streams from HBM, as inside a decode step
+            _lib.check(L.t5g_time_decode_mlp(eng.h, B, 208, st, C.byref(us)), "time_decode_mlp")
+            us_k, alg_bytes, kname = us.value, _lib.fused_mlp_bytes(B, d, f), _lib.FUSED_MLP_KERNEL
+            pmc = os.path.join(REPO, "profiles", "r03_pmc_fused_mlp.json")
+        else:
+            # rotate over every decoder layer's gate/up weights (2.2 GB >> 256 MiB Infinity
+            # Cache) so each launch streams its weights from HBM, as inside a decode step
+            X = torch.randn(B, d, device=dev).to(torch.bfloat16)
+            Y = torch.empty(B, f, dtype=torch.bfloat16, device=dev)
+            us_k = _lib.time_gate_up(X.data_ptr(), d, B, [lw.gate_up for lw in eng._dec], 2 * f, d, Y.data_ptr(),
+                                     208, st)
+            alg_bytes, kname = 2 * f * d * 2 + B * d * 2 + B * f * 2, _lib.GATE_UP_KERNEL
+            pmc = os.path.join(REPO, "profiles", "r02_pmc_gate_up.json")
+        achieved = alg_bytes / (us_k * 1e-6) / 1e9
         traffic = None
-        pmc = os.path.join(REPO, "profiles", "r02_pmc_gate_up.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and B == 8:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_call")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
-                "frac": round(achieved / 8000.0, 4), "traffic": traffic,
-                "kernel": _lib.GATE_UP_KERNEL,
-                "avg_us": round(us_gu, 2)}
+                "frac": round(achieved / 8000.0, 4), "traffic": traffic, "kernel": kname,
+                "algorithmic_bytes": int(alg_bytes), "avg_us": round(us_k, 2)}
         step_us = C.c_float()
         _lib.check(L.t5g_time_decode_step(eng.h, 20, st, C.byref(step_us)), "time_step")
         roof["decode_step_us"] = round(step_us.value, 1)

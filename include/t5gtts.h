@@ -280,6 +280,15 @@ int t5g_attention_decode(const t5g_attn_decode_args* args, void* stream);
  * the single-block kernel when a row's top-k / survivor set exceeds it; 1 the single-block
  * kernel only. Both pick the same tokens (tests/test_gpu_sampler.py). */
 int t5g_engine_set_sampler_path(t5g_engine* e, int32_t single_block);
+/* Decode MLP half (cross-attention residual norm -> gate/up GeGLU -> down) as one persistent
+ * launch with in-launch hand-offs (fused.hip) instead of three launches; bitwise equal.
+ * Default on (fast path only: parity mode runs the exact-order kernels). Replaces the
+ * reference's T5GemmaMLP call + residual (hf_export/modeling_t5gemma_voice.py:309-323,
+ * [tf] modeling_t5gemma.py:81-97); no reference-side equivalent switch. */
+int t5g_engine_set_fused(t5g_engine* e, int32_t enable);
+/* Average device time (us, hipEvents on `stream`) of the fused decode-MLP launch at B rows,
+ * rotating over the decoder layers (bench.py roofline leg; no reference equivalent). */
+int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us);
 
 /* --- parity mode (csrc/exact.hip) ------------------------------------------------
  * Switch an engine to the exact-order kernels: every Linear, RMSNorm mean, q.k / P.V of

@@ -121,6 +121,8 @@ SIGNATURES = {
     "t5g_attention_decode": (C.c_int, [C.POINTER(AttnDecodeArgs), _P]),
     "t5g_engine_set_exact": (C.c_int, [_P, _I, _P, _I]),
     "t5g_engine_set_sampler_path": (C.c_int, [_P, _I]),
+    "t5g_engine_set_fused": (C.c_int, [_P, _I]),
+    "t5g_time_decode_mlp": (C.c_int, [_P, _I, _I, _P, C.POINTER(_F)]),
     "t5g_exact_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
     "t5g_exact_attention": (C.c_int, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
 }
@@ -173,6 +175,15 @@ def lib():
 # (gemv_dec with layout_rx: register-resident X, EPI_GEGLU, 8 waves sharing each unit's K
 # stream, 9 fragments per wave per unit, one block per CU).
 GATE_UP_KERNEL = "gemv_rx_kernel<12, 1, 3 (GEGLU), 6> (decode gate/up, M=8, 84.9 MB weights)"
+FUSED_MLP_KERNEL = ("fused_mlp_kernel<1> (decode MLP half in one launch: cross-attention residual norm -> "
+                    "gate/up GeGLU -> down, 127.4 MB of weights)")
+
+
+def fused_mlp_bytes(M: int, d: int = 2304, f: int = 9216) -> int:
+    """Algorithmic HBM bytes of one fused decode-MLP launch (csrc/fused.hip): gate/up and down
+    weights, the 4 cross-o slabs, h and the two norm weights in; h and the 8 down slabs out.
+    xn and act are in-launch hand-offs (written and read once each, not counted)."""
+    return 2 * f * d * 2 + d * f * 2 + 4 * M * d * 4 + M * d * 2 + 2 * d * 2 + M * d * 2 + 8 * M * d * 4
 
 
 def time_gate_up(X_ptr: int, ldx: int, M: int, W_ptrs, N: int, K: int, Y_ptr: int, iters: int, stream) -> float:

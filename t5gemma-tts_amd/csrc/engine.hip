@@ -75,6 +75,10 @@ struct t5g_engine {
     unsigned* fs_ticket;
     int* fs_slow;
     bool fast_sampler = true;   // false: single-block sampler only (t5g_engine_set_sampler_path)
+    // decode MLP half as one persistent launch (fused.hip; t5g_engine_set_fused)
+    bool fused_mlp = true;
+    float* part2 = nullptr;     // the fused block's in-launch slabs: cross-q [2][B][q_dim] | cross-o [4][B][d]
+    unsigned* fsync = nullptr;  // timeout line + one counter set per decoder layer (zeroed at creation / after a timeout)
     // decode split-K factors (measured on MI355X): qkv 2, o / cross-q /
     // cross-o 4, down 8 k-slices; gate/up on the one-block-per-CU GEMV
     static constexpr int s_qkv = 2, s_o = 4, s_down = 8;
@@ -226,6 +230,8 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->fs_ami, (int64_t)B * FS_NB);
     rc |= alloc(e, &e->fs_ticket, B);
     rc |= alloc(e, &e->fs_slow, B);
+    rc |= alloc(e, &e->part2, (int64_t)2 * B * e->q_dim + (int64_t)4 * B * d);
+    rc |= alloc(e, &e->fsync, (int64_t)FM_LINE + (int64_t)FM_SET_WORDS * c.n_dec_layers);
     if (rc) {
         t5g_engine_destroy(e);
         return T5G_ENOMEM;
@@ -723,6 +729,65 @@ static int decode_attention(t5g_engine* e, int M, const bf16_t* K, const bf16_t*
     return attention_decode(a, st);
 }
 
+// the decode MLP half of decoder layer l as one persistent launch (fused.hip): cross-o
+// slabs in e->part -> h / xn -> act -> down slabs in e->part; layer l's counter set
+static FusedMlpArgs fused_args(t5g_engine* e, int M, int l) {
+    const t5g_config& c = e->c;
+    const t5g_layer_weights& L = e->dec[l];
+    FusedMlpArgs fa;
+    memset(&fa, 0, sizeof(fa));
+    fa.M = M;
+    fa.d = c.hidden;
+    fa.f = c.intermediate;
+    fa.part_in = e->part;
+    fa.post_w = (const bf16_t*)L.norms[3];
+    fa.pre_w = (const bf16_t*)L.norms[4];
+    fa.eps = c.rms_eps;
+    fa.h = e->dh;
+    fa.xn = e->dxn;
+    fa.Wgu = (const bf16_t*)L.gate_up;
+    fa.NGgu = ng_pad(2 * c.intermediate);
+    fa.act = e->dact;
+    fa.Wd = (const bf16_t*)L.down;
+    fa.NGd = ng_pad(c.hidden);
+    fa.part_out = e->part;
+    fa.timeout = e->fsync;
+    fa.sync = e->fsync + FM_LINE + (size_t)FM_SET_WORDS * l;
+    fa.sync_next = e->fsync + FM_LINE + (size_t)FM_SET_WORDS * ((l + 1) % c.n_dec_layers);
+    return fa;
+}
+
+// the same launch with the cross-attention chain in front (fused.hip fused_block_kernel):
+// o-proj slabs in e->part -> ... -> down slabs in e->part
+static FusedMlpArgs fused_block_args(t5g_engine* e, int M, int l) {
+    const t5g_config& c = e->c;
+    const t5g_layer_weights& L = e->dec[l];
+    FusedMlpArgs fa = fused_args(e, M, l);
+    fa.xattn = 1;
+    fa.o_slabs = e->part;
+    fa.post1_w = (const bf16_t*)L.norms[1];
+    fa.pre1_w = (const bf16_t*)L.norms[2];
+    fa.xn1 = e->dhh;
+    fa.Wq = (const bf16_t*)L.cross_q;
+    fa.NGq = ng_pad(e->q_dim);
+    fa.qslab = e->part2;
+    fa.ck = e->ck[l];
+    fa.cv = e->cv[l];
+    fa.kv_cap = c.max_text;
+    fa.enc_len = e->enc_len;
+    fa.rope_tab = e->rope_tab;
+    fa.q_dim = e->q_dim;
+    fa.Hq = c.n_heads;
+    fa.Hkv = c.n_kv_heads;
+    fa.D = c.head_dim;
+    fa.scale = c.attn_scale;
+    fa.att = e->datt;
+    fa.Wo = (const bf16_t*)L.cross_o;
+    fa.NGo = ng_pad(c.hidden);
+    fa.oslab = e->part2 + (size_t)2 * M * e->q_dim;
+    return fa;
+}
+
 static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row, const int* tok_t, const float* pos,
                         bool decode, hipStream_t st) {
     const t5g_config& c = e->c;
@@ -832,11 +897,36 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             RC(attn_packed(e, M, q, tok_row, tok_t, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1, win, att, st));
         }
         RC(out_proj(att, L.o));
+        const bool last = l == c.n_dec_layers - 1;
+        // the rest of the layer (cross attention + MLP half) as one persistent launch
+        // (fused.hip fused_block_kernel; bitwise equal to the launches below)
+        if (decode && e->fused_mlp && !eager && M <= 16 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 &&
+            e->q_dim == 2048 && c.n_dec_layers >= 2) {
+            const int rc = fused_mlp(fused_block_args(e, M, l), st);
+            if (rc == 0) {
+                RC(resid(s_down, L.norms[5], last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]));
+                continue;
+            }
+            if (rc != -1) RC(rc);   // -1: a shape / device the launch is not built for
+        }
         RC(resid(s_o, L.norms[1], L.norms[2]));
         // --- PM cross attention (q rotated by the decoder progress, :149-165)
         if (decode && !eager) {
-            RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, s_o, nullptr, e->part, e->q_dim, EPI_F32, st));
-            RC(decode_attention(e, M, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, 0, false, pos, tab, s_o,
+            // cross-q: at the 2b-2b width the register-X GEMV over 2 k-slices of 36 k-steps,
+            // 12 waves (the fused block's Q stage), so a row's sums never depend on the batch
+            int s_q = s_o, rcq = -1;
+            if (M <= 32 && d == 2304 && e->q_dim == 2048) {
+                DecGemmArgs g = dec_args(M, L.cross_q, e->q_dim, d, e->part, e->q_dim, 12);
+                g.X = xn;
+                g.ldx = d;
+                g.splits = 2;
+                g.layout_rx = 1;
+                rcq = gemv_dec(g, EPI_F32, st);
+                if (rcq == 0) s_q = 2;
+                else if (rcq != -1) RC(rcq);
+            }
+            if (rcq != 0) RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, s_o, nullptr, e->part, e->q_dim, EPI_F32, st));
+            RC(decode_attention(e, M, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, 0, false, pos, tab, s_q,
                                 e->q_dim, st));
         } else {
             RC(gemm(xn, d, M, L.cross_q, e->q_dim, d, 1, nullptr, q, e->q_dim, EPI_BF16, st, !decode));
@@ -849,6 +939,17 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             RC(attn_packed(e, M, q, tok_row, tok_t, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, st));
         }
         RC(out_proj(att, L.cross_o));
+        // --- norm + GeGLU MLP: at the 2b-2b width, decode rows <= 32, one persistent launch
+        // (fused.hip; bitwise equal to the three launches below)
+        if (decode && e->fused_mlp && !eager && M <= 32 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 &&
+            c.n_dec_layers >= 2) {
+            const int rc = fused_mlp(fused_args(e, M, l), st);
+            if (rc == 0) {
+                RC(resid(s_down, L.norms[5], last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]));
+                continue;
+            }
+            if (rc != -1) RC(rc);   // -1: a shape / device the launch is not built for
+        }
         RC(resid(s_o, L.norms[3], L.norms[4]));
         // --- GeGLU MLP (decode: the one-block-per-CU GEMV; register-resident X at the
         // 2b-2b width, up to 32 rows)
@@ -881,7 +982,6 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             RC(gemm(act, f, M, L.down, d, f, s_down, nullptr, s_down > 1 ? (void*)e->part : (void*)tmp, d,
                     s_down > 1 ? EPI_F32 : EPI_BF16, st, !decode));
         }
-        const bool last = l == c.n_dec_layers - 1;
         RC(resid(s_down, L.norms[5], last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]));
     }
     return T5G_OK;
@@ -1084,7 +1184,26 @@ extern "C" int t5g_read_tokens(t5g_engine* e, int32_t* out, int32_t B, void* str
     if (!e || !out || B <= 0 || B > e->c.max_batch) return T5G_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipMemcpyAsync(out, e->out_tokens, (size_t)B * e->c.max_gen * sizeof(int), hipMemcpyDeviceToHost, st));
+    unsigned tmo = 0;
+    HIPCHK(hipMemcpyAsync(&tmo, e->fsync, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (tmo) {
+        // an in-launch hand-off of the fused MLP gave up waiting (a workgroup was not
+        // resident): the outputs are garbage; clear the counters for the next call
+        fprintf(stderr, "[t5gtts] fused MLP hand-off timed out (code %u)\n", tmo);
+        hipMemsetAsync(e->fsync, 0, (FM_LINE + (size_t)FM_SET_WORDS * e->c.n_dec_layers) * sizeof(unsigned), st);
+        hipStreamSynchronize(st);
+        return T5G_EHIP;
+    }
+    return T5G_OK;
+}
+
+extern "C" int t5g_engine_set_fused(t5g_engine* e, int32_t enable) {
+    if (!e) return T5G_EINVAL;
+    if (e->fused_mlp != (enable != 0)) {
+        e->fused_mlp = enable != 0;
+        drop_graphs(e);   // captured launches follow the flag
+    }
     return T5G_OK;
 }
 
@@ -1231,6 +1350,34 @@ extern "C" int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, 
     *avg_us = ms * 1000.f / iters;
     hipEventDestroy(e0);
     hipEventDestroy(e1);
+    return T5G_OK;
+}
+
+// hipEvent-timed fused decode-MLP launches (bench.py roofline leg): layers rotated, so every
+// launch streams its weights from HBM (2.2 GB of gate/up + down > the 256 MiB Infinity Cache)
+extern "C" int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us) {
+    if (!e || iters <= 0 || !avg_us || B <= 0 || B > e->c.max_batch || e->c.n_dec_layers < 2) return T5G_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const int L = e->c.n_dec_layers;
+    // whole rotations over the layers, as a decode step runs them: layer l's launch finds
+    // its counter set zeroed by layer l - 1's (the last launch before this call was a step's
+    // last layer, which zeroed layer 0's set); one untimed rotation first
+    const int n = (iters + L - 1) / L * L;
+    int rc = T5G_OK;
+    for (int l = 0; l < L && !rc; ++l) rc = fused_mlp(fused_args(e, B, l), st);
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, st));
+    for (int i = 0; i < n && !rc; ++i) rc = fused_mlp(fused_args(e, B, i % L), st);
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    if (rc) return rc == -1 ? T5G_EUNSUPPORTED : T5G_EHIP;
+    *avg_us = ms * 1000.f / (float)n;
     return T5G_OK;
 }
 

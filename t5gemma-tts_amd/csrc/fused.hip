@@ -1,0 +1,826 @@
+// Decode MLP half of a decoder layer as ONE persistent launch (one workgroup per CU):
+//
+//   stage N (M workgroups):  h = h + RMSNorm_post(sum of the cross-o slabs); xn = RMSNorm_pre(h)
+//   stage G (every workgroup): act = GeGLU(xn . Wgate/up^T)            (gemv_rx_kernel's units)
+//   stage D (every workgroup): down slabs[s] = act[:, slice s] . Wdown^T (8 k-slices)
+//
+// replacing resid_norm_kernel<4,2> + gemv_rx_kernel<12,..,GEGLU> + gemv_rx_kernel<12,..,F32>
+// (PMDecoderLayer cross-attention residual + T5GemmaMLP, [tf] modeling_t5gemma.py:81-97,
+// hf_export/modeling_t5gemma_voice.py:256-323). What the launch buys is overlap: every
+// workgroup requests its whole gate/up weight stream BEFORE the normed rows exist, and its
+// down weights before the act slice it multiplies is complete, so the two weight streams
+// run back to back while the norm and the hand-offs happen underneath them. Two launch
+// boundaries, the norm's launch and the fill / drain of two GEMV launches go away.
+//
+// Hand-offs (gfx950 recipe, cdna_hip_programming.md Guideline 16 R1): the handed-off
+// bytes (xn rows, act) are stored write-through (sc1) by every storing wave, each storing
+// wave drains (vmcnt(0)), the workgroup meets at a barrier, ONE lane adds to a relaxed
+// agent-scope counter (one per 128-byte line); the consumer polls that counter relaxed from
+// ONE wave (which has no weight loads queued ahead of the poll), the workgroup meets at a
+// barrier, and every load of the handed-off bytes is an sc1 load. Counter sets start at
+// zero (zeroed at engine creation and by the host after a timeout); each decoder layer has
+// its own set, and each launch zeroes the NEXT layer's set as it starts (that set's last
+// user has completed), so no arrival count is needed at the end. Every wait is bounded:
+// a wait that gives up stores a
+// timeout code that makes every later wait give up at once (outputs are then garbage and
+// the host raises, t5g_read_tokens); no wave can spin forever.
+//
+// Numerics: every stage is the exact arithmetic of the kernels it replaces (the same
+// per-wave k-step chains, the same fixed-order wave reductions, the same norm reductions),
+// so the fused launch is bitwise equal to the three launches (tests/test_gpu_fused.py).
+#include "common.h"
+#include "t5g_kernels.h"
+
+namespace t5g {
+
+T5G_TS_UNIT(fused)
+
+constexpr int FM_NW = 12;         // waves per workgroup (the gate/up and down kernels' count)
+constexpr int FM_NS = 4;          // cross-o split-K slabs read by the norm stage
+constexpr int FM_DS = 8;          // down-projection k-slices
+constexpr int FM_NORM_UNITS = 3;  // gate/up units of a norm workgroup (tools/diag_fused.py)
+constexpr unsigned FM_SPIN_MAX = 1u << 18;   // ~0.3-0.5 s of polling before a wait gives up
+
+// lines of a counter set (FusedMlpArgs::sync), one word per 128-byte line
+constexpr int L_N1 = 0, L_Q0 = 1, L_A0 = 9, L_O0 = 17, L_N2 = 25, L_SL0 = 26;
+static_assert(L_SL0 + FM_DS == FM_SET_LINES, "counter set layout");
+__device__ __forceinline__ unsigned* cline(unsigned* set, int line) { return set + line * FM_LINE; }
+constexpr int FS_NORM = L_N2 * FM_LINE;
+__device__ __forceinline__ int fs_slice(int s) { return (L_SL0 + s) * FM_LINE; }
+
+__device__ __forceinline__ unsigned ld_rlx(unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one wave polls `w` until it reaches `target`; false if this or an earlier wait of the
+// launch (or of an earlier launch of the call) gave up
+__device__ __forceinline__ bool fm_wait(unsigned* w, unsigned target, unsigned* tmo, unsigned code) {
+    for (unsigned spins = 0;; ++spins) {
+        if (ld_rlx(w) >= target) return true;
+        if ((spins & 63) == 0 && ld_rlx(tmo) != 0) return false;
+        if (spins > FM_SPIN_MAX) {
+            __hip_atomic_store(tmo, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// workgroup rendezvous with no memory semantics for the compiler to add waits for (the
+// weight loads in flight must stay in flight across it); the "memory" clobber keeps the
+// handed-off loads below it
+__device__ __forceinline__ void wg_barrier() { asm volatile("s_barrier" ::: "memory"); }
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t p = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr int AUX_NT = 2, AUX_SC1 = 16;
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void unpack8f(u32x4 w, float (&v)[8]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[2 * j] = bf_lo(w[j]);
+        v[2 * j + 1] = bf_hi(w[j]);
+    }
+}
+__device__ __forceinline__ u32x4 pack8f(const float (&v)[8]) {
+    u32x4 w;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = pack2(v[2 * j], v[2 * j + 1]);
+    return w;
+}
+// norm.hip's block_sum_once over this launch's 12 waves: the waves past the 288 active
+// threads add +0.0f after the 5 real wave sums, which leaves the (non-negative) total
+// bitwise unchanged -- the same value as the 288-thread resid_norm launch
+__device__ __forceinline__ float fm_block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    float s = 0.f;
+    for (int i = 0; i < FM_NW; ++i) s += red[i];
+    return s;
+}
+__device__ __forceinline__ void fm_rms8(float (&v)[8], bool active, int d, u32x4 w8, float eps, float* red) {
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+    const float tot = fm_block_sum(active ? ss : 0.f, red);
+    const float r = 1.0f / sqrtf(tot / (float)d + eps);
+    if (!active) return;
+    float wf[8];
+    unpack8f(w8, wf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = rbf((v[j] * r) * (1.0f + wf[j]));
+}
+
+// Stage N for row m (resid_norm_kernel<4, 2> with post, resid and pre): xn published sc1.
+__device__ __forceinline__ void fm_norm_row(const FusedMlpArgs& a, int m, float* red) {
+    const int d = a.d;
+    const int c = threadIdx.x;
+    const bool active = 8 * c < d;
+    const int cc = active ? c : d / 8 - 1;
+    const u32x4 w_post = *(const u32x4*)(a.post_w + 8 * cc);
+    const u32x4 w_pre = *(const u32x4*)(a.pre_w + 8 * cc);
+    const u32x4 rw = *(const u32x4*)(a.h + (long)m * d + 8 * cc);
+    f32x4 p[FM_NS][2];
+#pragma unroll
+    for (int s = 0; s < FM_NS; ++s) {
+        const f32x4* ps = (const f32x4*)(a.part_in + ((long)s * a.M + m) * d + 8 * cc);
+        p[s][0] = ps[0];
+        p[s][1] = ps[1];
+    }
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < FM_NS; ++s) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] += p[s][0][j];
+            v[4 + j] += p[s][1][j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = rbf(v[j]);
+    fm_rms8(v, active, d, w_post, a.eps, red);
+    float r8[8];
+    unpack8f(rw, r8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = rbf(r8[j] + v[j]);
+    if (active) *(u32x4*)(a.h + (long)m * d + 8 * c) = pack8f(v);   // next launch reads it
+    fm_rms8(v, active, d, w_pre, a.eps, red + 32);
+    if (active) {
+        const __amdgpu_buffer_rsrc_t xr = raw_rsrc(a.xn, (uint32_t)(a.M * d * 2));
+        __builtin_amdgcn_raw_buffer_store_b128(pack8f(v), xr, (m * d + 8 * c) * 2, 0, AUX_SC1);
+    }
+}
+
+// One register-resident-X GEMV stage (gemv_rx_kernel's arithmetic): the workgroup's nu
+// units g = g0 + i * gs of W (KB k-steps of which [kb_lo, kb_lo + KBs) are summed), X rows from
+// `X` (handed off in this launch: sc1 loads), partial sums to LDS `red`, then the
+// epilogue. `wait` runs in wave 0 BEFORE its weight requests (the poll must not queue
+// behind them); the other waves request their weights first.
+template <int MT, int EPI, int SPU, int UMAX, typename Wait, typename Ts>
+__device__ __forceinline__ bool fm_gemv(const bf16_t* W, int NG, int KB, int kb_lo, int KBs, int g0, int gs, int nu,
+                                        const bf16_t* X, int ldx, int xbytes, int M, void* Y, int ldy, int ybytes,
+                                        int N, f32x4* red, Wait wait, Ts ts, int ts0) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int xr = lane & 15;
+    const __amdgpu_buffer_rsrc_t wr = frag_rsrc(W, (uint32_t)NG * (uint32_t)KB * 1024u);
+    auto wbatch = [&](int i, bf16x8_s(&w)[SPU]) __attribute__((always_inline)) {
+        const int g = g0 + i * gs;
+#pragma unroll
+        for (int j = 0; j < SPU; ++j) {
+            const int kb = wave + j * FM_NW;
+            const int off = (i < nu && kb < KBs) ? ((g * KB + kb_lo + kb) * 64 + lane) * 16 : (int)0xfffffff0u;
+            w[j] = __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, AUX_NT));
+        }
+    };
+    bool ok = true;
+    if (wave == 0) ok = wait();
+    ts(ts0);
+    bf16x8_s wa[SPU], wb[SPU];
+    bf16x8_s wall[UMAX > 0 ? UMAX : 1][SPU];
+    if constexpr (UMAX > 0) {
+#pragma unroll
+        for (int i = 0; i < UMAX; ++i) wbatch(i, wall[i]);
+    } else {
+        wbatch(0, wa);
+    }
+    wg_barrier();   // the hand-off is complete (or abandoned) for every wave past here
+    // this wave's X fragments: sc1 loads of bytes other workgroups stored sc1
+    const __amdgpu_buffer_rsrc_t xrs = raw_rsrc(X, (uint32_t)xbytes);
+    bf16x8_s xf[MT][SPU];
+    const bf16x8_s z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        const int row = 16 * t + xr;
+        const int xo = (min(row, M - 1) * ldx + kb_lo * 32 + 8 * (lane >> 4)) * 2;
+#pragma unroll
+        for (int j = 0; j < SPU; ++j) {
+            const int kb = min(wave + j * FM_NW, KBs - 1);
+            const bf16x8_s v =
+                __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo + kb * 64, 0, AUX_SC1));
+            xf[t][j] = (row < M && wave + j * FM_NW < KBs) ? v : z8;
+        }
+    }
+    auto mul = [&](int i, bf16x8_s(&w)[SPU]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < SPU; ++j) acc = mfma16(w[j], xf[t][j], acc);
+            if (i < nu) red[((i * MT + t) * FM_NW + wave) * 64 + lane] = acc;
+        }
+    };
+    if constexpr (UMAX > 0) {
+#pragma unroll
+        for (int i = 0; i < UMAX; ++i) mul(i, wall[i]);
+    } else {
+        for (int i = 0; i < nu; i += 2) {
+            wbatch(i + 1, wb);
+            mul(i, wa);
+            wbatch(i + 2, wa);
+            mul(i + 1, wb);
+        }
+    }
+    __syncthreads();
+    ts(ts0 + 1);
+
+    constexpr bool GLU = EPI == EPI_GEGLU;
+    const int n_out = GLU ? N / 2 : N;
+    const __amdgpu_buffer_rsrc_t yr = raw_rsrc(Y, (uint32_t)ybytes);
+    if (!(GLU && lane >= 32)) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const int m = 16 * t + xr;
+            if (m >= M) continue;
+            for (int i = wave; i < nu; i += FM_NW) {
+                const f32x4* ri = red + (size_t)(i * MT + t) * FM_NW * 64 + lane;
+                const int n0 = (g0 + i * gs) * (GLU ? 8 : 16) + 4 * (lane >> 4);
+                if constexpr (GLU) {
+                    f32x4 gs = {0.f, 0.f, 0.f, 0.f}, us = gs;
+#pragma unroll
+                    for (int s2 = 0; s2 < FM_NW; ++s2) {
+                        gs += ri[s2 * 64];
+                        us += ri[s2 * 64 + 32];
+                    }
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_tanh(rbf(gs[r]))) * rbf(us[r]);
+                    // act is handed to other workgroups: one 8-byte write-through store
+                    // (n_out is a multiple of 8 here: fused_mlp checks f % 64)
+                    const uint2 o2 = {pack2(v[0], v[1]), pack2(v[2], v[3])};
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, o2), yr, (m * ldy + n0) * 2, 0,
+                                                          AUX_SC1);
+                } else {
+                    f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s2 = 0; s2 < FM_NW; ++s2) s4 += ri[s2 * 64];
+                    float* y = (float*)Y + (long)m * ldy;   // slabs: read by the next launch
+                    if (n0 + 3 < n_out) *(f32x4*)(y + n0) = s4;
+                    else
+                        for (int r = 0; r < 4; ++r)
+                            if (n0 + r < n_out) y[n0 + r] = s4[r];
+                }
+            }
+        }
+    }
+    return ok;
+}
+
+template <int MT>
+__global__ __launch_bounds__(FM_NW * 64) void fused_mlp_kernel(FusedMlpArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    f32x4* red = (f32x4*)smem;                             // GEMV partial sums
+    float* nred = (float*)smem;                            // norm stage: 2 x 32 floats (before the GEMVs)
+    unsigned* tmo = a.timeout;
+    const int bu = (int)blockIdx.x, nb = (int)gridDim.x;
+    const int d = a.d, f = a.f;
+    auto ts = [&](int k) __attribute__((always_inline)) { T5G_TS(k); };
+    (void)ts;
+    T5G_TS(0);
+    // the next launch's counters: their last user (the previous step's launch of that
+    // layer) has completed, their next user starts after this launch
+    if (bu == 0 && threadIdx.x < FM_SET_LINES)
+        __hip_atomic_store(a.sync_next + threadIdx.x * FM_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    // ---- stage N: the norm workgroups publish xn rows
+    const int nrow = bu - a.norm_b0;
+    if (nrow >= 0 && nrow < a.M) {
+        fm_norm_row(a, nrow, nred);
+        drain_vm();            // every storing wave (R1)
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(a.sync + FS_NORM, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        T5G_TS(1);
+    }
+
+    // ---- stage G: a contiguous run of gate/up units (8 act features each). The norm
+    // workgroups (the last M) start streaming ~5 us late and take FM_NORM_UNITS units;
+    // the others share the rest, the first `uextra` of them one unit more. A run meets at
+    // most two down slices.
+    const int KBg = d / 32, NGg = a.NGgu;
+    const unsigned Mu = (unsigned)a.M;
+    constexpr int SPUg = 72 / FM_NW;
+    const int nr = nb - a.M, rest = NGg - a.M * FM_NORM_UNITS;
+    const int ubase = rest / nr, uextra = rest - ubase * nr;
+    const int nu_g = bu < nr ? ubase + (bu < uextra ? 1 : 0) : FM_NORM_UNITS;
+    const int g_lo = bu < nr ? bu * ubase + min(bu, uextra) : rest + (bu - nr) * FM_NORM_UNITS;
+    bool ok = fm_gemv<MT, EPI_GEGLU, SPUg, MT == 1 ? 5 : 0>(
+        a.Wgu, NGg, KBg, 0, KBg, g_lo, 1, nu_g, a.xn, d, a.M * d * 2, a.M, a.act, f, a.M * f * 2, 2 * f, red,
+        [&]() { return fm_wait(a.sync + FS_NORM, Mu, tmo, 1u); }, ts, 2);
+    drain_vm();                // act stores of every wave (R1)
+    __syncthreads();
+    const int units_per_slice = f / FM_DS / 8;   // gate/up units (8 act features each) per down k-slice
+    if (threadIdx.x == 0 && nu_g > 0) {   // one arrival per slice the run meets, counting its units
+        const int s0 = g_lo / units_per_slice, s1 = (g_lo + nu_g - 1) / units_per_slice;
+        for (int sl = s0; sl <= s1; ++sl) {
+            const int n = min(g_lo + nu_g, (sl + 1) * units_per_slice) - max(g_lo, sl * units_per_slice);
+            __hip_atomic_fetch_add(a.sync + fs_slice(sl), (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+
+    // ---- stage D: down slice s = bu / dg, units j, j + dg, ... (workgroups past 8 * dg idle)
+    const int dg = nb / FM_DS;
+    const int s = bu / dg, j = bu - s * dg;
+    if (s < FM_DS) {
+        const int KBd = f / 32, per = KBd / FM_DS;
+        constexpr int SPUd = 36 / FM_NW;
+        ok &= fm_gemv<MT, EPI_F32, SPUd, 5>(
+            a.Wd, a.NGd, KBd, s * per, per, j, dg, (a.NGd - j + dg - 1) / dg, a.act, f, a.M * f * 2, a.M, a.part_out + (long)s * a.M * d, d,
+            0, d, red, [&]() { return fm_wait(a.sync + fs_slice(s), (unsigned)units_per_slice, tmo, 2u + s); }, ts,
+            4);
+    }
+    (void)ok;
+
+    T5G_TS(6);
+}
+
+// ===========================================================================
+// fused_block_kernel: the cross-attention chain in front of the MLP half (xattn = 1).
+//
+//   N1 (M norm workgroups)   h1 = h + RMSNorm_post1(o-proj slabs) (kept in registers),
+//                            xn1 = RMSNorm_pre1(h1)                       -> L_N1
+//   Q  (every workgroup)     one cross-q unit-slice: 16 q columns x 36 k-steps -> L_Q[head]
+//   A  (8M workgroups)       PMCrossAttention of (row, q head): q from the 2 slabs, PM-RoPE,
+//                            scores / aten softmax / P.V over <= 64 text keys -> L_A[head]
+//   O  (every workgroup)     cross-o unit-slices (4 k-slices of 16 k-steps)     -> L_O[wg % 8]
+//   N2 (norm workgroups)     h = h1 + RMSNorm_post2(cross-o slabs), xn = RMSNorm_pre2(h) -> L_N2
+//   G, D                     as fused_mlp_kernel
+//
+// replacing resid_norm + cross-q (register-X GEMV, 12 waves, 2 k-slices) + cross attention
+// (attn_decode_kernel<256, 1, true>) + cross-o (register-X GEMV, 8 waves, 4 k-slices) in
+// front of the three MLP-half launches, with the same arithmetic in every stage (bitwise
+// equal to the seven launches: tests/test_gpu_fused.py). Every wave requests the weights
+// of a stage as early as its registers allow: Q's before N1 completes, O's during the
+// attention, gate/up's right after O (norm workgroups: after N2), down's after gate/up;
+// the cross K / V of the attention workgroups and their RoPE table at launch start.
+
+// Split form of fm_gemv: the weight requests (waves < NWG) ...
+template <int NWG, int SPU, int UMAX>
+__device__ __forceinline__ void fb_issue(bf16x8_s (&w)[UMAX][SPU], const bf16_t* W, int NG, int KB, int kb_lo, int KBs,
+                                         int g0, int gs, int nu) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave >= NWG) return;
+    const __amdgpu_buffer_rsrc_t wr = frag_rsrc(W, (uint32_t)NG * (uint32_t)KB * 1024u);
+#pragma unroll
+    for (int i = 0; i < UMAX; ++i) {
+        const int g = g0 + i * gs;
+#pragma unroll
+        for (int j = 0; j < SPU; ++j) {
+            const int kb = wave + j * NWG;
+            const int off = (i < nu && kb < KBs) ? ((g * KB + kb_lo + kb) * 64 + lane) * 16 : (int)0xfffffff0u;
+            w[i][j] = __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, AUX_NT));
+        }
+    }
+}
+// ... and the rest: rendezvous, X fragments (sc1), MFMAs, fixed-order wave reduction,
+// epilogue. OUT: 0 = GeGLU bf16 (sc1, 8 B), 1 = fp32 plain, 2 = fp32 sc1 (16 B).
+template <int NWG, int EPI, int SPU, int UMAX, int OUT>
+__device__ __forceinline__ void fb_finish(bf16x8_s (&w)[UMAX][SPU], int g0, int gs, int nu, int kb_lo, int KBs,
+                                          const bf16_t* X, int ldx, int xbytes, int M, void* Y, int ldy, int ybytes,
+                                          int N, f32x4* red) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int xr = lane & 15;
+    wg_barrier();   // the hand-off is complete (or abandoned) for every wave past here
+    if (wave < NWG) {
+        const __amdgpu_buffer_rsrc_t xrs = raw_rsrc(X, (uint32_t)xbytes);
+        bf16x8_s xf[SPU];
+        const bf16x8_s z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int xo = (min(xr, M - 1) * ldx + kb_lo * 32 + 8 * (lane >> 4)) * 2;
+#pragma unroll
+        for (int j = 0; j < SPU; ++j) {
+            const int kb = min(wave + j * NWG, KBs - 1);
+            const bf16x8_s v =
+                __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo + kb * 64, 0, AUX_SC1));
+            xf[j] = (xr < M && wave + j * NWG < KBs) ? v : z8;
+        }
+#pragma unroll
+        for (int i = 0; i < UMAX; ++i) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < SPU; ++j) acc = mfma16(w[i][j], xf[j], acc);
+            if (i < nu) red[(i * NWG + wave) * 64 + lane] = acc;
+        }
+    }
+    __syncthreads();
+    constexpr bool GLU = EPI == EPI_GEGLU;
+    const int n_out = GLU ? N / 2 : N;
+    const int m = xr;
+    if (wave >= NWG || m >= M || (GLU && lane >= 32)) return;
+    const __amdgpu_buffer_rsrc_t yr = raw_rsrc(Y, (uint32_t)ybytes);
+    for (int i = wave; i < nu; i += NWG) {
+        const f32x4* ri = red + (size_t)i * NWG * 64 + lane;
+        const int n0 = (g0 + i * gs) * (GLU ? 8 : 16) + 4 * (lane >> 4);
+        if constexpr (GLU) {
+            f32x4 gsum = {0.f, 0.f, 0.f, 0.f}, usum = gsum;
+#pragma unroll
+            for (int s2 = 0; s2 < NWG; ++s2) {
+                gsum += ri[s2 * 64];
+                usum += ri[s2 * 64 + 32];
+            }
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_tanh(rbf(gsum[r]))) * rbf(usum[r]);
+            const uint2 o2 = {pack2(v[0], v[1]), pack2(v[2], v[3])};
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, o2), yr, (m * ldy + n0) * 2, 0, AUX_SC1);
+        } else {
+            f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s2 = 0; s2 < NWG; ++s2) s4 += ri[s2 * 64];
+            if constexpr (OUT == 2) {
+                // n_out is a multiple of 16 here (the q / cross-o widths)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, s4), yr, (m * ldy + n0) * 4, 0,
+                                                       AUX_SC1);
+            } else {
+                float* y = (float*)Y + (long)m * ldy;   // slabs read by the next launch
+                if (n0 + 3 < n_out) *(f32x4*)(y + n0) = s4;
+                else
+                    for (int r = 0; r < 4; ++r)
+                        if (n0 + r < n_out) y[n0 + r] = s4[r];
+            }
+        }
+    }
+}
+
+// resid_norm_kernel<4, 2>'s arithmetic for row m: v = bf16(sum of the 4 slabs),
+// post-norm, h = bf16(r + v) (r8: the residual in, the new residual out, in registers),
+// xn = pre-norm(h) stored write-through. Slabs read plain (previous launch) or sc1.
+template <bool SC1>
+__device__ __forceinline__ void fb_norm(const float* part, int M, int m, int d, const bf16_t* post_w,
+                                        const bf16_t* pre_w, float eps, float (&r8)[8], bf16_t* xn, float* red) {
+    const int c = threadIdx.x;
+    const bool active = 8 * c < d;
+    const int cc = active ? c : d / 8 - 1;
+    const u32x4 w_post = *(const u32x4*)(post_w + 8 * cc);
+    const u32x4 w_pre = *(const u32x4*)(pre_w + 8 * cc);
+    f32x4 p[FM_NS][2];
+    const __amdgpu_buffer_rsrc_t pr = raw_rsrc(part, (uint32_t)(FM_NS * M * d * 4));
+#pragma unroll
+    for (int s = 0; s < FM_NS; ++s) {
+        const int o = ((s * M + m) * d + 8 * cc) * 4;
+        if constexpr (SC1) {
+            p[s][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, o, 0, AUX_SC1));
+            p[s][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, o + 16, 0, AUX_SC1));
+        } else {
+            const f32x4* ps = (const f32x4*)(part + ((long)s * M + m) * d + 8 * cc);
+            p[s][0] = ps[0];
+            p[s][1] = ps[1];
+        }
+    }
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < FM_NS; ++s) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] += p[s][0][j];
+            v[4 + j] += p[s][1][j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = rbf(v[j]);
+    fm_rms8(v, active, d, w_post, eps, red);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = rbf(r8[j] + v[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r8[j] = v[j];
+    fm_rms8(v, active, d, w_pre, eps, red + 32);
+    if (active) {
+        const __amdgpu_buffer_rsrc_t xr = raw_rsrc(xn, (uint32_t)(M * d * 2));
+        __builtin_amdgcn_raw_buffer_store_b128(pack8f(v), xr, (m * d + 8 * c) * 2, 0, AUX_SC1);
+    }
+}
+
+// every storing wave drains, the workgroup meets, one lane adds `n` to `ctr`
+__device__ __forceinline__ void fb_publish(unsigned* ctr, unsigned n) {
+    drain_vm();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// LDS of the attention stage (after the GEMV partial sums)
+struct FbAttnLds {
+    f32x4 ored[4][32][2];
+    float sm[64];
+    float pl[64 + 16];
+    float qs[256];
+    float stat_l;
+};
+
+template <bool XA_DUMMY = true>
+__global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    f32x4* red = (f32x4*)smem;                                   // GEMV partial sums, <= 60 KB
+    FbAttnLds& al = *(FbAttnLds*)(smem + 5 * FM_NW * 1024);      // attention scratch
+    float* nred = (float*)(smem + 5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16);   // norm: 2 x 32 floats
+    unsigned* tmo = a.timeout;
+    const int bu = (int)blockIdx.x, nb = (int)gridDim.x;
+    const int tq = (int)threadIdx.x, wave = tq >> 6, lane = tq & 63;
+    const int d = a.d, f = a.f, M = a.M, D = 256;
+    T5G_TS(0);
+    if (bu == 0 && tq < FM_SET_LINES)
+        __hip_atomic_store(a.sync_next + tq * FM_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int nrow = bu - a.norm_b0;
+    const bool normwg = nrow >= 0 && nrow < M;
+    const bool attnwg = bu < M * a.Hq;
+    const int am = bu / a.Hq, ah = bu - am * a.Hq;   // attention task (row, q head)
+    bool ok = true;
+
+    // ---- launch start: the attention workgroups request their row's cross K / V chunk
+    // and RoPE row (attn_decode_kernel<256, 1, true>'s VFIRST loads, waves 0-3)
+    constexpr int LPK = 32, KPW = 2, KPB = 8, NIT = 8;
+    const int kg = lane / LPK, dl = lane % LPK;
+    u32x4 kr[NIT], vr[NIT];
+    float c8[8], s8[8];
+    int alen = 0;
+    if (attnwg && wave < 4) {
+        alen = a.enc_len[am];
+        const int kvc = ah / (a.Hq / a.Hkv);
+        const long hs = (long)a.kv_cap * D, bs = hs * a.Hkv;
+        const __amdgpu_buffer_rsrc_t krs = frag_rsrc(a.ck + am * bs + kvc * hs, (uint32_t)a.kv_cap * D * 2u);
+        const __amdgpu_buffer_rsrc_t vrs = frag_rsrc(a.cv + am * bs + kvc * hs, (uint32_t)a.kv_cap * D * 2u);
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int j = i * KPB + wave * KPW + kg;
+            const int off = j < alen ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
+            kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
+            vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
+        }
+        const float* tr = a.rope_tab + (long)am * D + (8 * dl) % (D / 2);
+        const f32x4 ca = *(const f32x4*)tr, cb = *(const f32x4*)(tr + 4);
+        const f32x4 sa = *(const f32x4*)(tr + D / 2), sb = *(const f32x4*)(tr + D / 2 + 4);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            c8[jj] = ca[jj];
+            c8[4 + jj] = cb[jj];
+            s8[jj] = sa[jj];
+            s8[4 + jj] = sb[jj];
+        }
+    }
+
+    // ---- N1
+    float hreg[8];
+    if (normwg) {
+        const int cc = min(tq, d / 8 - 1);
+        unpack8f(*(const u32x4*)(a.h + (long)nrow * d + 8 * cc), hreg);
+        fb_norm<false>(a.o_slabs, M, nrow, d, a.post1_w, a.pre1_w, a.eps, hreg, a.xn1, nred);
+        fb_publish(cline(a.sync, L_N1), 1u);
+    }
+
+    // ---- Q: cross-q unit-slice bu (unit bu % NGq, k-slice bu / NGq)
+    {
+        const int uq = bu % a.NGq, sq = bu / a.NGq;
+        bf16x8_s wq[1][3];
+        if (wave == 0) ok &= fm_wait(cline(a.sync, L_N1), (unsigned)M, tmo, 1u);
+        T5G_TS(1);
+        fb_issue<FM_NW, 3, 1>(wq, a.Wq, a.NGq, d / 32, sq * 36, 36, uq, 1, 1);
+        fb_finish<FM_NW, EPI_F32, 3, 1, 2>(wq, uq, 1, 1, sq * 36, 36, a.xn1, d, M * d * 2, M,
+                                           a.qslab + (long)sq * M * a.q_dim, a.q_dim, M * a.q_dim * 4, a.q_dim, red);
+        fb_publish(cline(a.sync, L_Q0 + uq / (D / 16)), 1u);
+    }
+
+    // ---- A (attention workgroups) with O's weight requests around it
+    const int so = bu / (nb / 4), jo = bu - so * (nb / 4), go = nb / 4;
+    const int nu_o = (a.NGo - jo + go - 1) / go;
+    bf16x8_s wo[3][2];
+    if (attnwg && wave >= 4) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, go, nu_o);
+    if (attnwg) {
+        const int qcnt = 2 * (D / 16);   // 16 q units per head x 2 k-slices
+        if (wave == 0) ok &= fm_wait(cline(a.sync, L_Q0 + ah), (unsigned)qcnt, tmo, 2u);
+        wg_barrier();
+        const int n = alen;
+        const int span = alen;
+        if (tq < 256) {
+            const int c4 = tq < D / 4 ? tq : 0;
+            const int col = ah * D + 4 * c4;
+            const __amdgpu_buffer_rsrc_t qr = raw_rsrc(a.qslab, (uint32_t)(2 * M * a.q_dim * 4));
+            const f32x4 u0 = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(qr, (am * a.q_dim + col) * 4, 0, AUX_SC1));
+            const f32x4 u1 = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(qr, ((M + am) * a.q_dim + col) * 4, 0, AUX_SC1));
+            const f32x4 acc = u0 + u1;
+            if (tq < D / 4) {
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) al.qs[4 * c4 + jj] = rbf(acc[jj]);
+            }
+        }
+        __syncthreads();
+        if (tq < 256) {
+            float q[8];
+            const float sg = dl < LPK / 2 ? -1.0f : 1.0f;
+            const int pbase = (8 * dl + D / 2) % D;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const float x = al.qs[8 * dl + jj];
+                const float pr = al.qs[pbase + jj];
+                q[jj] = rbf(rbf(x * c8[jj]) + rbf((sg * pr) * s8[jj]));
+            }
+#pragma unroll
+            for (int i = 0; i < NIT; ++i) {
+                const int j = i * KPB + wave * KPW + kg;
+                if (j >= n) {
+                    kr[i] = (u32x4){0u, 0u, 0u, 0u};
+                    vr[i] = (u32x4){0u, 0u, 0u, 0u};
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NIT; ++i) {
+                float sc = 0.f;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const float k0 = bf_lo(kr[i][jj]), k1 = bf_hi(kr[i][jj]);
+                    sc += q[2 * jj] * k0 + q[2 * jj + 1] * k1;
+                }
+                sc = xsum<LPK>(sc);
+                const int jl = i * KPB + wave * KPW + kg;
+                if (dl == 0) al.sm[jl] = __fmul_rn(sc, a.scale);
+            }
+        }
+        __syncthreads();
+        if (wave == 0) {
+            const float sc = lane < n ? al.sm[lane] : -INFINITY;
+            const float mx = wave_max(sc);
+            const float p = lane < n ? sdpa_p(__fsub_rn(sc, mx), lane, span) : 0.f;
+            al.pl[lane] = p;
+            if (lane < 16) al.pl[64 + lane] = 0.f;
+            al.sm[lane] = rbf(p);
+            __builtin_amdgcn_wave_barrier();
+            const float l = sdpa_block_sum_lds<64>(al.pl, span, lane);
+            if (lane == 0) al.stat_l = l;
+        }
+        __syncthreads();
+        if (tq < 256) {
+            float o[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) o[jj] = 0.f;
+#pragma unroll
+            for (int i = 0; i < NIT; ++i) {
+                const int jl = i * KPB + wave * KPW + kg;
+                const float p = al.sm[jl];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    o[2 * jj] += p * bf_lo(vr[i][jj]);
+                    o[2 * jj + 1] += p * bf_hi(vr[i][jj]);
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+                for (int off = LPK; off < 64; off <<= 1) o[jj] += __shfl_xor(o[jj], off, 64);
+            if (kg == 0) {
+                al.ored[wave][dl][0] = (f32x4){o[0], o[1], o[2], o[3]};
+                al.ored[wave][dl][1] = (f32x4){o[4], o[5], o[6], o[7]};
+            }
+        }
+        __syncthreads();
+        if (tq < LPK && n > 0) {
+            const int d8 = tq;
+            const f32x4 lo4 = al.ored[0][d8][0] + al.ored[1][d8][0] + al.ored[2][d8][0] + al.ored[3][d8][0];
+            const f32x4 hi4 = al.ored[0][d8][1] + al.ored[1][d8][1] + al.ored[2][d8][1] + al.ored[3][d8][1];
+            const float inv = __fdiv_rn(1.0f, al.stat_l);
+            u32x4 w;
+            w[0] = pack2(__fmul_rn(lo4[0], inv), __fmul_rn(lo4[1], inv));
+            w[1] = pack2(__fmul_rn(lo4[2], inv), __fmul_rn(lo4[3], inv));
+            w[2] = pack2(__fmul_rn(hi4[0], inv), __fmul_rn(hi4[1], inv));
+            w[3] = pack2(__fmul_rn(hi4[2], inv), __fmul_rn(hi4[3], inv));
+            const __amdgpu_buffer_rsrc_t orr = raw_rsrc(a.att, (uint32_t)(M * a.q_dim * 2));
+            __builtin_amdgcn_raw_buffer_store_b128(w, orr, (am * a.q_dim + ah * D + 8 * d8) * 2, 0, AUX_SC1);
+        }
+        fb_publish(cline(a.sync, L_A0 + ah), 1u);
+    }
+
+    // ---- O: cross-o unit-slices (4 k-slices of 16 k-steps, 8 waves)
+    if (wave == 0) {
+        for (int h = 0; h < a.Hq; ++h) ok &= fm_wait(cline(a.sync, L_A0 + h), (unsigned)M, tmo, 3u);
+    }
+    T5G_TS(2);
+    if (!(attnwg && wave >= 4)) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, go, nu_o);
+    fb_finish<8, EPI_F32, 2, 3, 2>(wo, jo, go, nu_o, so * 16, 16, a.att, a.q_dim, M * a.q_dim * 2, M,
+                                   a.oslab + (long)so * M * d, d, M * d * 4, d, red);
+    fb_publish(cline(a.sync, L_O0 + (bu & 7)), 1u);
+
+    // ---- N2 (norm workgroups, before their gate/up requests)
+    if (normwg) {
+        if (wave == 0) {
+            for (int k = 0; k < 8; ++k) ok &= fm_wait(cline(a.sync, L_O0 + k), (unsigned)(nb / 8), tmo, 4u);
+        }
+        wg_barrier();
+        fb_norm<true>(a.oslab, M, nrow, d, a.post_w, a.pre_w, a.eps, hreg, a.xn, nred);
+        if (tq < d / 8) *(u32x4*)(a.h + (long)nrow * d + 8 * tq) = pack8f(hreg);   // read by the next launch
+        fb_publish(cline(a.sync, L_N2), 1u);
+    }
+
+    // ---- G: gate/up (contiguous unit runs, as fused_mlp_kernel)
+    const int KBg = d / 32, NGg = a.NGgu;
+    const int nr = nb - M, rest = NGg - M * FM_NORM_UNITS;
+    const int ubase = rest / nr, uextra = rest - ubase * nr;
+    const int nu_g = bu < nr ? ubase + (bu < uextra ? 1 : 0) : FM_NORM_UNITS;
+    const int g_lo = bu < nr ? bu * ubase + min(bu, uextra) : rest + (bu - nr) * FM_NORM_UNITS;
+    {
+        bf16x8_s wg[5][6];
+        if (wave == 0) ok &= fm_wait(cline(a.sync, L_N2), (unsigned)M, tmo, 5u);
+        T5G_TS(3);
+        fb_issue<FM_NW, 6, 5>(wg, a.Wgu, NGg, KBg, 0, KBg, g_lo, 1, nu_g);
+        fb_finish<FM_NW, EPI_GEGLU, 6, 5, 0>(wg, g_lo, 1, nu_g, 0, KBg, a.xn, d, M * d * 2, M, a.act, f, M * f * 2,
+                                             2 * f, red);
+    }
+    T5G_TS(4);
+    const int units_per_slice = f / FM_DS / 8;
+    drain_vm();
+    __syncthreads();
+    if (tq == 0 && nu_g > 0) {
+        const int s0 = g_lo / units_per_slice, s1 = (g_lo + nu_g - 1) / units_per_slice;
+        for (int sl = s0; sl <= s1; ++sl) {
+            const int n = min(g_lo + nu_g, (sl + 1) * units_per_slice) - max(g_lo, sl * units_per_slice);
+            __hip_atomic_fetch_add(a.sync + fs_slice(sl), (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+
+    // ---- D: down slices (as fused_mlp_kernel)
+    const int dg = nb / FM_DS;
+    const int s = bu / dg, j = bu - s * dg;
+    if (s < FM_DS) {
+        const int KBd = f / 32, per = KBd / FM_DS;
+        const int nu_d = (a.NGd - j + dg - 1) / dg;
+        bf16x8_s wd[5][3];
+        if (wave == 0) ok &= fm_wait(a.sync + fs_slice(s), (unsigned)units_per_slice, tmo, 6u + s);
+        T5G_TS(5);
+        fb_issue<FM_NW, 3, 5>(wd, a.Wd, a.NGd, KBd, s * per, per, j, dg, nu_d);
+        fb_finish<FM_NW, EPI_F32, 3, 5, 1>(wd, j, dg, nu_d, s * per, per, a.act, f, M * f * 2, M,
+                                           a.part_out + (long)s * M * d, d, 0, d, red);
+    }
+    (void)ok;
+    T5G_TS(6);
+}
+
+constexpr size_t FM_LDS_MAX = 160 * 1024;
+
+int fused_mlp(const FusedMlpArgs& a_in, hipStream_t st) {
+    FusedMlpArgs a = a_in;
+    if (a.M <= 0) return 0;
+    // the shapes the stages are built for: K = 2304 gate/up (72 k-steps), f = 9216 down in
+    // 8 slices of 36 k-steps, 4 cross-o slabs, <= 32 rows
+    if (a.M > 32 || a.d != 2304 || a.f != 9216 || a.f % 64) return -1;
+    if (!a.part_in || !a.post_w || !a.pre_w || !a.h || !a.xn || !a.Wgu || !a.act || !a.Wd || !a.part_out || !a.sync ||
+        !a.sync_next || !a.timeout || a.sync_next == a.sync)
+        return -1;
+    if (a.NGgu * 8 != a.f || a.NGd * 16 != a.d) return -1;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev))
+        return -2;
+    const int nb = a.grid > 0 ? a.grid : cus;
+    if (nb > cus || nb < FM_DS || nb < a.M) return -1;   // every workgroup must be resident at once
+    const int nr = nb - a.M, rest = a.NGgu - a.M * FM_NORM_UNITS;
+    if (nr <= 0 || rest < 0) return -1;
+    const int nu_g = (rest + nr - 1) / nr;
+    const int nu_d = (a.NGd + nb / FM_DS - 1) / (nb / FM_DS);
+    if (nu_g > 5 || nu_d > 5) return -1;   // UMAX = 5 batches per wave (needs >= 231 workgroups)
+    const int MT = a.M > 16 ? 2 : 1;
+    if (a.xattn) {
+        // the cross-attention chain: 2 k-slices x NGq cross-q units = one unit-slice per
+        // workgroup, 4 x 64 cross-o workgroups, 8 x 32 down workgroups; one 64-key chunk of
+        // text keys; attention and norm workgroups disjoint
+        if (MT != 1 || nb != 2 * a.NGq || nb % 32 || a.D != 256 || a.Hq * a.D != a.q_dim || a.Hq % a.Hkv ||
+            a.NGq * 16 != a.q_dim || a.NGo * 16 != a.d || a.kv_cap > 64 || a.M * a.Hq > nb - a.M || !a.o_slabs ||
+            !a.post1_w || !a.pre1_w || !a.xn1 || !a.Wq || !a.qslab || !a.ck || !a.cv || !a.enc_len || !a.rope_tab ||
+            !a.att || !a.Wo || !a.oslab)
+            return -1;
+        if ((a.NGo + nb / 4 - 1) / (nb / 4) > 3) return -1;
+        a.norm_b0 = nb - a.M;
+        const size_t shm = (size_t)5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16 + 64 * sizeof(float);
+        static bool attr_b = false;
+        if (!attr_b) {
+            (void)hipFuncSetAttribute((const void*)fused_block_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)FM_LDS_MAX);
+            int occ = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fused_block_kernel<true>, FM_NW * 64, shm) !=
+                    hipSuccess || occ < 1)
+                return -1;
+            attr_b = true;
+        }
+        hipLaunchKernelGGL(fused_block_kernel<true>, dim3((unsigned)nb), dim3(FM_NW * 64), shm, st, a);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
+    const size_t shm = (size_t)5 * MT * FM_NW * 64 * 16;
+    if (shm > FM_LDS_MAX) return -1;
+    // norm rows on workgroups with one gate/up unit fewer (their weight stream starts after
+    // the norm): the last ones
+    a.norm_b0 = nb - a.M;
+    auto* fn = MT == 1 ? fused_mlp_kernel<1> : fused_mlp_kernel<2>;
+    static bool attr[2] = {false, false};
+    if (!attr[MT - 1]) {
+        (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FM_LDS_MAX);
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, FM_NW * 64, shm) != hipSuccess || occ < 1) return -1;
+        attr[MT - 1] = true;
+    }
+    hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(FM_NW * 64), shm, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace t5g

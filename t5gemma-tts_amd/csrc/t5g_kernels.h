@@ -45,6 +45,61 @@ struct DecGemmArgs {
 int gemv_dec(const DecGemmArgs& a, int epi, hipStream_t st);
 size_t gemv_dec_lds_bytes(const DecGemmArgs& a, int rg);
 
+// decode MLP half in one persistent launch (fused.hip): norm of the cross-o slabs ->
+// gate/up GeGLU -> down slabs, hand-offs in-launch
+struct FusedMlpArgs {
+    int M, d, f;              // rows (<= 32), hidden (2304), intermediate (9216)
+    const float* part_in;     // cross-o fp32 slabs [4][M][d]
+    const bf16_t* post_w;     // RMSNorm(1+w) of the cross-attention output
+    const bf16_t* pre_w;      // RMSNorm(1+w) in front of the MLP
+    float eps;
+    bf16_t* h;                // residual [M][d], updated in place
+    bf16_t* xn;               // normed rows [M][d] (handed off in-launch)
+    const bf16_t* Wgu;        // packed P16 gate/up (interleaved), NGgu row groups, K = d
+    int NGgu;
+    bf16_t* act;              // [M][f] (handed off in-launch)
+    const bf16_t* Wd;         // packed P16 down, NGd row groups, K = f
+    int NGd;
+    float* part_out;          // down fp32 slabs [8][M][d] (may alias part_in: written only after
+                              // every norm workgroup has consumed part_in)
+    unsigned* sync;           // this launch's FM_SET_WORDS counter words (zero when it starts)
+    unsigned* sync_next;      // the next launch's set: zeroed by this launch (its last user is done)
+    unsigned* timeout;        // sticky: a wait that gave up stores its code here
+    int grid;                 // 0: one workgroup per CU
+    int norm_b0;              // set by fused_mlp: first norm workgroup
+    int dbg_seq;              // diagnostic timeline slot (T5G_DBG_TS builds only)
+    // ---- cross-attention chain in front (xattn = 1: fused.hip fused_block_kernel):
+    //   N1: h1 = h + RMSNorm_post1(o-proj slabs), xn1 = RMSNorm_pre1(h1)
+    //   Q:  cross-q fp32 slabs [2][M][q_dim] = xn1 . Wq^T (2 k-slices of 36 k-steps)
+    //   A:  att = PMCrossAttention(q slabs, cross K/V) per (row, q head)
+    //   O:  cross-o fp32 slabs [4][M][d] = att . Wo^T; then part_in := those slabs
+    int xattn;
+    const float* o_slabs;     // self-attention o-projection slabs [4][M][d] (previous launch)
+    const bf16_t* post1_w;    // post_self_attn_layernorm
+    const bf16_t* pre1_w;     // pre_cross_attn_layernorm
+    bf16_t* xn1;              // [M][d] handed off in-launch
+    const bf16_t* Wq;         // packed cross q_proj, NGq row groups, K = d
+    int NGq;
+    float* qslab;             // [2][M][q_dim] handed off in-launch
+    const bf16_t* ck;         // cross K / V cache of the layer [B][Hkv][kv_cap][D]
+    const bf16_t* cv;
+    int kv_cap;
+    const int* enc_len;       // [B] text lengths (keys of each row)
+    const float* rope_tab;    // [B][D] this step's PM-RoPE cos | sin
+    int q_dim, Hq, Hkv, D;
+    float scale;
+    bf16_t* att;              // [M][q_dim] handed off in-launch
+    const bf16_t* Wo;         // packed cross o_proj, NGo row groups, K = q_dim
+    int NGo;
+    float* oslab;             // [4][M][d] handed off in-launch (the N2 norm's input)
+};
+int fused_mlp(const FusedMlpArgs& a, hipStream_t st);
+// counter words of one fused launch, each on its own 128-byte line (arrivals on one line
+// serialise at ~12 ns each): N1, 8 cross-q heads, 8 attention heads, 8 cross-o groups,
+// N2, 8 down slices. The engine keeps one set per decoder layer after one line for the
+// timeout word.
+constexpr int FM_LINE = 32, FM_SET_LINES = 34, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
+
 // ---- row-wise residual / RMSNorm / embedding -------------------------------
 struct NormArgs {
     int M, d;

@@ -210,6 +210,11 @@ class T5GemmaTTSEngine:
         self._logits_ptr = self.L.t5g_logits_ptr(h, C.byref(ld))
         self.logits_ld = ld.value
 
+    def set_fused(self, enable: bool) -> None:
+        """Decode MLP half (norm -> gate/up -> down) as one persistent launch (default) or as
+        three launches; the two are bitwise equal (csrc/fused.hip)."""
+        _lib.check(self.L.t5g_engine_set_fused(self.h, 1 if enable else 0), "set_fused")
+
     def close(self):
         if getattr(self, "h", None):
             self.L.t5g_engine_destroy(self.h)

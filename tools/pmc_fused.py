@@ -1,0 +1,34 @@
+"""Drive the fused decode-MLP launch (csrc/fused.hip) at C3 shape (M = 8, 2b-2b widths) over
+the 26 decoder layers' weights (3.3 GB, beyond the 256 MiB Infinity Cache), as bench.py's
+roofline leg does, so rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE can count its HBM bytes per
+launch (separate passes, tools/gpu_r3_pmc.sh). GPU only."""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import t5gemma_tts_amd  # noqa: E402,F401
+from t5gemma_tts_amd import _lib  # noqa: E402
+
+
+def main():
+    from t5gemma_tts_amd.config import config_2b2b
+    from t5gemma_tts_amd.engine import T5GemmaTTSEngine
+    from t5gemma_tts_amd.weights import synthetic_weights
+    L = _lib.lib()
+    cfg = config_2b2b()
+    B = 8
+    sd = synthetic_weights(cfg, seed=1234, device="cuda:0")
+    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=B, max_text=64, max_audio=256, max_gen=64)
+    del sd
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    us = C.c_float()
+    _lib.check(L.t5g_time_decode_mlp(eng.h, B, 52, st, C.byref(us)), "time_decode_mlp")
+    alg = _lib.fused_mlp_bytes(B)
+    print(f"fused_mlp avg {us.value:.2f} us/launch, algorithmic {alg} B -> {alg / us.value / 1e3:.1f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -16,6 +16,12 @@ OPS = {
                 "algorithmic": 2 * 9216 * 2304 * 2 + 8 * 2304 * 2 + 8 * 9216 * 2,
                 "what": "decode gate/up GEGLU GEMV, M=8, N=18432, K=2304 (tools/pmc_gateup.py: 26 weight sets "
                         "rotated, 2.2 GB > 256 MiB Infinity Cache)"},
+    "fused_mlp": {"kernels": ["fused_mlp_kernel<1>"],
+                  "algorithmic": 2 * 9216 * 2304 * 2 + 2304 * 9216 * 2 + 4 * 8 * 2304 * 4 + 8 * 2304 * 2 + 2 * 2304 * 2
+                  + 8 * 2304 * 2 + 8 * 8 * 2304 * 4,
+                  "what": "fused decode MLP half (norm -> gate/up GeGLU -> down), M=8, 2b-2b widths "
+                          "(tools/pmc_fused.py: 26 layers' weights rotated, 3.3 GB > 256 MiB Infinity Cache); "
+                          "algorithmic = weights + cross-o slabs, h, norm weights in + h, down slabs out"},
     "attention": {"kernels": ["attn_decode_kernel<256, 2, false>", "attn_pvc_kernel<256, 2, 32>"],
                   "algorithmic": None,
                   "what": "decode self attention (scores + P.V/combine launches), 8 rows x 8/4 heads x 256, L ~ 527 "
