@@ -288,8 +288,13 @@ def main():
             # 208 launches rotated over the 26 layers' weights (3.3 GB >> 256 MiB Infinity
             # Cache): every launch streams from HBM, as inside a decode step
             _lib.check(L.t5g_time_decode_mlp(eng.h, B, 208, st, C.byref(us)), "time_decode_mlp")
-            us_k, alg_bytes, kname = us.value, _lib.fused_mlp_bytes(B, d, f), _lib.FUSED_MLP_KERNEL
-            pmc = os.path.join(REPO, "profiles", "r03_pmc_fused_mlp.json")
+            if B <= 16:   # the step runs the whole post-self-attention block in one launch
+                us_k, kname = us.value, _lib.FUSED_BLOCK_KERNEL
+                alg_bytes = _lib.fused_block_bytes(B, wl_tx, d, f)
+                pmc = os.path.join(REPO, "profiles", "r03_pmc_fused_block.json")
+            else:
+                us_k, alg_bytes, kname = us.value, _lib.fused_mlp_bytes(B, d, f), _lib.FUSED_MLP_KERNEL
+                pmc = os.path.join(REPO, "profiles", "r03_pmc_fused_mlp.json")
         else:
             # rotate over every decoder layer's gate/up weights (2.2 GB >> 256 MiB Infinity
             # Cache) so each launch streams its weights from HBM, as inside a decode step

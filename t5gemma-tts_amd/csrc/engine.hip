@@ -1363,13 +1363,17 @@ extern "C" int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void
     // its counter set zeroed by layer l - 1's (the last launch before this call was a step's
     // last layer, which zeroed layer 0's set); one untimed rotation first
     const int n = (iters + L - 1) / L * L;
+    // the launch decoder_pass runs at B rows: the cross-attention chain + MLP block up to
+    // 16 rows when the device supports it, the MLP half alone otherwise
+    const bool block = B <= 16 && fused_mlp_check(fused_block_args(e, B, 0)) == 0;
+    auto args = [&](int l) { return block ? fused_block_args(e, B, l) : fused_args(e, B, l); };
     int rc = T5G_OK;
-    for (int l = 0; l < L && !rc; ++l) rc = fused_mlp(fused_args(e, B, l), st);
+    for (int l = 0; l < L && !rc; ++l) rc = fused_mlp(args(l), st);
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, st));
-    for (int i = 0; i < n && !rc; ++i) rc = fused_mlp(fused_args(e, B, i % L), st);
+    for (int i = 0; i < n && !rc; ++i) rc = fused_mlp(args(i % L), st);
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;

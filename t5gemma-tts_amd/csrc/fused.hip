@@ -52,17 +52,23 @@ __device__ __forceinline__ unsigned ld_rlx(unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one wave polls `w` until it reaches `target`; false if this or an earlier wait of the
-// launch (or of an earlier launch of the call) gave up
-__device__ __forceinline__ bool fm_wait(unsigned* w, unsigned target, unsigned* tmo, unsigned code) {
+// one wave polls N counter lines of a set at once (lane i reads line line0 + i, lane 63 the
+// timeout word): every round is ONE memory round trip whatever N is; true when every line
+// has reached `target`, false on a timeout (this wait's or an earlier one's)
+template <int N>
+__device__ __forceinline__ bool fm_wait_n(unsigned* set, int line0, unsigned target, unsigned* tmo, unsigned code) {
+    static_assert(N >= 1 && N < 64, "lines per poll");
+    const int lane = threadIdx.x & 63;
+    unsigned* p = lane == 63 ? tmo : set + (line0 + min(lane, N - 1)) * FM_LINE;
     for (unsigned spins = 0;; ++spins) {
-        if (ld_rlx(w) >= target) return true;
-        if ((spins & 63) == 0 && ld_rlx(tmo) != 0) return false;
+        const unsigned v = ld_rlx(p);
+        if (__all(lane == 63 || v >= target)) return true;
+        if (__shfl(v, 63, 64) != 0) return false;
         if (spins > FM_SPIN_MAX) {
-            __hip_atomic_store(tmo, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(tmo, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
     }
 }
 
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_mlp_kernel(FusedMlpArgs a) {
     const int g_lo = bu < nr ? bu * ubase + min(bu, uextra) : rest + (bu - nr) * FM_NORM_UNITS;
     bool ok = fm_gemv<MT, EPI_GEGLU, SPUg, MT == 1 ? 5 : 0>(
         a.Wgu, NGg, KBg, 0, KBg, g_lo, 1, nu_g, a.xn, d, a.M * d * 2, a.M, a.act, f, a.M * f * 2, 2 * f, red,
-        [&]() { return fm_wait(a.sync + FS_NORM, Mu, tmo, 1u); }, ts, 2);
+        [&]() { return fm_wait_n<1>(a.sync, L_N2, Mu, tmo, 1u); }, ts, 2);
     drain_vm();                // act stores of every wave (R1)
     __syncthreads();
     const int units_per_slice = f / FM_DS / 8;   // gate/up units (8 act features each) per down k-slice
@@ -333,7 +339,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_mlp_kernel(FusedMlpArgs a) {
         constexpr int SPUd = 36 / FM_NW;
         ok &= fm_gemv<MT, EPI_F32, SPUd, 5>(
             a.Wd, a.NGd, KBd, s * per, per, j, dg, (a.NGd - j + dg - 1) / dg, a.act, f, a.M * f * 2, a.M, a.part_out + (long)s * a.M * d, d,
-            0, d, red, [&]() { return fm_wait(a.sync + fs_slice(s), (unsigned)units_per_slice, tmo, 2u + s); }, ts,
+            0, d, red, [&]() { return fm_wait_n<1>(a.sync, L_SL0 + s, (unsigned)units_per_slice, tmo, 2u + s); }, ts,
             4);
     }
     (void)ok;
@@ -576,7 +582,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     {
         const int uq = bu % a.NGq, sq = bu / a.NGq;
         bf16x8_s wq[1][3];
-        if (wave == 0) ok &= fm_wait(cline(a.sync, L_N1), (unsigned)M, tmo, 1u);
+        if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N1, (unsigned)M, tmo, 1u);
         T5G_TS(1);
         fb_issue<FM_NW, 3, 1>(wq, a.Wq, a.NGq, d / 32, sq * 36, 36, uq, 1, 1);
         fb_finish<FM_NW, EPI_F32, 3, 1, 2>(wq, uq, 1, 1, sq * 36, 36, a.xn1, d, M * d * 2, M,
@@ -591,7 +597,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     if (attnwg && wave >= 4) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, go, nu_o);
     if (attnwg) {
         const int qcnt = 2 * (D / 16);   // 16 q units per head x 2 k-slices
-        if (wave == 0) ok &= fm_wait(cline(a.sync, L_Q0 + ah), (unsigned)qcnt, tmo, 2u);
+        if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_Q0 + ah, (unsigned)qcnt, tmo, 2u);
         wg_barrier();
         const int n = alen;
         const int span = alen;
@@ -695,9 +701,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     }
 
     // ---- O: cross-o unit-slices (4 k-slices of 16 k-steps, 8 waves)
-    if (wave == 0) {
-        for (int h = 0; h < a.Hq; ++h) ok &= fm_wait(cline(a.sync, L_A0 + h), (unsigned)M, tmo, 3u);
-    }
+    if (wave == 0) ok &= fm_wait_n<8>(a.sync, L_A0, (unsigned)M, tmo, 3u);   // the 8 q heads
     T5G_TS(2);
     if (!(attnwg && wave >= 4)) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, go, nu_o);
     fb_finish<8, EPI_F32, 2, 3, 2>(wo, jo, go, nu_o, so * 16, 16, a.att, a.q_dim, M * a.q_dim * 2, M,
@@ -706,9 +710,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
 
     // ---- N2 (norm workgroups, before their gate/up requests)
     if (normwg) {
-        if (wave == 0) {
-            for (int k = 0; k < 8; ++k) ok &= fm_wait(cline(a.sync, L_O0 + k), (unsigned)(nb / 8), tmo, 4u);
-        }
+        if (wave == 0) ok &= fm_wait_n<8>(a.sync, L_O0, (unsigned)(nb / 8), tmo, 4u);
         wg_barrier();
         fb_norm<true>(a.oslab, M, nrow, d, a.post_w, a.pre_w, a.eps, hreg, a.xn, nred);
         if (tq < d / 8) *(u32x4*)(a.h + (long)nrow * d + 8 * tq) = pack8f(hreg);   // read by the next launch
@@ -723,7 +725,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     const int g_lo = bu < nr ? bu * ubase + min(bu, uextra) : rest + (bu - nr) * FM_NORM_UNITS;
     {
         bf16x8_s wg[5][6];
-        if (wave == 0) ok &= fm_wait(cline(a.sync, L_N2), (unsigned)M, tmo, 5u);
+        if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N2, (unsigned)M, tmo, 5u);
         T5G_TS(3);
         fb_issue<FM_NW, 6, 5>(wg, a.Wgu, NGg, KBg, 0, KBg, g_lo, 1, nu_g);
         fb_finish<FM_NW, EPI_GEGLU, 6, 5, 0>(wg, g_lo, 1, nu_g, 0, KBg, a.xn, d, M * d * 2, M, a.act, f, M * f * 2,
@@ -748,7 +750,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         const int KBd = f / 32, per = KBd / FM_DS;
         const int nu_d = (a.NGd - j + dg - 1) / dg;
         bf16x8_s wd[5][3];
-        if (wave == 0) ok &= fm_wait(a.sync + fs_slice(s), (unsigned)units_per_slice, tmo, 6u + s);
+        if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_SL0 + s, (unsigned)units_per_slice, tmo, 6u + s);
         T5G_TS(5);
         fb_issue<FM_NW, 3, 5>(wd, a.Wd, a.NGd, KBd, s * per, per, j, dg, nu_d);
         fb_finish<FM_NW, EPI_F32, 3, 5, 1>(wd, j, dg, nu_d, s * per, per, a.act, f, M * f * 2, M,
@@ -760,7 +762,11 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
 
 constexpr size_t FM_LDS_MAX = 160 * 1024;
 
-int fused_mlp(const FusedMlpArgs& a_in, hipStream_t st) {
+static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launch);
+int fused_mlp(const FusedMlpArgs& a_in, hipStream_t st) { return fused_mlp_launch(a_in, st, true); }
+int fused_mlp_check(const FusedMlpArgs& a_in) { return fused_mlp_launch(a_in, nullptr, false); }
+
+static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launch) {
     FusedMlpArgs a = a_in;
     if (a.M <= 0) return 0;
     // the shapes the stages are built for: K = 2304 gate/up (72 k-steps), f = 9216 down in
@@ -803,6 +809,7 @@ int fused_mlp(const FusedMlpArgs& a_in, hipStream_t st) {
                 return -1;
             attr_b = true;
         }
+        if (!launch) return 0;
         hipLaunchKernelGGL(fused_block_kernel<true>, dim3((unsigned)nb), dim3(FM_NW * 64), shm, st, a);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
@@ -819,6 +826,7 @@ int fused_mlp(const FusedMlpArgs& a_in, hipStream_t st) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, FM_NW * 64, shm) != hipSuccess || occ < 1) return -1;
         attr[MT - 1] = true;
     }
+    if (!launch) return 0;
     hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(FM_NW * 64), shm, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -94,6 +94,7 @@ struct FusedMlpArgs {
     float* oslab;             // [4][M][d] handed off in-launch (the N2 norm's input)
 };
 int fused_mlp(const FusedMlpArgs& a, hipStream_t st);
+int fused_mlp_check(const FusedMlpArgs& a);   // 0: fused_mlp would launch these args; -1: not built for them
 // counter words of one fused launch, each on its own 128-byte line (arrivals on one line
 // serialise at ~12 ns each): N1, 8 cross-q heads, 8 attention heads, 8 cross-o groups,
 // N2, 8 down slices. The engine keeps one set per decoder layer after one line for the

@@ -16,4 +16,4 @@ run fm_write 180 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_fm/write -o pmc --
 for d in pmc_fm/fetch pmc_fm/write; do
   f=$(ls gpurun_out/$d/*counter_collection.csv 2>/dev/null | head -1); [ -n "$f" ] && mv "$f" gpurun_out/$d/pmc_counter_collection.csv
 done
-python tools/pmc_summarize.py fused_mlp gpurun_out/pmc_fm gpurun_out/r03_pmc_fused_mlp.json > gpurun_out/pmc_fm.txt 2>&1
+python tools/pmc_summarize.py fused_block gpurun_out/pmc_fm gpurun_out/r03_pmc_fused_block.json > gpurun_out/pmc_fm.txt 2>&1

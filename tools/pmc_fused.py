@@ -1,4 +1,5 @@
-"""Drive the fused decode-MLP launch (csrc/fused.hip) at C3 shape (M = 8, 2b-2b widths) over
+"""Drive the fused decode launch (csrc/fused.hip; at M = 8 the fused_block_kernel) at C3 shape
+(M = 8, T_x 60, 2b-2b widths) over
 the 26 decoder layers' weights (3.3 GB, beyond the 256 MiB Infinity Cache), as bench.py's
 roofline leg does, so rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE can count its HBM bytes per
 launch (separate passes, tools/gpu_r3_pmc.sh). GPU only."""
@@ -23,11 +24,20 @@ def main():
     sd = synthetic_weights(cfg, seed=1234, device="cuda:0")
     eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=B, max_text=64, max_audio=256, max_gen=64)
     del sd
+    # one short C3-shaped generate (T_x 60) so the engine's rows, text lengths and cross K / V
+    # are those of the bench workload
+    from t5gemma_tts_amd.engine import SamplingParams, Utterance
+    import numpy as np
+    rng = np.random.default_rng(0)
+    utts = [Utterance(x=rng.integers(3, 4000, size=60).tolist(),
+                      y=rng.integers(0, 65536, size=150).tolist() + [cfg.y_sep_token], tgt_y_len=151 + 8)
+            for _ in range(B)]
+    eng.generate(utts, SamplingParams(top_k=30, top_p=0.9, temperature=0.8), seeds=list(range(B)))
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     us = C.c_float()
     _lib.check(L.t5g_time_decode_mlp(eng.h, B, 52, st, C.byref(us)), "time_decode_mlp")
-    alg = _lib.fused_mlp_bytes(B)
-    print(f"fused_mlp avg {us.value:.2f} us/launch, algorithmic {alg} B -> {alg / us.value / 1e3:.1f} GB/s", flush=True)
+    alg = _lib.fused_block_bytes(B, 60)
+    print(f"fused_block avg {us.value:.2f} us/launch, algorithmic {alg} B -> {alg / us.value / 1e3:.1f} GB/s", flush=True)
 
 
 if __name__ == "__main__":
