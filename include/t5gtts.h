@@ -198,6 +198,9 @@ int t5g_sample_only(t5g_engine* e, int32_t B, const void* logits_dev, int32_t ld
 /* Y = X . W^T on a packed W; epi: 0 bf16, 1 +bias bf16, 2 +bias GELU(erf) bf16, 3 GeGLU(tanh), 4 fp32 slabs;
  * epi | T5G_GEMM_PREFILL selects the many-token (encoder / prefill) kernel the engine uses for those phases */
 #define T5G_GEMM_PREFILL 0x100
+/* with T5G_GEMM_PREFILL: the register-ring many-token kernel instead of the LDS-staged one
+ * (A/B probes only; the two are bitwise equal) */
+#define T5G_GEMM_PREFILL_REG 0x200
 int t5g_gemm(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K, int32_t splits,
              const void* bias_dev, void* Y_dev, int32_t ldy, int32_t epi, void* stream);
 /* Time `iters` launches of one GEMM shape with hipEvents on `stream`; launch i uses packed

@@ -77,7 +77,7 @@ struct t5g_engine {
     bool fast_sampler = true;   // false: single-block sampler only (t5g_engine_set_sampler_path)
     // decode MLP half as one persistent launch (fused.hip; t5g_engine_set_fused)
     bool fused_mlp = true;
-    float* part2 = nullptr;     // the fused block's in-launch slabs: cross-q [2][B][q_dim] | cross-o [4][B][d]
+    float* part2 = nullptr;     // the fused block's in-launch slabs: cross-q [2][B][q_dim] | cross-o [4][B][d] | down [8][B][d]
     unsigned* fsync = nullptr;  // timeout line + one counter set per decoder layer (zeroed at creation / after a timeout)
     // decode split-K factors (measured on MI355X): qkv 2, o / cross-q /
     // cross-o 4, down 8 k-slices; gate/up on the one-block-per-CU GEMV
@@ -230,7 +230,7 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->fs_ami, (int64_t)B * FS_NB);
     rc |= alloc(e, &e->fs_ticket, B);
     rc |= alloc(e, &e->fs_slow, B);
-    rc |= alloc(e, &e->part2, (int64_t)2 * B * e->q_dim + (int64_t)4 * B * d);
+    rc |= alloc(e, &e->part2, (int64_t)2 * B * e->q_dim + (int64_t)4 * B * d + (int64_t)8 * B * d);
     rc |= alloc(e, &e->fsync, (int64_t)FM_LINE + (int64_t)FM_SET_WORDS * c.n_dec_layers);
     if (rc) {
         t5g_engine_destroy(e);
@@ -242,10 +242,10 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
 
 // ---------------------------------------------------------------------------
 static int gemm(const bf16_t* X, int ldx, int M, const void* W, int N, int K, int splits, const void* bias,
-                void* Y, int ldy, int epi, hipStream_t st, bool prefill = false) {
+                void* Y, int ldy, int epi, hipStream_t st, bool prefill = false, bool pf_reg = false) {
     GemmArgs a;
     memset(&a, 0, sizeof(a));
-    a.prefill = prefill ? 1 : 0;
+    a.prefill = prefill ? (pf_reg ? 2 : 1) : 0;
     a.X = X;
     a.ldx = ldx;
     a.M = M;
@@ -493,6 +493,7 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         n.normed_out = xn;
         return resid_norm(n, st);
     };
+    bool qkv_done = false;   // the previous layer's fused block projected this layer's q|k|v
     for (int l = 0; l < c.n_dec_layers; ++l) {
         const t5g_layer_weights& L = e->dec[l];
         if (l == 0) {
@@ -785,6 +786,14 @@ static FusedMlpArgs fused_block_args(t5g_engine* e, int M, int l) {
     fa.Wo = (const bf16_t*)L.cross_o;
     fa.NGo = ng_pad(c.hidden);
     fa.oslab = e->part2 + (size_t)2 * M * e->q_dim;
+    fa.dslab = fa.oslab + (size_t)4 * M * c.hidden;
+    fa.post3_w = (const bf16_t*)L.norms[5];
+    const bool last = l == c.n_dec_layers - 1;
+    fa.pre3_w = (const bf16_t*)(last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]);
+    fa.Wqkv = last ? nullptr : (const bf16_t*)e->dec[l + 1].qkv;
+    fa.NGqkv = ng_pad(e->qkv_dim);
+    fa.qkv_dim = e->qkv_dim;
+    fa.qkv_out = e->part;
     return fa;
 }
 
@@ -855,6 +864,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         r.ldq = e->q_dim;
         return r;
     };
+    bool qkv_done = false;   // the previous layer's fused block projected this layer's q|k|v
     for (int l = 0; l < c.n_dec_layers; ++l) {
         const t5g_layer_weights& L = e->dec[l];
         if (l == 0) {
@@ -877,8 +887,23 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         // --- self attention
         const int win = c.dec_sliding[l] ? c.sliding_window : 0;
         if (decode && !eager) {
-            // q|k|v as fp32 split-K slabs; q rotated, k rotated + appended inside attention
-            RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, s_qkv, nullptr, e->part, e->qkv_dim, EPI_F32, st));
+            // q|k|v as fp32 split-K slabs; q rotated, k rotated + appended inside attention.
+            // At the 2b-2b width: the 12-wave register-X GEMV over 2 k-slices (the fused
+            // block's QKV stage, which produced them already when qkv_done)
+            if (!qkv_done) {
+                int rcq = -1;
+                if (M <= 32 && d == 2304 && s_qkv == 2) {
+                    DecGemmArgs g = dec_args(M, L.qkv, e->qkv_dim, d, e->part, e->qkv_dim, 12);
+                    g.X = xn;
+                    g.ldx = d;
+                    g.splits = 2;
+                    g.layout_rx = 1;
+                    rcq = gemv_dec(g, EPI_F32, st);
+                    if (rcq != 0 && rcq != -1) RC(rcq);
+                }
+                if (rcq != 0) RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, s_qkv, nullptr, e->part, e->qkv_dim, EPI_F32, st));
+            }
+            qkv_done = false;
             RC(decode_attention(e, M, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1, win, 0, true, pos, tab, s_qkv,
                                 e->qkv_dim, st));
         } else {
@@ -903,8 +928,8 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         if (decode && e->fused_mlp && !eager && M <= 16 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 &&
             e->q_dim == 2048 && c.n_dec_layers >= 2) {
             const int rc = fused_mlp(fused_block_args(e, M, l), st);
-            if (rc == 0) {
-                RC(resid(s_down, L.norms[5], last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]));
+            if (rc == 0) {   // also ran the layer's last norm and the next layer's q|k|v projection
+                qkv_done = !last;
                 continue;
             }
             if (rc != -1) RC(rc);   // -1: a shape / device the launch is not built for
@@ -1301,8 +1326,9 @@ extern "C" int t5g_sample_only(t5g_engine* e, int32_t B, const void* logits, int
 extern "C" int t5g_gemm(const void* X, int32_t ldx, int32_t M, const void* Wp, int32_t N, int32_t K, int32_t splits,
                         const void* bias, void* Y, int32_t ldy, int32_t epi, void* stream) {
     if (!X || !Wp || !Y || M <= 0 || N <= 0 || K % 32) return T5G_EINVAL;
-    const bool prefill = (epi & T5G_GEMM_PREFILL) != 0;
-    RC(gemm((const bf16_t*)X, ldx, M, Wp, N, K, splits, bias, Y, ldy, epi & 0xff, (hipStream_t)stream, prefill));
+    const bool prefill = (epi & T5G_GEMM_PREFILL) != 0, pf_reg = (epi & T5G_GEMM_PREFILL_REG) != 0;
+    RC(gemm((const bf16_t*)X, ldx, M, Wp, N, K, splits, bias, Y, ldy, epi & 0xff, (hipStream_t)stream, prefill,
+            pf_reg));
     return T5G_OK;
 }
 
@@ -1316,12 +1342,12 @@ extern "C" int t5g_time_gemm(const void* X, int32_t ldx, int32_t M, const void* 
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    const bool pf = (epi & T5G_GEMM_PREFILL) != 0;
+    const bool pf = (epi & T5G_GEMM_PREFILL) != 0, pf_reg = (epi & T5G_GEMM_PREFILL_REG) != 0;
     epi &= 0xff;
-    RC(gemm((const bf16_t*)X, ldx, M, Wp_list[0], N, K, splits, nullptr, Y, ldy, epi, st, pf));  // warm
+    RC(gemm((const bf16_t*)X, ldx, M, Wp_list[0], N, K, splits, nullptr, Y, ldy, epi, st, pf, pf_reg));  // warm
     HIPCHK(hipEventRecord(e0, st));
     for (int i = 0; i < iters; ++i)
-        RC(gemm((const bf16_t*)X, ldx, M, Wp_list[i % n_w], N, K, splits, nullptr, Y, ldy, epi, st, pf));
+        RC(gemm((const bf16_t*)X, ldx, M, Wp_list[i % n_w], N, K, splits, nullptr, Y, ldy, epi, st, pf, pf_reg));
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;

@@ -42,8 +42,8 @@ constexpr int FM_NORM_UNITS = 3;  // gate/up units of a norm workgroup (tools/di
 constexpr unsigned FM_SPIN_MAX = 1u << 18;   // ~0.3-0.5 s of polling before a wait gives up
 
 // lines of a counter set (FusedMlpArgs::sync), one word per 128-byte line
-constexpr int L_N1 = 0, L_Q0 = 1, L_A0 = 9, L_O0 = 17, L_N2 = 25, L_SL0 = 26;
-static_assert(L_SL0 + FM_DS == FM_SET_LINES, "counter set layout");
+constexpr int L_N1 = 0, L_Q0 = 1, L_A0 = 9, L_O0 = 17, L_N2 = 25, L_SL0 = 26, L_D0 = 34, L_N3 = 42;
+static_assert(L_N3 + 1 == FM_SET_LINES, "counter set layout");
 __device__ __forceinline__ unsigned* cline(unsigned* set, int line) { return set + line * FM_LINE; }
 constexpr int FS_NORM = L_N2 * FM_LINE;
 __device__ __forceinline__ int fs_slice(int s) { return (L_SL0 + s) * FM_LINE; }
@@ -60,6 +60,27 @@ __device__ __forceinline__ bool fm_wait_n(unsigned* set, int line0, unsigned tar
     static_assert(N >= 1 && N < 64, "lines per poll");
     const int lane = threadIdx.x & 63;
     unsigned* p = lane == 63 ? tmo : set + (line0 + min(lane, N - 1)) * FM_LINE;
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned v = ld_rlx(p);
+        if (__all(lane == 63 || v >= target)) return true;
+        if (__shfl(v, 63, 64) != 0) return false;
+        if (spins > FM_SPIN_MAX) {
+            if (lane == 0) __hip_atomic_store(tmo, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// the same over 8 lines that share `total` arrivals round-robin (arrival k goes to line
+// k % 8): line i waits for (total - i + 7) / 8
+template <int N>
+__device__ __forceinline__ bool fm_wait_split(unsigned* set, int line0, unsigned total, unsigned* tmo, unsigned code) {
+    static_assert(N >= 1 && N < 64, "lines per poll");
+    const int lane = threadIdx.x & 63;
+    const int li = min(lane, N - 1);
+    unsigned* p = lane == 63 ? tmo : set + (line0 + li) * FM_LINE;
+    const unsigned target = (total + (unsigned)(N - 1 - li)) / (unsigned)N;
     for (unsigned spins = 0;; ++spins) {
         const unsigned v = ld_rlx(p);
         if (__all(lane == 63 || v >= target)) return true;
@@ -457,7 +478,7 @@ __device__ __forceinline__ void fb_finish(bf16x8_s (&w)[UMAX][SPU], int g0, int 
 // resid_norm_kernel<4, 2>'s arithmetic for row m: v = bf16(sum of the 4 slabs),
 // post-norm, h = bf16(r + v) (r8: the residual in, the new residual out, in registers),
 // xn = pre-norm(h) stored write-through. Slabs read plain (previous launch) or sc1.
-template <bool SC1>
+template <int NS, bool SC1>
 __device__ __forceinline__ void fb_norm(const float* part, int M, int m, int d, const bf16_t* post_w,
                                         const bf16_t* pre_w, float eps, float (&r8)[8], bf16_t* xn, float* red) {
     const int c = threadIdx.x;
@@ -465,10 +486,10 @@ __device__ __forceinline__ void fb_norm(const float* part, int M, int m, int d, 
     const int cc = active ? c : d / 8 - 1;
     const u32x4 w_post = *(const u32x4*)(post_w + 8 * cc);
     const u32x4 w_pre = *(const u32x4*)(pre_w + 8 * cc);
-    f32x4 p[FM_NS][2];
-    const __amdgpu_buffer_rsrc_t pr = raw_rsrc(part, (uint32_t)(FM_NS * M * d * 4));
+    f32x4 p[NS][2];
+    const __amdgpu_buffer_rsrc_t pr = raw_rsrc(part, (uint32_t)(NS * M * d * 4));
 #pragma unroll
-    for (int s = 0; s < FM_NS; ++s) {
+    for (int s = 0; s < NS; ++s) {
         const int o = ((s * M + m) * d + 8 * cc) * 4;
         if constexpr (SC1) {
             p[s][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, o, 0, AUX_SC1));
@@ -481,7 +502,7 @@ __device__ __forceinline__ void fb_norm(const float* part, int M, int m, int d, 
     }
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < FM_NS; ++s) {
+    for (int s = 0; s < NS; ++s) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             v[j] += p[s][0][j];
@@ -524,6 +545,8 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     f32x4* red = (f32x4*)smem;                                   // GEMV partial sums, <= 60 KB
     FbAttnLds& al = *(FbAttnLds*)(smem + 5 * FM_NW * 1024);      // attention scratch
     float* nred = (float*)(smem + 5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16);   // norm: 2 x 32 floats
+    // a norm workgroup's residual row between N1, N2 and N3 (bf16, exact: every h is rounded)
+    u32x4* hrow = (u32x4*)(smem + 5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16 + 64 * sizeof(float));
     unsigned* tmo = a.timeout;
     const int bu = (int)blockIdx.x, nb = (int)gridDim.x;
     const int tq = (int)threadIdx.x, wave = tq >> 6, lane = tq & 63;
@@ -569,32 +592,68 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         }
     }
 
-    // ---- N1
-    float hreg[8];
+    // ---- the norm workgroups (the last M): N1, N2, N3 for their row and nothing else, so no
+    // weight stream of their own ever queues ahead of a norm on the critical path
+    const int nw = nb - M;   // GEMV / attention workers
     if (normwg) {
-        const int cc = min(tq, d / 8 - 1);
-        unpack8f(*(const u32x4*)(a.h + (long)nrow * d + 8 * cc), hreg);
-        fb_norm<false>(a.o_slabs, M, nrow, d, a.post1_w, a.pre1_w, a.eps, hreg, a.xn1, nred);
-        fb_publish(cline(a.sync, L_N1), 1u);
+        {
+            float hreg[8];
+            const int cc = min(tq, d / 8 - 1);
+            unpack8f(*(const u32x4*)(a.h + (long)nrow * d + 8 * cc), hreg);
+            fb_norm<FM_NS, false>(a.o_slabs, M, nrow, d, a.post1_w, a.pre1_w, a.eps, hreg, a.xn1, nred);
+            if (tq < d / 8) hrow[tq] = pack8f(hreg);
+            fb_publish(cline(a.sync, L_N1), 1u);
+        }
+        {
+            if (wave == 0) ok &= fm_wait_split<8>(a.sync, L_O0, (unsigned)(4 * (nw / 4)), tmo, 4u);
+            wg_barrier();
+            float r2[8];
+            unpack8f(hrow[min(tq, d / 8 - 1)], r2);
+            fb_norm<FM_NS, true>(a.oslab, M, nrow, d, a.post_w, a.pre_w, a.eps, r2, a.xn, nred);
+            if (tq < d / 8) hrow[tq] = pack8f(r2);
+            fb_publish(cline(a.sync, L_N2), 1u);
+        }
+        {
+            if (wave == 0) ok &= fm_wait_split<8>(a.sync, L_D0, (unsigned)(FM_DS * (nw / FM_DS)), tmo, 14u);
+            wg_barrier();
+            float r3[8];
+            unpack8f(hrow[min(tq, d / 8 - 1)], r3);
+            fb_norm<FM_DS, true>(a.dslab, M, nrow, d, a.post3_w, a.pre3_w, a.eps, r3, a.xn, nred);
+            if (tq < d / 8) *(u32x4*)(a.h + (long)nrow * d + 8 * tq) = pack8f(r3);   // read by the next launch
+            fb_publish(cline(a.sync, L_N3), 1u);
+        }
+        T5G_TS(6);
+        return;
     }
+    const int w = bu;   // worker index
 
-    // ---- Q: cross-q unit-slice bu (unit bu % NGq, k-slice bu / NGq)
+    // ---- Q: cross-q, 2 k-slices of 36 k-steps over nw / 2 workers each (<= 2 units)
     {
-        const int uq = bu % a.NGq, sq = bu / a.NGq;
-        bf16x8_s wq[1][3];
-        if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N1, (unsigned)M, tmo, 1u);
-        T5G_TS(1);
-        fb_issue<FM_NW, 3, 1>(wq, a.Wq, a.NGq, d / 32, sq * 36, 36, uq, 1, 1);
-        fb_finish<FM_NW, EPI_F32, 3, 1, 2>(wq, uq, 1, 1, sq * 36, 36, a.xn1, d, M * d * 2, M,
-                                           a.qslab + (long)sq * M * a.q_dim, a.q_dim, M * a.q_dim * 4, a.q_dim, red);
-        fb_publish(cline(a.sync, L_Q0 + uq / (D / 16)), 1u);
+        const int qper = nw / 2, sq = w / qper, jq = w - sq * qper;
+        if (sq < 2) {
+            const int nu_q = (a.NGq - jq + qper - 1) / qper;
+            bf16x8_s wq[2][3];
+            if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N1, (unsigned)M, tmo, 1u);
+            T5G_TS(1);
+            fb_issue<FM_NW, 3, 2>(wq, a.Wq, a.NGq, d / 32, sq * 36, 36, jq, qper, nu_q);
+            fb_finish<FM_NW, EPI_F32, 3, 2, 2>(wq, jq, qper, nu_q, sq * 36, 36, a.xn1, d, M * d * 2, M,
+                                               a.qslab + (long)sq * M * a.q_dim, a.q_dim, M * a.q_dim * 4, a.q_dim,
+                                               red);
+            drain_vm();
+            __syncthreads();
+            if (tq == 0)
+                for (int i = 0; i < nu_q; ++i)
+                    __hip_atomic_fetch_add(cline(a.sync, L_Q0 + (jq + i * qper) / (D / 16)), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 
-    // ---- A (attention workgroups) with O's weight requests around it
-    const int so = bu / (nb / 4), jo = bu - so * (nb / 4), go = nb / 4;
-    const int nu_o = (a.NGo - jo + go - 1) / go;
+    // ---- A (attention workers) with O's weight requests around it
+    const int oper = nw / 4, so = w / oper, jo = w - so * oper;
+    const bool owork = so < 4;
+    const int nu_o = owork ? (a.NGo - jo + oper - 1) / oper : 0;
     bf16x8_s wo[3][2];
-    if (attnwg && wave >= 4) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, go, nu_o);
+    if (attnwg && wave >= 4 && owork) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, oper, nu_o);
     if (attnwg) {
         const int qcnt = 2 * (D / 16);   // 16 q units per head x 2 k-slices
         if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_Q0 + ah, (unsigned)qcnt, tmo, 2u);
@@ -700,29 +759,21 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         fb_publish(cline(a.sync, L_A0 + ah), 1u);
     }
 
-    // ---- O: cross-o unit-slices (4 k-slices of 16 k-steps, 8 waves)
-    if (wave == 0) ok &= fm_wait_n<8>(a.sync, L_A0, (unsigned)M, tmo, 3u);   // the 8 q heads
-    T5G_TS(2);
-    if (!(attnwg && wave >= 4)) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, go, nu_o);
-    fb_finish<8, EPI_F32, 2, 3, 2>(wo, jo, go, nu_o, so * 16, 16, a.att, a.q_dim, M * a.q_dim * 2, M,
-                                   a.oslab + (long)so * M * d, d, M * d * 4, d, red);
-    fb_publish(cline(a.sync, L_O0 + (bu & 7)), 1u);
-
-    // ---- N2 (norm workgroups, before their gate/up requests)
-    if (normwg) {
-        if (wave == 0) ok &= fm_wait_n<8>(a.sync, L_O0, (unsigned)(nb / 8), tmo, 4u);
-        wg_barrier();
-        fb_norm<true>(a.oslab, M, nrow, d, a.post_w, a.pre_w, a.eps, hreg, a.xn, nred);
-        if (tq < d / 8) *(u32x4*)(a.h + (long)nrow * d + 8 * tq) = pack8f(hreg);   // read by the next launch
-        fb_publish(cline(a.sync, L_N2), 1u);
+    // ---- O: cross-o, 4 k-slices of 16 k-steps over nw / 4 workers each (<= 3 units, 8 waves)
+    if (owork) {
+        if (wave == 0) ok &= fm_wait_n<8>(a.sync, L_A0, (unsigned)M, tmo, 3u);   // the 8 q heads
+        T5G_TS(2);
+        if (!(attnwg && wave >= 4)) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, oper, nu_o);
+        fb_finish<8, EPI_F32, 2, 3, 2>(wo, jo, oper, nu_o, so * 16, 16, a.att, a.q_dim, M * a.q_dim * 2, M,
+                                       a.oslab + (long)so * M * d, d, M * d * 4, d, red);
+        fb_publish(cline(a.sync, L_O0 + (w & 7)), 1u);
     }
 
-    // ---- G: gate/up (contiguous unit runs, as fused_mlp_kernel)
+    // ---- G: gate/up, contiguous unit runs over the workers (<= 5 units)
     const int KBg = d / 32, NGg = a.NGgu;
-    const int nr = nb - M, rest = NGg - M * FM_NORM_UNITS;
-    const int ubase = rest / nr, uextra = rest - ubase * nr;
-    const int nu_g = bu < nr ? ubase + (bu < uextra ? 1 : 0) : FM_NORM_UNITS;
-    const int g_lo = bu < nr ? bu * ubase + min(bu, uextra) : rest + (bu - nr) * FM_NORM_UNITS;
+    const int ubase = NGg / nw, uextra = NGg - ubase * nw;
+    const int nu_g = ubase + (w < uextra ? 1 : 0);
+    const int g_lo = w * ubase + min(w, uextra);
     {
         bf16x8_s wg[5][6];
         if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N2, (unsigned)M, tmo, 5u);
@@ -743,18 +794,32 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         }
     }
 
-    // ---- D: down slices (as fused_mlp_kernel)
-    const int dg = nb / FM_DS;
-    const int s = bu / dg, j = bu - s * dg;
+    // ---- D: down, 8 k-slices of 36 k-steps over nw / 8 workers each (<= 5 units)
+    const int dper = nw / FM_DS, s = w / dper, j = w - s * dper;
     if (s < FM_DS) {
         const int KBd = f / 32, per = KBd / FM_DS;
-        const int nu_d = (a.NGd - j + dg - 1) / dg;
+        const int nu_d = (a.NGd - j + dper - 1) / dper;
         bf16x8_s wd[5][3];
         if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_SL0 + s, (unsigned)units_per_slice, tmo, 6u + s);
         T5G_TS(5);
-        fb_issue<FM_NW, 3, 5>(wd, a.Wd, a.NGd, KBd, s * per, per, j, dg, nu_d);
-        fb_finish<FM_NW, EPI_F32, 3, 5, 1>(wd, j, dg, nu_d, s * per, per, a.act, f, M * f * 2, M,
-                                           a.part_out + (long)s * M * d, d, 0, d, red);
+        fb_issue<FM_NW, 3, 5>(wd, a.Wd, a.NGd, KBd, s * per, per, j, dper, nu_d);
+        fb_finish<FM_NW, EPI_F32, 3, 5, 2>(wd, j, dper, nu_d, s * per, per, a.act, f, M * f * 2, M,
+                                           a.dslab + (long)s * M * d, d, M * d * 4, d, red);
+        fb_publish(cline(a.sync, L_D0 + (w & 7)), 1u);
+    }
+
+    // ---- QKV: the next layer's q|k|v, 2 k-slices of 36 k-steps over nw / 2 workers each
+    // (<= 3 units), weights requested while N3 runs
+    if (a.Wqkv) {
+        const int kper = nw / 2, sk = w / kper, jk = w - sk * kper;
+        if (sk < 2) {
+            const int nu_k = (a.NGqkv - jk + kper - 1) / kper;
+            bf16x8_s wk[3][3];
+            fb_issue<FM_NW, 3, 3>(wk, a.Wqkv, a.NGqkv, d / 32, sk * 36, 36, jk, kper, nu_k);
+            if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N3, (unsigned)M, tmo, 15u);
+            fb_finish<FM_NW, EPI_F32, 3, 3, 1>(wk, jk, kper, nu_k, sk * 36, 36, a.xn, d, M * d * 2, M,
+                                               a.qkv_out + (long)sk * M * a.qkv_dim, a.qkv_dim, 0, a.qkv_dim, red);
+        }
     }
     (void)ok;
     T5G_TS(6);
@@ -791,14 +856,20 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
         // the cross-attention chain: 2 k-slices x NGq cross-q units = one unit-slice per
         // workgroup, 4 x 64 cross-o workgroups, 8 x 32 down workgroups; one 64-key chunk of
         // text keys; attention and norm workgroups disjoint
-        if (MT != 1 || nb != 2 * a.NGq || nb % 32 || a.D != 256 || a.Hq * a.D != a.q_dim || a.Hq % a.Hkv ||
-            a.NGq * 16 != a.q_dim || a.NGo * 16 != a.d || a.kv_cap > 64 || a.M * a.Hq > nb - a.M || !a.o_slabs ||
+        const int nw = nb - a.M;   // workers (the last M workgroups run the norms)
+        auto most = [](int units, int per) { return per > 0 ? (units + per - 1) / per : 1 << 20; };
+        if (MT != 1 || most(a.NGq, nw / 2) > 2 || most(a.NGo, nw / 4) > 3 || most(a.NGd, nw / FM_DS) > 5 ||
+            most(a.NGgu, nw) > 5 || (a.Wqkv && most(a.NGqkv, nw / 2) > 3))
+            return -1;
+        if (a.D != 256 || a.Hq * a.D != a.q_dim || a.Hq % a.Hkv || a.Hq > 8 ||
+            a.NGq * 16 != a.q_dim || a.NGo * 16 != a.d || a.kv_cap > 64 || a.M * a.Hq > nw || !a.o_slabs ||
             !a.post1_w || !a.pre1_w || !a.xn1 || !a.Wq || !a.qslab || !a.ck || !a.cv || !a.enc_len || !a.rope_tab ||
             !a.att || !a.Wo || !a.oslab)
             return -1;
-        if ((a.NGo + nb / 4 - 1) / (nb / 4) > 3) return -1;
+        if (!a.dslab || !a.post3_w || !a.pre3_w) return -1;
+        if (a.Wqkv && (!a.qkv_out || a.NGqkv * 16 != a.qkv_dim)) return -1;
         a.norm_b0 = nb - a.M;
-        const size_t shm = (size_t)5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16 + 64 * sizeof(float);
+        const size_t shm = (size_t)5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16 + 64 * sizeof(float) + (size_t)a.d * 2;
         static bool attr_b = false;
         if (!attr_b) {
             (void)hipFuncSetAttribute((const void*)fused_block_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,

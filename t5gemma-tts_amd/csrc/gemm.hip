@@ -339,6 +339,63 @@ static int launch_epi(const GemmArgs& a, int epi, int mblocks, hipStream_t st) {
 #ifndef PF_STAGES
 #define PF_STAGES 4
 #endif
+#ifndef PFL_NBUF
+#define PFL_NBUF 4
+#endif
+// prefill epilogue: lane l holds outputs 4*(l>>4)..+3 of each of the wave's 4 row groups
+// (from g0) for token l&15 of each of its 4 token tiles (from mb)
+template <int EPI>
+__device__ __forceinline__ void pf_epilogue(const GemmArgs& a, const f32x4 (&acc)[4][4], int g0, int mb, int lane) {
+    constexpr bool GLU = EPI == EPI_GEGLU;
+    const int n_out = GLU ? a.N / 2 : a.N;
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+        const int g = g0 + rg;
+        if (g >= a.NG) break;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const int m = mb + mt * 16 + (lane & 15);
+            float v[4];
+            int n0;
+            if constexpr (GLU) {
+                // 8 gate rows then the same 8 features' up rows: the up sums sit 32 lanes up
+                f32x4 up;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) up[r] = __shfl_down(acc[rg][mt][r], 32, 64);
+                if (lane >= 32) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_tanh(rbf(acc[rg][mt][r]))) * rbf(up[r]);
+                n0 = g * 8 + 4 * (lane >> 4);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = acc[rg][mt][r];
+                n0 = g * 16 + 4 * (lane >> 4);
+            }
+            if (m >= a.M) continue;
+            bf16_t o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float x = v[r];
+                if constexpr (EPI == EPI_BIAS_BF16 || EPI == EPI_BIAS_GELU) {
+                    if (n0 + r < n_out) x = x + bf2f(a.bias[n0 + r]);
+                }
+                if constexpr (EPI == EPI_BIAS_GELU) x = gelu_erf(rbf(x));
+                o[r] = f2bf(x);
+            }
+            bf16_t* y = (bf16_t*)a.Y + (long)m * a.ldy;
+            if (n0 + 3 < n_out && (a.ldy & 3) == 0) {
+                uint2 w2;
+                w2.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+                w2.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+                *(uint2*)(y + n0) = w2;
+            } else {
+                for (int r = 0; r < 4; ++r)
+                    if (n0 + r < n_out) y[n0 + r] = o[r];
+            }
+        }
+    }
+}
+
 template <int EPI, int S>
 __global__ __launch_bounds__(256) void gemm_pf_kernel(GemmArgs a) {
     static_assert(S % 2 == 0, "even ring: stage parity = k-step parity");
@@ -392,55 +449,104 @@ __global__ __launch_bounds__(256) void gemm_pf_kernel(GemmArgs a) {
     for (int rg = 0; rg < 4; ++rg)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) acc[rg][mt] += acc2[rg][mt];
-    // epilogue: lane l holds outputs 4*(l>>4)..+3 of each row group for token l&15
-    constexpr bool GLU = EPI == EPI_GEGLU;
-    const int n_out = GLU ? a.N / 2 : a.N;
+    pf_epilogue<EPI>(a, acc, g0, mb, lane);
+}
+
+// LDS-staged form of the same tile (round 3): each k-step's 8 weight and 8 activation
+// fragments of the block (16 KiB) are moved by buffer_load ... lds (no VGPR round trip,
+// range-checked like the register form) into a ring of NBUF LDS stages, one fragment per
+// wave instruction in MFMA operand lane order, so every wave reads its 4 + 4 fragments back
+// with conflict-free ds_read_b128; NBUF - 1 k-steps are in flight, one counted vmcnt and
+// one barrier per k-step. Fragments are fetched once per block instead of once per wave
+// pair, which is what bounded the register form (load issue, not MFMA). The two
+// accumulator chains and every sum are those of gemm_pf_kernel: outputs bitwise equal.
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" : : "n"(N) : "memory");
+}
+template <int EPI, int NBUF>
+__global__ __launch_bounds__(256, 2) void gemm_pfl_kernel(GemmArgs a) {
+    constexpr int P = NBUF - 1;   // k-steps in flight
+    extern __shared__ __attribute__((aligned(16))) char smem[];   // [NBUF][16 fragments][1 KiB]
+    // wave-uniform in a scalar register: the LDS destination of buffer_load ... lds (M0) must
+    // be, or the compiler wraps every load in a waterfall loop
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int gb = blockIdx.x * 8;                          // first row group of the block
+    const int tb = blockIdx.y * 128;                        // first token of the block
+    const int KB = a.KB;
+    const __amdgpu_buffer_rsrc_t wrs = frag_rsrc(a.W, (uint32_t)a.NG * (uint32_t)KB * 1024u);
+    const __amdgpu_buffer_rsrc_t xrs = frag_rsrc(a.X, (uint32_t)a.M * (uint32_t)a.ldx * 2u);
+    // fragments 4 * wave .. + 3 of every stage: 0-7 the block's row groups, 8-15 its token tiles
+    const int xk = 8 * (lane >> 4);
+    int src[4];
 #pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-        const int g = g0 + rg;
-        if (g >= a.NG) break;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const int m = mb + mt * 16 + (lane & 15);
-            float v[4];
-            int n0;
-            if constexpr (GLU) {
-                // 8 gate rows then the same 8 features' up rows: the up sums sit 32 lanes up
-                f32x4 up;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) up[r] = __shfl_down(acc[rg][mt][r], 32, 64);
-                if (lane >= 32) continue;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = rbf(gelu_tanh(rbf(acc[rg][mt][r]))) * rbf(up[r]);
-                n0 = g * 8 + 4 * (lane >> 4);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = acc[rg][mt][r];
-                n0 = g * 16 + 4 * (lane >> 4);
-            }
-            if (m >= a.M) continue;
-            bf16_t o[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float x = v[r];
-                if constexpr (EPI == EPI_BIAS_BF16 || EPI == EPI_BIAS_GELU) {
-                    if (n0 + r < n_out) x = x + bf2f(a.bias[n0 + r]);
-                }
-                if constexpr (EPI == EPI_BIAS_GELU) x = gelu_erf(rbf(x));
-                o[r] = f2bf(x);
-            }
-            bf16_t* y = (bf16_t*)a.Y + (long)m * a.ldy;
-            if (n0 + 3 < n_out && (a.ldy & 3) == 0) {
-                uint2 w2;
-                w2.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
-                w2.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
-                *(uint2*)(y + n0) = w2;
-            } else {
-                for (int r = 0; r < 4; ++r)
-                    if (n0 + r < n_out) y[n0 + r] = o[r];
-            }
-        }
+    for (int q = 0; q < 4; ++q) {
+        const int f = 4 * wave + q;
+        src[q] = f < 8 ? ((gb + f) * KB * 64 + lane) * 16                       // + kb * 1024
+                       : ((tb + (f - 8) * 16 + (lane & 15)) * a.ldx + xk) * 2;    // + kb * 64; rows >= M: out of range
     }
+    auto stage = [&](int kb) __attribute__((always_inline)) {
+        __attribute__((address_space(3))) char* base =
+            (__attribute__((address_space(3))) char*)smem + (kb % NBUF) * 16384 + 4 * wave * 1024;
+        const bool live = kb < KB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (4 * wave + q < 8)   // wave-uniform: waves 0-1 stage weights, 2-3 activations
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, base + q * 1024, 16,
+                                                         live ? src[q] + kb * 1024 : (int)0xfffffff0u, 0, 0, 0);
+            else
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, base + q * 1024, 16,
+                                                         live ? src[q] + kb * 64 : (int)0xfffffff0u, 0, 0, 0);
+        }
+    };
+    f32x4 acc[4][4], acc2[4][4];
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[rg][mt] = acc2[rg][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < P; ++p) stage(p);
+    auto kstep = [&](int kb, f32x4(&c)[4][4]) __attribute__((always_inline)) {
+        // this wave's fragments of k-step kb have landed (the P - 1 later stages may still be
+        // in flight); after the barrier every wave's have, and nobody reads stage kb - 1 any more
+        wait_vm_barrier<4 * (P - 1)>();
+        stage(kb + P);
+        const char* buf = smem + (kb % NBUF) * 16384 + lane * 16;
+        bf16x8_s w[4], x[4];
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) w[rg] = *(const bf16x8_s*)(buf + (wr * 4 + rg) * 1024);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) x[mt] = *(const bf16x8_s*)(buf + (8 + wc * 4 + mt) * 1024);
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) c[rg][mt] = mfma16(w[rg], x[mt], c[rg][mt]);
+    };
+    // even k-steps into acc, odd into acc2 (gemm_pf_kernel's two chains)
+    for (int kb = 0; kb < KB; kb += 2) {   // KB even (gemm_prefill)
+        kstep(kb, acc);
+        kstep(kb + 1, acc2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's out-of-range stages
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[rg][mt] += acc2[rg][mt];
+    pf_epilogue<EPI>(a, acc, gb + wr * 4, tb + wc * 64, lane);
+}
+
+template <int NBUF>
+static int launch_pfl(const GemmArgs& a, int epi, dim3 grid, hipStream_t st) {
+    const size_t shm = (size_t)NBUF * 16384;
+    switch (epi) {
+        case EPI_BF16: hipLaunchKernelGGL((gemm_pfl_kernel<EPI_BF16, NBUF>), grid, dim3(256), shm, st, a); break;
+        case EPI_BIAS_BF16: hipLaunchKernelGGL((gemm_pfl_kernel<EPI_BIAS_BF16, NBUF>), grid, dim3(256), shm, st, a); break;
+        case EPI_BIAS_GELU: hipLaunchKernelGGL((gemm_pfl_kernel<EPI_BIAS_GELU, NBUF>), grid, dim3(256), shm, st, a); break;
+        case EPI_GEGLU: hipLaunchKernelGGL((gemm_pfl_kernel<EPI_GEGLU, NBUF>), grid, dim3(256), shm, st, a); break;
+        default: return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 template <int S>
@@ -458,6 +564,8 @@ static int launch_pf(const GemmArgs& a, int epi, dim3 grid, hipStream_t st) {
 static int gemm_prefill(const GemmArgs& a, int epi, hipStream_t st) {
     if ((long)a.M * a.ldx * 2 >= 0x7fffffffL || (long)a.NG * a.KB * 1024 >= 0x7fffffffL) return -1;
     const dim3 grid((unsigned)((a.NG + 7) / 8), (unsigned)((a.M + 127) / 128));
+    // prefill == 1: the LDS-staged kernel; 2: the register-ring kernel (A/B, tools/probe_pf_lds.py)
+    if (a.prefill == 1 && a.ldx % 8 == 0 && a.KB % 2 == 0) return launch_pfl<PFL_NBUF>(a, epi, grid, st);
     // ring depth: PF_STAGES k-steps when they divide KB (no partial ring turn), else 2
     if (a.KB % PF_STAGES == 0) return launch_pf<PF_STAGES>(a, epi, grid, st);
     return launch_pf<2>(a, epi, grid, st);

@@ -92,14 +92,24 @@ struct FusedMlpArgs {
     const bf16_t* Wo;         // packed cross o_proj, NGo row groups, K = q_dim
     int NGo;
     float* oslab;             // [4][M][d] handed off in-launch (the N2 norm's input)
+    // ---- the layer's last norm and the next layer's q|k|v projection at the end (xattn):
+    //   D writes its slabs to dslab (in-launch), N3: h = h + RMSNorm_post3(down slabs),
+    //   xn = RMSNorm_pre3(h) (the next layer's pre_self_attn or the final norm), then, unless
+    //   Wqkv is null (last layer), QKV: fp32 slabs [2][M][qkv_dim] -> qkv_out (next launch)
+    float* dslab;             // [8][M][d]
+    const bf16_t* post3_w;    // post_feedforward_layernorm
+    const bf16_t* pre3_w;     // next layer's pre_self_attn_layernorm, or the final norm
+    const bf16_t* Wqkv;       // next layer's packed q|k|v (NGqkv row groups, K = d), or null
+    int NGqkv, qkv_dim;
+    float* qkv_out;           // [2][M][qkv_dim]
 };
 int fused_mlp(const FusedMlpArgs& a, hipStream_t st);
 int fused_mlp_check(const FusedMlpArgs& a);   // 0: fused_mlp would launch these args; -1: not built for them
 // counter words of one fused launch, each on its own 128-byte line (arrivals on one line
 // serialise at ~12 ns each): N1, 8 cross-q heads, 8 attention heads, 8 cross-o groups,
-// N2, 8 down slices. The engine keeps one set per decoder layer after one line for the
-// timeout word.
-constexpr int FM_LINE = 32, FM_SET_LINES = 34, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
+// N2, 8 down slices, 8 down groups, N3. The engine keeps one set per decoder layer after
+// one line for the timeout word.
+constexpr int FM_LINE = 32, FM_SET_LINES = 43, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
 
 // ---- row-wise residual / RMSNorm / embedding -------------------------------
 struct NormArgs {

@@ -65,7 +65,7 @@ def main():
         pc = np.percentile(e, [0, 10, 50, 90, 100]).astype(int)
         print(f"  {k} {names[k]:24s} from first start: min {pc[0]} p10 {pc[1]} p50 {pc[2]} p90 {pc[3]} "
               f"max {pc[4]} ns [{int(ok.sum())}]")
-        if norm.any() and (k > 1 or B <= 16):
+        if (norm & ok).any() and (k > 1 or B <= 16):
             en = (v[norm & ok] - base) * 10
             print(f"      norm workgroups: p50 {int(np.median(en))} max {int(en.max())} ns")
     xcc = (rows[:, 7] >> 32) & 0xf

@@ -1,0 +1,8 @@
+# Dedicated-norm fused block + LDS-staged prefill GEMM: tests, timeline, prefill A/B, bench.
+source tools/gpu_run.sh
+export TMPDIR=/tmp
+run t_fused 400 python -u -m pytest tests/test_gpu_fused.py -x -v --timeout 300 --timeout-method thread
+grep -q " passed" gpurun_out/t_fused.log || exit 1
+run pf_lds 300 python tools/probe_pf_lds.py
+T5G_LIB=$PWD/t5gemma-tts_amd/lib/libt5gtts_dbg.so run diag 300 python tools/diag_fused.py 8
+run bench_f 400 python bench.py --no-cpu-baseline

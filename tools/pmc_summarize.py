@@ -23,12 +23,12 @@ OPS = {
                           "(tools/pmc_fused.py: 26 layers' weights rotated, 3.3 GB > 256 MiB Infinity Cache); "
                           "algorithmic = weights + cross-o slabs, h, norm weights in + h, down slabs out"},
     "fused_block": {"kernels": ["fused_block_kernel"],
-                    "algorithmic": 2 * 2048 * 2304 * 2 + 2 * 9216 * 2304 * 2 + 2304 * 9216 * 2 + 4 * 8 * 2304 * 4
-                    + 8 * 2304 * 2 + 4 * 2304 * 2 + 8 * 60 * 2 * 1024 * 2 + 8 * 256 * 4 + 8 * 2304 * 2 + 8 * 8 * 2304 * 4,
+                    "algorithmic": None,   # _lib.fused_block_bytes(8, 60): the average over a step's 26 layers
                     "what": "fused decode block after the self-attention o-projection (norm -> cross-q -> PM cross "
-                            "attention -> cross-o -> norm -> gate/up GeGLU -> down), M=8, T_x=60, 2b-2b widths "
-                            "(tools/pmc_fused.py: 26 layers rotated, 3.8 GB > 256 MiB Infinity Cache); algorithmic = "
-                            "weights + cross K/V + o slabs, h, norm weights, RoPE rows in + h, down slabs out"},
+                            "attention -> cross-o -> norm -> gate/up GeGLU -> down -> norm -> next q|k|v), M=8, "
+                            "T_x=60, 2b-2b widths (tools/pmc_fused.py: 26 layers rotated, 4.3 GB > 256 MiB Infinity "
+                            "Cache); algorithmic = weights + cross K/V + o slabs, h, norm weights, RoPE rows in + h, "
+                            "q|k|v slabs out"},
     "attention": {"kernels": ["attn_decode_kernel<256, 2, false>", "attn_pvc_kernel<256, 2, 32>"],
                   "algorithmic": None,
                   "what": "decode self attention (scores + P.V/combine launches), 8 rows x 8/4 heads x 256, L ~ 527 "
@@ -49,7 +49,12 @@ def per_call(path, kernels):
 def main(op, out_dir, dst):
     spec = OPS[op]
     alg = spec["algorithmic"]
-    if alg is None:
+    if alg is None and op == "fused_block":
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import t5gemma_tts_amd  # noqa: F401
+        from t5gemma_tts_amd._lib import fused_block_bytes
+        alg = fused_block_bytes(8, 60)
+    elif alg is None:
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from pmc_attention import algorithmic_bytes
         alg = algorithmic_bytes()
