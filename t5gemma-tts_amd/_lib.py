@@ -177,21 +177,22 @@ def lib():
 GATE_UP_KERNEL = "gemv_rx_kernel<12, 1, 3 (GEGLU), 6> (decode gate/up, M=8, 84.9 MB weights)"
 FUSED_MLP_KERNEL = ("fused_mlp_kernel<1> (decode MLP half in one launch: cross-attention residual norm -> "
                     "gate/up GeGLU -> down, 127.4 MB of weights)")
-FUSED_BLOCK_KERNEL = ("fused_block_kernel (decode layer after the self-attention o-projection in one launch: "
-                      "norm -> cross-q -> PM cross attention -> cross-o -> norm -> gate/up GeGLU -> down -> norm -> "
-                      "next layer's q|k|v, 165.2 MB of weights)")
+FUSED_BLOCK_KERNEL = ("fused_block_kernel (decode layer after the self attention in one launch: "
+                      "o-proj -> norm -> cross-q -> PM cross attention -> cross-o -> norm -> gate/up GeGLU -> down -> "
+                      "norm -> next layer's q|k|v, 174.6 MB of weights)")
 
 
 def fused_block_bytes(M: int, T_x: int, d: int = 2304, f: int = 9216, q_dim: int = 2048, kv_dim: int = 1024,
                       n_layers: int = 26) -> float:
     """Algorithmic HBM bytes of one fused_block_kernel launch, averaged over a step's layers (the
-    last layer projects no next q|k|v): cross q / o, gate/up, down and the next layer's q|k|v
-    weights; the o-projection slabs, h, the six norm weights, the rows' cross K / V (T_x keys)
-    and RoPE rows in; h and the q|k|v slabs (last layer: the final normed rows) out. xn1, the
-    q slabs, att, the cross-o slabs, xn, act and the down slabs are in-launch hand-offs."""
+    last layer projects no next q|k|v): self o, cross q / o, gate/up, down and the next layer's
+    q|k|v weights; the self-attention output, h, the six norm weights, the rows' cross K / V
+    (T_x keys) and RoPE rows in; h and the q|k|v slabs (last layer: the final normed rows) out.
+    The o slabs, xn1, the q slabs, att, the cross-o slabs, xn, act and the down slabs are
+    in-launch hand-offs."""
     qkv_dim = q_dim + 2 * kv_dim
-    base = 2 * q_dim * d * 2 + 2 * f * d * 2 + d * f * 2
-    base += 4 * M * d * 4 + M * d * 2 + 6 * d * 2 + M * T_x * 2 * kv_dim * 2 + M * 256 * 4 + M * d * 2
+    base = 3 * q_dim * d * 2 + 2 * f * d * 2 + d * f * 2   # self o, cross q, cross o, gate/up, down
+    base += M * q_dim * 2 + M * d * 2 + 6 * d * 2 + M * T_x * 2 * kv_dim * 2 + M * 256 * 4 + M * d * 2
     mid = base + qkv_dim * d * 2 + 2 * M * qkv_dim * 4
     last = base + M * d * 2
     return ((n_layers - 1) * mid + last) / n_layers

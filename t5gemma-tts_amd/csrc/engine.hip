@@ -77,7 +77,8 @@ struct t5g_engine {
     bool fast_sampler = true;   // false: single-block sampler only (t5g_engine_set_sampler_path)
     // decode MLP half as one persistent launch (fused.hip; t5g_engine_set_fused)
     bool fused_mlp = true;
-    float* part2 = nullptr;     // the fused block's in-launch slabs: cross-q [2][B][q_dim] | cross-o [4][B][d] | down [8][B][d]
+    float* part2 = nullptr;     // the fused block's in-launch slabs: cross-q [2][B][q_dim] | cross-o [4][B][d] | down [8][B][d] | self o [4][B][d]
+    bf16_t* datt2 = nullptr;    // the fused block's cross-attention output [B][q_dim]
     unsigned* fsync = nullptr;  // timeout line + one counter set per decoder layer (zeroed at creation / after a timeout)
     // decode split-K factors (measured on MI355X): qkv 2, o / cross-q /
     // cross-o 4, down 8 k-slices; gate/up on the one-block-per-CU GEMV
@@ -230,7 +231,8 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->fs_ami, (int64_t)B * FS_NB);
     rc |= alloc(e, &e->fs_ticket, B);
     rc |= alloc(e, &e->fs_slow, B);
-    rc |= alloc(e, &e->part2, (int64_t)2 * B * e->q_dim + (int64_t)4 * B * d + (int64_t)8 * B * d);
+    rc |= alloc(e, &e->part2, (int64_t)2 * B * e->q_dim + (int64_t)4 * B * d + (int64_t)8 * B * d + (int64_t)4 * B * d);
+    rc |= alloc(e, &e->datt2, (int64_t)B * e->q_dim);
     rc |= alloc(e, &e->fsync, (int64_t)FM_LINE + (int64_t)FM_SET_WORDS * c.n_dec_layers);
     if (rc) {
         t5g_engine_destroy(e);
@@ -782,7 +784,7 @@ static FusedMlpArgs fused_block_args(t5g_engine* e, int M, int l) {
     fa.Hkv = c.n_kv_heads;
     fa.D = c.head_dim;
     fa.scale = c.attn_scale;
-    fa.att = e->datt;
+    fa.att = e->datt2;
     fa.Wo = (const bf16_t*)L.cross_o;
     fa.NGo = ng_pad(c.hidden);
     fa.oslab = e->part2 + (size_t)2 * M * e->q_dim;
@@ -794,6 +796,9 @@ static FusedMlpArgs fused_block_args(t5g_engine* e, int M, int l) {
     fa.NGqkv = ng_pad(e->qkv_dim);
     fa.qkv_dim = e->qkv_dim;
     fa.qkv_out = e->part;
+    fa.att_self = e->datt;
+    fa.Wo1 = (const bf16_t*)L.o;
+    fa.o1slab = fa.dslab + (size_t)8 * M * c.hidden;
     return fa;
 }
 
@@ -921,19 +926,20 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             RC(rope_store(r, st));
             RC(attn_packed(e, M, q, tok_row, tok_t, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1, win, att, st));
         }
-        RC(out_proj(att, L.o));
         const bool last = l == c.n_dec_layers - 1;
-        // the rest of the layer (cross attention + MLP half) as one persistent launch
-        // (fused.hip fused_block_kernel; bitwise equal to the launches below)
+        // the rest of the layer (o-projection, cross attention, MLP half, the last norm and
+        // the next layer's q|k|v) as one persistent launch (fused.hip fused_block_kernel;
+        // bitwise equal to the launches below)
         if (decode && e->fused_mlp && !eager && M <= 16 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 &&
             e->q_dim == 2048 && c.n_dec_layers >= 2) {
-            const int rc = fused_mlp(fused_block_args(e, M, l), st);
-            if (rc == 0) {   // also ran the layer's last norm and the next layer's q|k|v projection
+            const FusedMlpArgs fa = fused_block_args(e, M, l);
+            if (fused_mlp_check(fa) == 0) {
+                RC(fused_mlp(fa, st));
                 qkv_done = !last;
                 continue;
             }
-            if (rc != -1) RC(rc);   // -1: a shape / device the launch is not built for
         }
+        RC(out_proj(att, L.o));
         RC(resid(s_o, L.norms[1], L.norms[2]));
         // --- PM cross attention (q rotated by the decoder progress, :149-165)
         if (decode && !eager) {

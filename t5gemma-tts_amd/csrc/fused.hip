@@ -42,8 +42,8 @@ constexpr int FM_NORM_UNITS = 3;  // gate/up units of a norm workgroup (tools/di
 constexpr unsigned FM_SPIN_MAX = 1u << 18;   // ~0.3-0.5 s of polling before a wait gives up
 
 // lines of a counter set (FusedMlpArgs::sync), one word per 128-byte line
-constexpr int L_N1 = 0, L_Q0 = 1, L_A0 = 9, L_O0 = 17, L_N2 = 25, L_SL0 = 26, L_D0 = 34, L_N3 = 42;
-static_assert(L_N3 + 1 == FM_SET_LINES, "counter set layout");
+constexpr int L_N1 = 0, L_Q0 = 1, L_A0 = 9, L_O0 = 17, L_N2 = 25, L_SL0 = 26, L_D0 = 34, L_N3 = 42, L_P0 = 43;
+static_assert(L_P0 + 8 == FM_SET_LINES, "counter set layout");
 __device__ __forceinline__ unsigned* cline(unsigned* set, int line) { return set + line * FM_LINE; }
 constexpr int FS_NORM = L_N2 * FM_LINE;
 __device__ __forceinline__ int fs_slice(int s) { return (L_SL0 + s) * FM_LINE; }
@@ -560,13 +560,14 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     const int am = bu / a.Hq, ah = bu - am * a.Hq;   // attention task (row, q head)
     bool ok = true;
 
-    // ---- launch start: the attention workgroups request their row's cross K / V chunk
-    // and RoPE row (attn_decode_kernel<256, 1, true>'s VFIRST loads, waves 0-3)
+    // ---- the attention workers request their row's cross K / V chunk and RoPE row
+    // (attn_decode_kernel<256, 1, true>'s VFIRST loads, waves 0-3) right after O1
     constexpr int LPK = 32, KPW = 2, KPB = 8, NIT = 8;
     const int kg = lane / LPK, dl = lane % LPK;
     u32x4 kr[NIT], vr[NIT];
     float c8[8], s8[8];
     int alen = 0;
+    auto kv_prefetch = [&]() __attribute__((always_inline)) {
     if (attnwg && wave < 4) {
         alen = a.enc_len[am];
         const int kvc = ah / (a.Hq / a.Hkv);
@@ -591,6 +592,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
             s8[4 + jj] = sb[jj];
         }
     }
+    };
 
     // ---- the norm workgroups (the last M): N1, N2, N3 for their row and nothing else, so no
     // weight stream of their own ever queues ahead of a norm on the critical path
@@ -600,7 +602,13 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
             float hreg[8];
             const int cc = min(tq, d / 8 - 1);
             unpack8f(*(const u32x4*)(a.h + (long)nrow * d + 8 * cc), hreg);
-            fb_norm<FM_NS, false>(a.o_slabs, M, nrow, d, a.post1_w, a.pre1_w, a.eps, hreg, a.xn1, nred);
+            if (a.Wo1) {   // the o-projection slabs come from this launch's O1 stage
+                if (wave == 0) ok &= fm_wait_split<8>(a.sync, L_P0, (unsigned)(4 * (nw / 4)), tmo, 16u);
+                wg_barrier();
+                fb_norm<FM_NS, true>(a.o1slab, M, nrow, d, a.post1_w, a.pre1_w, a.eps, hreg, a.xn1, nred);
+            } else {
+                fb_norm<FM_NS, false>(a.o_slabs, M, nrow, d, a.post1_w, a.pre1_w, a.eps, hreg, a.xn1, nred);
+            }
             if (tq < d / 8) hrow[tq] = pack8f(hreg);
             fb_publish(cline(a.sync, L_N1), 1u);
         }
@@ -626,6 +634,20 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         return;
     }
     const int w = bu;   // worker index
+    const int oper = nw / 4, so = w / oper, jo = w - so * oper;   // o-projection mapping (O1 and O)
+    const bool owork = so < 4;
+    const int nu_o = owork ? (a.NGo - jo + oper - 1) / oper : 0;
+
+    // ---- O1: the self-attention o-projection, 4 k-slices of 16 k-steps over nw / 4 workers
+    // each (<= 3 units, 8 waves); its input is the previous launch's, so no wait
+    if (a.Wo1 && owork) {
+        bf16x8_s w1[3][2];
+        fb_issue<8, 2, 3>(w1, a.Wo1, a.NGo, a.q_dim / 32, so * 16, 16, jo, oper, nu_o);
+        fb_finish<8, EPI_F32, 2, 3, 2>(w1, jo, oper, nu_o, so * 16, 16, a.att_self, a.q_dim, M * a.q_dim * 2, M,
+                                       a.o1slab + (long)so * M * d, d, M * d * 4, d, red);
+        fb_publish(cline(a.sync, L_P0 + (w & 7)), 1u);
+    }
+    kv_prefetch();
 
     // ---- Q: cross-q, 2 k-slices of 36 k-steps over nw / 2 workers each (<= 2 units)
     {
@@ -649,9 +671,6 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     }
 
     // ---- A (attention workers) with O's weight requests around it
-    const int oper = nw / 4, so = w / oper, jo = w - so * oper;
-    const bool owork = so < 4;
-    const int nu_o = owork ? (a.NGo - jo + oper - 1) / oper : 0;
     bf16x8_s wo[3][2];
     if (attnwg && wave >= 4 && owork) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, oper, nu_o);
     if (attnwg) {
@@ -867,6 +886,7 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
             !a.att || !a.Wo || !a.oslab)
             return -1;
         if (!a.dslab || !a.post3_w || !a.pre3_w) return -1;
+        if (a.Wo1 && (!a.att_self || !a.o1slab)) return -1;
         if (a.Wqkv && (!a.qkv_out || a.NGqkv * 16 != a.qkv_dim)) return -1;
         a.norm_b0 = nb - a.M;
         const size_t shm = (size_t)5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16 + 64 * sizeof(float) + (size_t)a.d * 2;

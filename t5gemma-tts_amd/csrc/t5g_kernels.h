@@ -102,14 +102,19 @@ struct FusedMlpArgs {
     const bf16_t* Wqkv;       // next layer's packed q|k|v (NGqkv row groups, K = d), or null
     int NGqkv, qkv_dim;
     float* qkv_out;           // [2][M][qkv_dim]
+    // ---- the self-attention o-projection in front (Wo1 non-null): O1 = att_self . Wo1^T as
+    //   fp32 slabs [4][M][d] in o1slab (in-launch), the N1 norm's input instead of o_slabs
+    const bf16_t* att_self;   // [M][q_dim] self-attention output (previous launch)
+    const bf16_t* Wo1;        // packed self o_proj, NGo row groups, K = q_dim
+    float* o1slab;
 };
 int fused_mlp(const FusedMlpArgs& a, hipStream_t st);
 int fused_mlp_check(const FusedMlpArgs& a);   // 0: fused_mlp would launch these args; -1: not built for them
 // counter words of one fused launch, each on its own 128-byte line (arrivals on one line
 // serialise at ~12 ns each): N1, 8 cross-q heads, 8 attention heads, 8 cross-o groups,
-// N2, 8 down slices, 8 down groups, N3. The engine keeps one set per decoder layer after
-// one line for the timeout word.
-constexpr int FM_LINE = 32, FM_SET_LINES = 43, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
+// N2, 8 down slices, 8 down groups, N3, 8 o-projection groups. The engine keeps one set per
+// decoder layer after one line for the timeout word.
+constexpr int FM_LINE = 32, FM_SET_LINES = 51, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
 
 // ---- row-wise residual / RMSNorm / embedding -------------------------------
 struct NormArgs {
