@@ -18,19 +18,25 @@ def main():
     L = _lib.lib()
     dev = torch.device("cuda:0")
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    # prefill gate/up GEGLU, M = 1216 tokens (8 x 152), register-tiled prefill kernel
-    M, N, K = 1216, 18432, 2304
-    w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
-    p = torch.empty(L.t5g_packed_bytes(N, K) // 2, dtype=torch.bfloat16, device=dev)
-    _lib.check(L.t5g_pack_weight(C.c_void_p(w.data_ptr()), N, K, K, C.c_void_p(p.data_ptr()), st), "pack")
-    X = torch.randn(M, K, device=dev).to(torch.bfloat16)
-    Y = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
-    arr = (C.c_void_p * 1)(p.data_ptr())
-    us = C.c_float()
-    _lib.check(L.t5g_time_gemm(C.c_void_p(X.data_ptr()), K, M, arr, 1, N, K, 1, C.c_void_p(Y.data_ptr()), N // 2,
-                               3 | 0x100, 10, st, C.byref(us)), "prefill")
-    print("prefill gate/up us", us.value, "TF/s", 2 * M * N * K / us.value / 1e6, flush=True)
-    del w, p
+    # prefill GEMMs at the C3 decoder prefill (1216 tokens = 8 x 152) and a C5 one (4864):
+    # the LDS-staged kernel (gemm_pfl_kernel, the engine's) and the register ring
+    # (gemm_pf_kernel, flag 0x200) on the same operands
+    for M in (1216, 4864):
+        for N, K, epi in ((18432, 2304, 3), (2304, 9216, 0), (4096, 2304, 0)):
+            w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+            p = torch.empty(L.t5g_packed_bytes(N, K) // 2, dtype=torch.bfloat16, device=dev)
+            _lib.check(L.t5g_pack_weight(C.c_void_p(w.data_ptr()), N, K, K, C.c_void_p(p.data_ptr()), st), "pack")
+            X = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+            ldy = N // 2 if epi == 3 else N
+            Y = torch.empty(M, ldy, dtype=torch.bfloat16, device=dev)
+            arr = (C.c_void_p * 1)(p.data_ptr())
+            for flag in (0x100, 0x300):
+                us = C.c_float()
+                _lib.check(L.t5g_time_gemm(C.c_void_p(X.data_ptr()), K, M, arr, 1, N, K, 1, C.c_void_p(Y.data_ptr()),
+                                           ldy, epi | flag, 10, st, C.byref(us)), "prefill")
+                print(f"prefill M={M} N={N} K={K} {'lds' if flag == 0x100 else 'reg'} us {us.value:.1f} "
+                      f"TF/s {2 * M * N * K / us.value / 1e6:.1f}", flush=True)
+            del w, p
     # XCodec2 decoder, B = 32 x 500 frames
     from t5gemma_tts_amd.codec import XCodec2Decoder, codec_16k, synthetic_codec_weights
     cfg = codec_16k()
