@@ -30,6 +30,10 @@ extern "C" {
 #define T5G_EUNSUPPORTED (-3)
 #define T5G_ENOMEM (-4)
 #define T5G_ECAPACITY (-5)   /* exceeds engine capacity (max_batch / max_text / max_audio) */
+#define T5G_EHANDOFF (-6)    /* a fused decode launch's in-launch hand-off gave up waiting (not all of its
+                              * workgroups were resident, e.g. another process shares the GPU): that
+                              * call's outputs are invalid; the counters are cleared, rerun with
+                              * t5g_engine_set_fused(e, 0) -> FusedHandoffError */
 
 #define T5G_MAX_LAYERS 64
 

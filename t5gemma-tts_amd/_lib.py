@@ -13,11 +13,16 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("T5G_LIB", os.path.join(_PKG, "lib", "libt5gtts.so"))
 MAX_LAYERS = 64
 
-T5G_ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "EUNSUPPORTED", -4: "ENOMEM", -5: "ECAPACITY"}
+T5G_ERRORS = {-1: "EINVAL", -2: "EHIP", -3: "EUNSUPPORTED", -4: "ENOMEM", -5: "ECAPACITY", -6: "EHANDOFF"}
 
 
 class T5GError(RuntimeError):
     pass
+
+
+class FusedHandoffError(T5GError):
+    """A fused decode launch gave up waiting for a hand-off (its workgroups were not all
+    resident, e.g. another process shares the GPU); the call's outputs are invalid."""
 
 
 def check(rc: int, what: str) -> None:
@@ -26,6 +31,8 @@ def check(rc: int, what: str) -> None:
     name = T5G_ERRORS.get(rc, str(rc))
     if rc in (-1, -5):
         raise ValueError(f"{what}: {name}")
+    if rc == -6:
+        raise FusedHandoffError(f"{what}: {name}")
     raise T5GError(f"{what}: {name}")
 
 

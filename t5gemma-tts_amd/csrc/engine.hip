@@ -1224,7 +1224,7 @@ extern "C" int t5g_read_tokens(t5g_engine* e, int32_t* out, int32_t B, void* str
         fprintf(stderr, "[t5gtts] fused MLP hand-off timed out (code %u)\n", tmo);
         hipMemsetAsync(e->fsync, 0, (FM_LINE + (size_t)FM_SET_WORDS * e->c.n_dec_layers) * sizeof(unsigned), st);
         hipStreamSynchronize(st);
-        return T5G_EHIP;
+        return T5G_EHANDOFF;
     }
     return T5G_OK;
 }

@@ -285,17 +285,30 @@ class T5GemmaTTSEngine:
                                      f"reference K-split table ({_lib.EXACT_MAX_TOKENS})")
         self.set_exact(exact)
         stream = _stream(self.device)
+        gen_state = [g.get_state() for g in generators] if generators is not None else None
+        try:
+            out = self._generate_once(utts, params, seeds, generators, parity, use_graph, chunk, record_logits, stream)
+        except _lib.FusedHandoffError:
+            # the fused decode launch could not have all its workgroups resident (another
+            # process on this GPU): rerun on the per-op launches, which compute the same bits
+            self.set_fused(False)
+            if gen_state is not None:
+                for g, st_ in zip(generators, gen_state):
+                    g.set_state(st_)
+            out = self._generate_once(utts, params, seeds, generators, parity, use_graph, chunk, record_logits, stream)
+        if generators is not None:
+            for g, row in zip(generators, out["gen"]):
+                consume_noise(g, len(row), self.V)
+        return out
+
+    def _generate_once(self, utts, params, seeds, generators, parity, use_graph, chunk, record_logits, stream):
         ctx = self._prepare(utts, params, generators if generators is not None else seeds, parity, stream)
         if parity:
             self._run_parity(ctx, stream, record_logits)
         else:
             while not self._decode_chunk(ctx, chunk, use_graph, stream):
                 pass
-        out = self._collect(ctx, stream)
-        if generators is not None:
-            for g, row in zip(generators, out["gen"]):
-                consume_noise(g, len(row), self.V)
-        return out
+        return self._collect(ctx, stream)
 
     # -- phases ------------------------------------------------------------------
     def _prepare(self, utts, params, seeds, parity, stream):

@@ -93,3 +93,21 @@ def test_gemv_rejects_unsupported_shapes(layout, M, K, splits, epi, nw):
     a.X, a.ldx, a.Y, a.ldy, a.splits, a.layout, a.max_grid = 16, K, 16, 2304, splits, layout, 0
     a.W = 16   # never dereferenced: every case is rejected before a launch
     assert L.t5g_gemv(C.byref(a), None) < 0
+
+
+def test_status_codes_map_to_python_errors():
+    """The C ABI's statuses raise what the reference's code paths would (ValueError for bad
+    arguments / capacity) and a FusedHandoffError for a fused decode launch whose hand-off
+    gave up (engine.generate reruns such a call on the per-op launches)."""
+    import pytest as _pt
+    from t5gemma_tts_amd import _lib
+    _lib.check(0, "ok")
+    with _pt.raises(ValueError):
+        _lib.check(-1, "x")
+    with _pt.raises(ValueError):
+        _lib.check(-5, "x")
+    with _pt.raises(_lib.FusedHandoffError):
+        _lib.check(-6, "x")
+    with _pt.raises(_lib.T5GError):
+        _lib.check(-2, "x")
+    assert issubclass(_lib.FusedHandoffError, _lib.T5GError)
