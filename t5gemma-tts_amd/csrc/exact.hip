@@ -122,6 +122,18 @@ __device__ __forceinline__ float exact_chunk_v(const u32x4* xr4, const float* wf
     return __fadd_rn(e, o);
 }
 
+// exact_chunk_v on X words already in registers
+__device__ __forceinline__ float exact_chunk_x(const u32x4 (&xv)[4], const float* wf) {
+    float e = 0.f, o = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t xw = xv[i >> 2][i & 3];
+        e = fmaf(bf_lo(xw), wf[2 * i], e);
+        o = fmaf(bf_hi(xw), wf[2 * i + 1], o);
+    }
+    return __fadd_rn(e, o);
+}
+
 __device__ __forceinline__ void exact_load_chunk(const bf16_t* wg, int kb, int r16, float* wf) {
     u32x4 wv[4];
 #pragma unroll
@@ -220,12 +232,23 @@ __global__ __launch_bounds__(1024) void exact_linear_g16_kernel(ExactLinArgs a) 
     if (folder) kbc = exact_lin_kbc(a, min(fr, a.M - 1), g * 16 + fc);
     int nb = 0;   // next K part boundary (chunk index)
     const int nst = (KB + SC - 1) / SC;
-    // this lane's weight chunk of the current stage, loaded one stage ahead
+    // this lane's weight chunk of the current stage, loaded one stage ahead; at 1-2 rows
+    // (batch-1 / batch-2 decode) the X chunks too, so a stage never waits for a load
+    constexpr bool XPRE = RT <= 2;
     u32x4 wv[4];
+    u32x4 xq[XPRE ? RT : 1][4];
     auto load = [&](int kb) {
         if (kb < KB) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) wv[j] = *(const u32x4*)(wg + ((long)kb * 64 + j * 16 + r16) * 8);
+            if constexpr (XPRE) {
+#pragma unroll
+                for (int r = 0; r < RT; ++r) {
+                    const u32x4* xr4 = (const u32x4*)(a.X + (long)min(r, a.M - 1) * a.ldx + kb * 32);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) xq[r][j] = xr4[j];
+                }
+            }
         }
     };
     load(w * 4 + q);
@@ -243,7 +266,8 @@ __global__ __launch_bounds__(1024) void exact_linear_g16_kernel(ExactLinArgs a) 
 #pragma unroll
             for (int r = 0; r < RT; ++r) {
                 const int m = min(r, a.M - 1);
-                cs[s & 1][r][r16][w * 4 + q] = exact_chunk_v((const u32x4*)(a.X + (long)m * a.ldx + kb * 32), wf);
+                if constexpr (XPRE) cs[s & 1][r][r16][w * 4 + q] = exact_chunk_x(xq[r], wf);
+                else cs[s & 1][r][r16][w * 4 + q] = exact_chunk_v((const u32x4*)(a.X + (long)m * a.ldx + kb * 32), wf);
             }
         }
         load(kb + SC);
@@ -372,7 +396,52 @@ __global__ __launch_bounds__(256) void exact_attn_kernel(ExactAttnArgs a) {
     for (int bs = 0; bs < nk; bs += XA_BLOCK) {
         const int blen = min(XA_BLOCK, Tk - bs);
         // ---- scores of the block (masked keys -inf)
-        for (int kk = tid; kk < blen; kk += 256) {
+        if (gemv && !has_mask && !sdpa_causal) {
+            // decode rows (one query, no mask): both of this thread's keys' rows requested
+            // before either dot product (the loop below would wait for each in turn)
+            u32x4 kv2[2][XA_MAXD / 8];
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {
+                const int kk = tid + 256 * r2;
+                const bf16_t* kr = Kb + (long)(bs + (kk < blen && bs + kk < nk ? kk : 0)) * D;
+#pragma unroll
+                for (int j = 0; j < XA_MAXD / 8; ++j)
+                    kv2[r2][j] = j * 8 < D ? *(const u32x4*)(kr + 8 * j) : (u32x4){0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {
+                const int kk = tid + 256 * r2;
+                if (kk < blen) {
+                    float s = -INFINITY;
+                    if (bs + kk < nk) {
+                        float acc[16];
+#pragma unroll
+                        for (int l2 = 0; l2 < 16; ++l2) acc[l2] = 0.f;
+#pragma unroll
+                        for (int cb = 0; cb < XA_MAXD / 32; ++cb) {
+                            if (cb * 32 < D) {
+                                const int c = cb * 32;
+#pragma unroll
+                                for (int l2 = 0; l2 < 16; ++l2) {
+                                    const uint32_t kw = kv2[r2][cb * 4 + (l2 >> 2)][l2 & 3];
+                                    acc[l2] = fmaf(qs_[c + 2 * l2 + 1], bf_hi(kw), acc[l2]);
+                                    acc[l2] = fmaf(qs_[c + 2 * l2], bf_lo(kw), acc[l2]);
+                                }
+                            }
+                        }
+                        float v8[8], v4[4];
+#pragma unroll
+                        for (int l2 = 0; l2 < 8; ++l2) v8[l2] = __fadd_rn(acc[l2], acc[l2 + 8]);
+#pragma unroll
+                        for (int l2 = 0; l2 < 4; ++l2) v4[l2] = __fadd_rn(v8[2 * l2], v8[2 * l2 + 1]);
+                        s = __fmul_rn(__fadd_rn(__fadd_rn(v4[0], v4[1]), __fadd_rn(v4[2], v4[3])), a.scale);
+                    }
+                    sp[kk] = s;
+                    XA_DBG(0, bs + kk, s);
+                }
+            }
+        }
+        for (int kk = tid; !(gemv && !has_mask && !sdpa_causal) && kk < blen; kk += 256) {
             const int key = bs + kk;               // index into the call's keys
             const int kabs = key + lo;
             bool vis;
@@ -468,23 +537,45 @@ __global__ __launch_bounds__(256) void exact_attn_kernel(ExactAttnArgs a) {
             const int ch = gemv ? 8 : (pack ? xa_even_div_chunk(blen) : 32);
             const int nch = (blen + ch - 1) / ch;
             const bf16_t* vc = Vb + (long)bs * D + d;
-            for (int c = part; d < D && c < nch; c += XA_PARTS) {
+            if (gemv) {
+                // pairs (odd key first), one chain per 8-key group. Every V value of this
+                // thread's groups (<= 8 groups x 8 keys) is requested before the first
+                // chain: one memory round trip instead of one per group. Keys past the block
+                // read key 0 and count as 0 (clamped address, no branch around the load).
+                constexpr int MAXG = XA_BLOCK / 8 / XA_PARTS;
+                const int dd = min(d, D - 1);
+                float vv[MAXG][8];
+#pragma unroll
+                for (int i = 0; i < MAXG; ++i) {
+                    const int c0 = (part + i * XA_PARTS) * 8;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int key = c0 + j;
+                        const float v = bf2f(Vb[(long)(bs + (key < blen ? key : 0)) * D + dd]);
+                        vv[i][j] = key < blen ? v : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < MAXG; ++i) {
+                    const int c = part + i * XA_PARTS;
+                    if (d < D && c < nch) {
+                        const int c0 = c * 8, cn = min(8, blen - c0);
+                        float tmp = 0.f;
+#pragma unroll
+                        for (int j = 0; j < 8; j += 2) {
+                            if (j < cn) {
+                                if (j + 1 < cn) tmp = fmaf(sp[c0 + j + 1], vv[i][j + 1], tmp);
+                                tmp = fmaf(sp[c0 + j], vv[i][j], tmp);
+                            }
+                        }
+                        csum[c * XA_DS + dl] = tmp;
+                    }
+                }
+            }
+            for (int c = part; !gemv && d < D && c < nch; c += XA_PARTS) {
                 const int c0 = c * ch, cn = min(ch, blen - c0);
                 float cs;
-                if (gemv) {   // pairs (odd key first), one chain per 8-key group
-                    float vv[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) vv[j] = j < cn ? bf2f(vc[(long)(c0 + j) * D]) : 0.f;
-                    float tmp = 0.f;
-#pragma unroll
-                    for (int j = 0; j < 8; j += 2) {
-                        if (j < cn) {
-                            if (j + 1 < cn) tmp = fmaf(sp[c0 + j + 1], vv[j + 1], tmp);
-                            tmp = fmaf(sp[c0 + j], vv[j], tmp);
-                        }
-                    }
-                    cs = tmp;
-                } else {      // E/O chains of the chunk
+                {             // E/O chains of the chunk
                     float e = 0.f, o = 0.f;
                     for (int j0 = 0; j0 < cn; j0 += 8) {
                         float vv[8];
