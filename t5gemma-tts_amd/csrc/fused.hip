@@ -408,10 +408,13 @@ __device__ __forceinline__ void fb_issue(bf16x8_s (&w)[UMAX][SPU], const bf16_t*
 }
 // ... and the rest: rendezvous, X fragments (sc1), MFMAs, fixed-order wave reduction,
 // epilogue. OUT: 0 = GeGLU bf16 (sc1, 8 B), 1 = fp32 plain, 2 = fp32 sc1 (16 B).
-template <int NWG, int EPI, int SPU, int UMAX, int OUT>
+// LDSU: units i < nu_reg come from w, unit nu_reg (if < nu) from the LDS image lw (k-steps
+// 0 .. NWG * SPU - 1 of one unit, 1 KiB each, fragment layout) -- the same MFMAs in the
+// same order as from registers.
+template <int NWG, int EPI, int SPU, int UMAX, int OUT, bool LDSU = false>
 __device__ __forceinline__ void fb_finish(bf16x8_s (&w)[UMAX][SPU], int g0, int gs, int nu, int kb_lo, int KBs,
                                           const bf16_t* X, int ldx, int xbytes, int M, void* Y, int ldy, int ybytes,
-                                          int N, f32x4* red) {
+                                          int N, f32x4* red, const char* lw = nullptr, int nu_reg = 0) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int xr = lane & 15;
     wg_barrier();   // the hand-off is complete (or abandoned) for every wave past here
@@ -427,12 +430,22 @@ __device__ __forceinline__ void fb_finish(bf16x8_s (&w)[UMAX][SPU], int g0, int 
                 __builtin_bit_cast(bf16x8_s, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo + kb * 64, 0, AUX_SC1));
             xf[j] = (xr < M && wave + j * NWG < KBs) ? v : z8;
         }
+        const int nr = LDSU ? nu_reg : nu;
 #pragma unroll
         for (int i = 0; i < UMAX; ++i) {
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int j = 0; j < SPU; ++j) acc = mfma16(w[i][j], xf[j], acc);
-            if (i < nu) red[(i * NWG + wave) * 64 + lane] = acc;
+            if (i < nr) red[(i * NWG + wave) * 64 + lane] = acc;
+        }
+        if constexpr (LDSU) {
+            if (nu_reg < nu) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int j = 0; j < SPU; ++j)
+                    acc = mfma16(*(const bf16x8_s*)(lw + ((wave + j * NWG) * 64 + lane) * 16), xf[j], acc);
+                red[(nu_reg * NWG + wave) * 64 + lane] = acc;
+            }
         }
     }
     __syncthreads();
@@ -538,6 +551,10 @@ struct FbAttnLds {
     float qs[256];
     float stat_l;
 };
+constexpr int FB_D = 2304;                                    // the block kernel's model width
+constexpr int FB_GU_KB = FB_D / 32;                           // gate/up k-steps (= FM_NW x 6)
+constexpr size_t FB_GU_OFF = (5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16 + 64 * sizeof(float) + FB_D * 2 + 1023) / 1024 * 1024;
+constexpr size_t FB_LDS = FB_GU_OFF + (size_t)FB_GU_KB * 1024;
 
 template <bool XA_DUMMY = true>
 __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a) {
@@ -547,6 +564,8 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     float* nred = (float*)(smem + 5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16);   // norm: 2 x 32 floats
     // a norm workgroup's residual row between N1, N2 and N3 (bf16, exact: every h is rounded)
     u32x4* hrow = (u32x4*)(smem + 5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16 + 64 * sizeof(float));
+    // a worker's last gate/up unit (72 KiB), fetched by LDS-DMA while the chain runs O1 -> O
+    char* gul = smem + FB_GU_OFF;
     unsigned* tmo = a.timeout;
     const int bu = (int)blockIdx.x, nb = (int)gridDim.x;
     const int tq = (int)threadIdx.x, wave = tq >> 6, lane = tq & 63;
@@ -634,6 +653,12 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         return;
     }
     const int w = bu;   // worker index
+    // gate/up: contiguous unit runs over the workers (<= 5 units, the last one from LDS)
+    const int KBg = d / 32, NGg = a.NGgu;
+    const int ubase = NGg / nw, uextra = NGg - ubase * nw;
+    const int nu_g = ubase + (w < uextra ? 1 : 0);
+    const int g_lo = w * ubase + min(w, uextra);
+    const bool gu_lds = nu_g > 0 && !attnwg;
     const int oper = nw / 4, so = w / oper, jo = w - so * oper;   // o-projection mapping (O1 and O)
     const bool owork = so < 4;
     const int nu_o = owork ? (a.NGo - jo + oper - 1) / oper : 0;
@@ -668,6 +693,21 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
                     __hip_atomic_fetch_add(cline(a.sync, L_Q0 + (jq + i * qper) / (D / 16)), 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+
+    // waves 8-11 of the workers that run no attention request the run's last gate/up unit
+    // into LDS: 18 x 1 KiB each, no registers, while the attention workers run A (on an
+    // attention worker the copies would queue ahead of its q loads). O's publish drains
+    // them (vmcnt); its barrier makes them visible to the other waves.
+    if (gu_lds && wave >= 8) {
+        const int wv = __builtin_amdgcn_readfirstlane(wave - 8);
+        const __amdgpu_buffer_rsrc_t gr = frag_rsrc(a.Wgu, (uint32_t)NGg * (uint32_t)KBg * 1024u);
+        const int gb = ((g_lo + nu_g - 1) * KBg + wv * (FB_GU_KB / 4)) * 1024 + lane * 16;
+        __attribute__((address_space(3))) char* dst =
+            (__attribute__((address_space(3))) char*)gul + wv * (FB_GU_KB / 4) * 1024;
+#pragma unroll
+        for (int q = 0; q < FB_GU_KB / 4; ++q)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, dst + q * 1024, 16, gb + q * 1024, 0, 0, AUX_NT);
     }
 
     // ---- A (attention workers) with O's weight requests around it
@@ -788,18 +828,16 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         fb_publish(cline(a.sync, L_O0 + (w & 7)), 1u);
     }
 
-    // ---- G: gate/up, contiguous unit runs over the workers (<= 5 units)
-    const int KBg = d / 32, NGg = a.NGgu;
-    const int ubase = NGg / nw, uextra = NGg - ubase * nw;
-    const int nu_g = ubase + (w < uextra ? 1 : 0);
-    const int g_lo = w * ubase + min(w, uextra);
+    // ---- G: gate/up, contiguous unit runs over the workers (<= 5 units; the last from LDS
+    // on the workers that fetched it)
     {
         bf16x8_s wg[5][6];
         if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N2, (unsigned)M, tmo, 5u);
         T5G_TS(3);
-        fb_issue<FM_NW, 6, 5>(wg, a.Wgu, NGg, KBg, 0, KBg, g_lo, 1, nu_g);
-        fb_finish<FM_NW, EPI_GEGLU, 6, 5, 0>(wg, g_lo, 1, nu_g, 0, KBg, a.xn, d, M * d * 2, M, a.act, f, M * f * 2,
-                                             2 * f, red);
+        const int nu_r = gu_lds ? nu_g - 1 : nu_g;
+        fb_issue<FM_NW, 6, 5>(wg, a.Wgu, NGg, KBg, 0, KBg, g_lo, 1, nu_r);
+        fb_finish<FM_NW, EPI_GEGLU, 6, 5, 0, true>(wg, g_lo, 1, nu_g, 0, KBg, a.xn, d, M * d * 2, M, a.act, f,
+                                                   M * f * 2, 2 * f, red, gul, nu_r);
     }
     T5G_TS(4);
     const int units_per_slice = f / FM_DS / 8;
@@ -889,7 +927,9 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
         if (a.Wo1 && (!a.att_self || !a.o1slab)) return -1;
         if (a.Wqkv && (!a.qkv_out || a.NGqkv * 16 != a.qkv_dim)) return -1;
         a.norm_b0 = nb - a.M;
-        const size_t shm = (size_t)5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16 + 64 * sizeof(float) + (size_t)a.d * 2;
+        static_assert(FB_GU_KB == FM_NW * 6 && FB_GU_KB % 4 == 0 && FB_LDS <= FM_LDS_MAX, "gate/up LDS unit");
+        if (a.d != FB_D) return -1;
+        const size_t shm = FB_LDS;
         static bool attr_b = false;
         if (!attr_b) {
             (void)hipFuncSetAttribute((const void*)fused_block_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
