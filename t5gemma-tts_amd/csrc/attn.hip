@@ -656,8 +656,8 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
     const int nblk = (r.span + SDPA_KV_BLOCK - 1) / SDPA_KV_BLOCK;
     const int nsr = nblk * RPB;
     const int cr = tid / TPC, slot = (tid % TPC) / NOCT, od = tid % NOCT;
-    // V slices of sub-rounds 0 and 1 and the scores of blocks 0 and 1 first (all loads
-    // unconditional; keys past the row read as zeros through the buffer range check)
+    // a sub-round's V slice (unconditional: keys past the row read as zeros through the
+    // buffer range check)
     const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride;
     const __amdgpu_buffer_rsrc_t vrs = frag_rsrc(Vb, (uint32_t)a.kv_cap * D * 2u);
     auto vload = [&](u32x4 (&v)[NIT], int sr) {
@@ -665,13 +665,16 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
 #pragma unroll
         for (int i = 0; i < NIT; ++i) {
             const int j = r.lo + c * DCH + i * KPB + slot;
-            const int off = (sr < nsr && j < r.hi) ? (j * D + PVC_DZ * z + 8 * od) * 2 : (int)0x7ffffff0;
+            int off = (sr < nsr && j < r.hi) ? (j * D + PVC_DZ * z + 8 * od) * 2 : (int)0x7ffffff0;
+            // an opaque offset: otherwise the uniform sr < nsr test becomes a branch between
+            // two forms of the load, and its join waits for every load in flight
+            asm volatile("" : "+v"(off));
             v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
         }
     };
-    u32x4 vn[NIT], v1[NIT];
-    vload(vn, 0);
-    if constexpr (RPB == 1) vload(v1, 1);   // the second block's slice (zeros if none)
+    // the scores and chunk maxima first (small, L2-resident: the scores launch wrote them),
+    // then the V slices: the running maxima, the exact p and the block sums are computed
+    // while V is in flight (vmcnt is in order). Every load unconditional (clamped index).
     const float* sb = a.sbuf + ((long)qi * a.Hkv * G + kvh * G) * a.kv_cap + r.lo;
     auto sload = [&](float (&sc)[G][PPT], int b) {
 #pragma unroll
@@ -685,9 +688,13 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
     float scn[G][PPT], sc1[G][PPT];
     sload(scn, 0);
     if constexpr (RPB == 1) sload(sc1, 1);
+    const float cmv = a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + min(lane, a.nsplit - 1)) * G + min(wave, G - 1)];
+    u32x4 vn[NIT], v1[NIT];
+    vload(vn, 0);
+    if constexpr (RPB == 1) vload(v1, 1);   // the second block's slice (zeros if none)
     if (wave < G) {   // running maxima through each block, from the chunk maxima
         const int g = wave;
-        const float cm = lane < nch ? a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + lane) * G + g] : -INFINITY;
+        const float cm = lane < nch ? cmv : -INFINITY;
         for (int b = 0; b < nblk; ++b) {
             const float mb = wave_max(lane < min(nch, (b + 1) * CPB) ? cm : -INFINITY);
             if (lane == 0) mrun[g][b] = mb;
@@ -698,6 +705,7 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
         }
     }
     __syncthreads();
+    T5G_TS(2);
     const bool folder = tid < G * PVC_DZ;
     const int fg = tid / PVC_DZ, fdd = tid % PVC_DZ;
     if constexpr (RPB == 1) {
@@ -725,6 +733,7 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
                 }
             }
             __syncthreads();
+            T5G_TS(3);
             if (wave < G * nblk) {
                 const int g = wave % G, bb = wave / G;
                 const int blen = min(SDPA_KV_BLOCK, r.span - bb * SDPA_KV_BLOCK);
@@ -761,7 +770,7 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
                 }
             }
             __syncthreads();
-            T5G_TS(1);
+            T5G_TS(4);
             if (!folder) return;
             float lsum = 0.f, mo = -INFINITY, dd = 0.f;
             for (int bb = 0; bb < nblk; ++bb) {
@@ -791,6 +800,7 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
             }
             const float inv = __fdiv_rn(1.0f, lsum);
             a.O[(long)qi * a.ldo + (kvh * G + fg) * D + PVC_DZ * z + fdd] = f2bf(__fmul_rn(dd, inv));
+            T5G_TS(1);
             return;
         }
     }

@@ -46,13 +46,24 @@ def main():
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3, eos_disabled=True)
     eng.generate(utts, p, seeds=list(range(8)), chunk=64)
     torch.cuda.synchronize()
-    # the attn buffer holds the last layer's launches, each overwriting block slots from 0:
-    # cross attention (blocks 0-31), P.V/combine (32-255), scores (256-479)
-    # norm: the last layer's final norm (blocks 0-7); gemm: head1 (blocks 0-143); blocks past
-    # those hold older launches (prefill) and are not read
-    groups = [("norm", "norm (final, 8 rows)", 0, 8), ("attn", "attn cross", 0, 32), ("attn", "attn pvc", 32, 256),
-              ("attn", "attn scores", 256, 480), ("gemm", "gemm head1", 0, 144),
+    # the attn buffer holds the last layer's self-attention launches, each overwriting block
+    # slots from 0: scores (480 blocks), then P.V/combine (slots 0-255); slots 256-479 keep
+    # the scores launch. norm: the last per-op resid_norm; gemm: head1 (blocks 0-143)
+    groups = [("norm", "norm (8 rows)", 0, 8), ("attn", "attn pvc", 0, 256),
+              ("attn", "attn scores (blocks 256-479)", 256, 480), ("gemm", "gemm head1", 0, 144),
               ("sampler", "sampler_fast (last step with live rows)", 0, 128)]
+    a = bufs["attn"].view(-1, 8).cpu().numpy()
+    sc, pv = a[256:480], a[0:256]
+    sc, pv = sc[sc[:, 0] > 0], pv[pv[:, 0] > 0]
+    if len(sc) and len(pv):
+        base = sc[:, 0].min()
+        ends = np.maximum.reduce([sc[:, k] for k in range(1, 7)])
+        print(f"== scores -> pvc (absolute, from the first scores block start): scores last end "
+              f"{(ends.max() - base) * 10} ns, median end {int(np.median(ends - base)) * 10} ns; pvc first start "
+              f"{(pv[:, 0].min() - base) * 10} ns, median start {int(np.median(pv[:, 0] - base)) * 10} ns, "
+              f"median point 1 {int(np.median(pv[:, 1] - base)) * 10} ns, last point 1 {(pv[:, 1].max() - base) * 10} ns")
+        print("   pvc points (one-pass rows): 2 = scores / chunk maxima in, 3 = p staged, 4 = P.V chains in LDS, "
+              "1 = output stored")
     for u, name, lo, hi in groups:
         a = bufs[u].view(-1, 8).cpu().numpy()[lo:hi]
         rows = a[(a[:, 0] > 0)]
