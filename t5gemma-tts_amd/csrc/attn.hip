@@ -640,11 +640,14 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
     __shared__ float pbf[G][SDPA_KV_BLOCK];        // bf16-rounded p (P.V)
     __shared__ float mrun[G][SDPA_MAX_BLOCKS];     // running max through block b
     __shared__ float et_s[G], stat_l[G];
-    __shared__ float ol[CPR][KPB][G][PVC_DZ];      // slot chain sums of the sub-round
+    // slot chain sums of the sub-round, one padded row per slot: a wave's slots then start
+    // on different banks (unpadded, the 16 slots of a wave's lanes met on 4 banks: 16-way)
+    constexpr int OLW = G * PVC_DZ + 4;
+    __shared__ __attribute__((aligned(16))) float ol[CPR][KPB][OLW];
     // second block of the one-pass path (rows of <= 1024 keys)
     __shared__ float pex1[G][SDPA_KV_BLOCK + 16];
     __shared__ float pbf1[G][SDPA_KV_BLOCK];
-    __shared__ float ol1[CPR][KPB][G][PVC_DZ];
+    __shared__ __attribute__((aligned(16))) float ol1[CPR][KPB][OLW];
     __shared__ float tsum[G][2];
     const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -764,9 +767,11 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
                         }
                     }
 #pragma unroll
-                    for (int g = 0; g < G; ++g)
-#pragma unroll
-                        for (int jj = 0; jj < 8; ++jj) (bb ? ol1 : ol)[cr][slot][g][8 * od + jj] = o[g][jj];
+                    for (int g = 0; g < G; ++g) {
+                        float* dst = &(bb ? ol1 : ol)[cr][slot][g * PVC_DZ + 8 * od];
+                        *(f32x4*)dst = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
+                        *(f32x4*)(dst + 4) = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
+                    }
                 }
             }
             __syncthreads();
@@ -786,7 +791,7 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
                     for (int w = 0; w < 4; ++w) {
                         float t[KPW];
 #pragma unroll
-                        for (int k = 0; k < KPW; ++k) t[k] = (bb ? ol1 : ol)[c][w * KPW + k][fg][fdd];
+                        for (int k = 0; k < KPW; ++k) t[k] = (bb ? ol1 : ol)[c][w * KPW + k][fg * PVC_DZ + fdd];
 #pragma unroll
                         for (int st = 1; st < KPW; st <<= 1)
 #pragma unroll
@@ -852,9 +857,11 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
             }
         }
 #pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) ol[cr][slot][g][8 * od + jj] = o[g][jj];
+        for (int g = 0; g < G; ++g) {
+            float* dst = &ol[cr][slot][g * PVC_DZ + 8 * od];
+            *(f32x4*)dst = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
+            *(f32x4*)(dst + 4) = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
+        }
         __syncthreads();
         if (folder) {
             if (rr == 0) blk = 0.f;
@@ -865,7 +872,7 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
                 for (int w = 0; w < 4; ++w) {
                     float t[KPW];
 #pragma unroll
-                    for (int k = 0; k < KPW; ++k) t[k] = ol[c][w * KPW + k][fg][fdd];
+                    for (int k = 0; k < KPW; ++k) t[k] = ol[c][w * KPW + k][fg * PVC_DZ + fdd];
 #pragma unroll
                     for (int st = 1; st < KPW; st <<= 1)
 #pragma unroll
