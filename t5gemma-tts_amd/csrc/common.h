@@ -298,6 +298,15 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
                     __builtin_amdgcn_s_getreg((31 << 11) | 4);                                     \
         }                                                                                          \
     } while (0)
+// the same, stored by thread `tid` (a point reached first by another wave)
+#define T5G_TS_BY(k, tid)                                                                          \
+    do {                                                                                           \
+        if (threadIdx.x == (tid) && t5g_dbg_ts_buf) {                                             \
+            const size_t blin_ = (size_t)a.dbg_seq * 4096 +                                         \
+                                 blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);   \
+            t5g_dbg_ts_buf[blin_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                    \
+        }                                                                                          \
+    } while (0)
 // the block-start clock read now, stored later (T5G_TS_START / T5G_TS_COMMIT): a block
 // that exits early (a finished sampler row) leaves the previous record intact
 #define T5G_TS_START() const unsigned long long t5g_ts0_ = __builtin_amdgcn_s_memrealtime()
@@ -312,6 +321,7 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_s a, bf16x8_s b, f32x4 c) {
 #else
 #define T5G_TS_UNIT(unit)
 #define T5G_TS(k) do { } while (0)
+#define T5G_TS_BY(k, tid) do { } while (0)
 #define T5G_TS_START() do { } while (0)
 #define T5G_TS_COMMIT() do { } while (0)
 #endif

@@ -680,9 +680,12 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         if (sq < 2) {
             const int nu_q = (a.NGq - jq + qper - 1) / qper;
             bf16x8_s wq[2][3];
+            // every wave's weights first, the poller's too: they were requested ~5 us before
+            // N1 completes, so its poll is not held back by them, and wave 0's share no
+            // longer starts only when the hand-off is seen
+            fb_issue<FM_NW, 3, 2>(wq, a.Wq, a.NGq, d / 32, sq * 36, 36, jq, qper, nu_q);
             if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N1, (unsigned)M, tmo, 1u);
             T5G_TS(1);
-            fb_issue<FM_NW, 3, 2>(wq, a.Wq, a.NGq, d / 32, sq * 36, 36, jq, qper, nu_q);
             fb_finish<FM_NW, EPI_F32, 3, 2, 2>(wq, jq, qper, nu_q, sq * 36, 36, a.xn1, d, M * d * 2, M,
                                                a.qslab + (long)sq * M * a.q_dim, a.q_dim, M * a.q_dim * 4, a.q_dim,
                                                red);
@@ -695,18 +698,18 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         }
     }
 
-    // waves 8-11 of the workers that run no attention request the run's last gate/up unit
-    // into LDS: 18 x 1 KiB each, no registers, while the attention workers run A (on an
+    // waves 8-10 of the workers that run no attention request the run's last gate/up unit
+    // into LDS: 24 x 1 KiB each, no registers, while the attention workers run A (on an
     // attention worker the copies would queue ahead of its q loads). O's publish drains
     // them (vmcnt); its barrier makes them visible to the other waves.
-    if (gu_lds && wave >= 8) {
+    if (gu_lds && wave >= 8 && wave < 11) {
         const int wv = __builtin_amdgcn_readfirstlane(wave - 8);
         const __amdgpu_buffer_rsrc_t gr = frag_rsrc(a.Wgu, (uint32_t)NGg * (uint32_t)KBg * 1024u);
-        const int gb = ((g_lo + nu_g - 1) * KBg + wv * (FB_GU_KB / 4)) * 1024 + lane * 16;
+        const int gb = ((g_lo + nu_g - 1) * KBg + wv * (FB_GU_KB / 3)) * 1024 + lane * 16;
         __attribute__((address_space(3))) char* dst =
-            (__attribute__((address_space(3))) char*)gul + wv * (FB_GU_KB / 4) * 1024;
+            (__attribute__((address_space(3))) char*)gul + wv * (FB_GU_KB / 3) * 1024;
 #pragma unroll
-        for (int q = 0; q < FB_GU_KB / 4; ++q)
+        for (int q = 0; q < FB_GU_KB / 3; ++q)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(gr, dst + q * 1024, 16, gb + q * 1024, 0, 0, AUX_NT);
     }
 
@@ -820,9 +823,11 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
 
     // ---- O: cross-o, 4 k-slices of 16 k-steps over nw / 4 workers each (<= 3 units, 8 waves)
     if (owork) {
-        if (wave == 0) ok &= fm_wait_n<8>(a.sync, L_A0, (unsigned)M, tmo, 3u);   // the 8 q heads
-        T5G_TS(2);
+        // waves 0-7 (the GEMV) request their weights first; wave 11, idle in this stage and
+        // with nothing queued, polls the 8 q heads
         if (!(attnwg && wave >= 4)) fb_issue<8, 2, 3>(wo, a.Wo, a.NGo, a.q_dim / 32, so * 16, 16, jo, oper, nu_o);
+        if (wave == FM_NW - 1) ok &= fm_wait_n<8>(a.sync, L_A0, (unsigned)M, tmo, 3u);
+        T5G_TS_BY(2, (FM_NW - 1) * 64);
         fb_finish<8, EPI_F32, 2, 3, 2>(wo, jo, oper, nu_o, so * 16, 16, a.att, a.q_dim, M * a.q_dim * 2, M,
                                        a.oslab + (long)so * M * d, d, M * d * 4, d, red);
         fb_publish(cline(a.sync, L_O0 + (w & 7)), 1u);
@@ -832,10 +837,10 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     // on the workers that fetched it)
     {
         bf16x8_s wg[5][6];
-        if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N2, (unsigned)M, tmo, 5u);
-        T5G_TS(3);
         const int nu_r = gu_lds ? nu_g - 1 : nu_g;
         fb_issue<FM_NW, 6, 5>(wg, a.Wgu, NGg, KBg, 0, KBg, g_lo, 1, nu_r);
+        if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N2, (unsigned)M, tmo, 5u);
+        T5G_TS(3);
         fb_finish<FM_NW, EPI_GEGLU, 6, 5, 0, true>(wg, g_lo, 1, nu_g, 0, KBg, a.xn, d, M * d * 2, M, a.act, f,
                                                    M * f * 2, 2 * f, red, gul, nu_r);
     }
@@ -857,9 +862,9 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
         const int KBd = f / 32, per = KBd / FM_DS;
         const int nu_d = (a.NGd - j + dper - 1) / dper;
         bf16x8_s wd[5][3];
+        fb_issue<FM_NW, 3, 5>(wd, a.Wd, a.NGd, KBd, s * per, per, j, dper, nu_d);
         if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_SL0 + s, (unsigned)units_per_slice, tmo, 6u + s);
         T5G_TS(5);
-        fb_issue<FM_NW, 3, 5>(wd, a.Wd, a.NGd, KBd, s * per, per, j, dper, nu_d);
         fb_finish<FM_NW, EPI_F32, 3, 5, 2>(wd, j, dper, nu_d, s * per, per, a.act, f, M * f * 2, M,
                                            a.dslab + (long)s * M * d, d, M * d * 4, d, red);
         fb_publish(cline(a.sync, L_D0 + (w & 7)), 1u);
@@ -927,7 +932,7 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
         if (a.Wo1 && (!a.att_self || !a.o1slab)) return -1;
         if (a.Wqkv && (!a.qkv_out || a.NGqkv * 16 != a.qkv_dim)) return -1;
         a.norm_b0 = nb - a.M;
-        static_assert(FB_GU_KB == FM_NW * 6 && FB_GU_KB % 4 == 0 && FB_LDS <= FM_LDS_MAX, "gate/up LDS unit");
+        static_assert(FB_GU_KB == FM_NW * 6 && FB_GU_KB % 3 == 0 && FB_LDS <= FM_LDS_MAX, "gate/up LDS unit");
         if (a.d != FB_D) return -1;
         const size_t shm = FB_LDS;
         static bool attr_b = false;
