@@ -394,18 +394,15 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     // NIT V registers are not held through the K stream: <= 128 VGPRs, four workgroups per
     // CU, 1 024 chunk workgroups in one round (32 rows x 4 kv heads x 8 chunks)
     u32x4 kr[NIT], vr[NIT];
-    auto k_issue = [&]() __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < NIT; ++i) {
-            const int j = c0 + i * KPB + wave * KPW + kg;
-            const int off = j < c1 ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
-            kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
-            if constexpr (VFIRST)
-                vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      vrs, single ? off : (int)0x7ffffff0, 0, 0));
-        }
-    };
-    if constexpr (VFIRST) k_issue();
+    for (int i = 0; i < NIT; ++i) {
+        const int j = c0 + i * KPB + wave * KPW + kg;
+        const int off = j < c1 ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
+        kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
+        if constexpr (VFIRST)
+            vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  vrs, single ? off : (int)0x7ffffff0, 0, 0));
+    }
     float q[G][8];
     if (a.Qpart) {
         f32x4 acc = u[0];
@@ -453,9 +450,6 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         }
     }
     if (n <= 0) return;
-    // multi-chunk launches request K only once q is staged (in flight with K, the q-slab
-    // responses queued behind the K stream: q staged at 4.0 instead of 1.5 us)
-    if constexpr (!VFIRST) k_issue();
     u32x4 vt = (u32x4){0u, 0u, 0u, 0u};   // the appended value, for the lane holding key t
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {

@@ -207,6 +207,26 @@ __device__ void finish_row(const SamplerArgs& a, const SamplerRow& pr, SamplerSt
     a.state[b] = st;
 }
 
+// A row's state and parameters read in ONE batch at this point: without the register pins
+// the compiler fetches some fields lazily after later branches (one dependent round trip
+// each) and hoists the `done` test above the logit requests.
+__device__ __forceinline__ void load_row(const SamplerArgs& a, int b, SamplerState& st, SamplerRow& pr) {
+    constexpr int NS = (int)(sizeof(SamplerState) / 4), NR = (int)(sizeof(SamplerRow) / 4);
+    static_assert(sizeof(SamplerState) % 4 == 0 && sizeof(SamplerRow) % 4 == 0, "dword structs");
+    uint32_t ws[NS], wr[NR];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) ws[i] = ((const uint32_t*)(a.state + b))[i];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) wr[i] = ((const uint32_t*)(a.rows + b))[i];
+    asm volatile("" ::: "memory");   // every request above is issued before the first pin
+#pragma unroll
+    for (int i = 0; i < NS; ++i) asm volatile("" : "+v"(ws[i]));
+#pragma unroll
+    for (int i = 0; i < NR; ++i) asm volatile("" : "+v"(wr[i]));
+    __builtin_memcpy(&st, ws, sizeof(st));
+    __builtin_memcpy(&pr, wr, sizeof(pr));
+}
+
 __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
     __shared__ float redv[NW];
     __shared__ int redi[NW];
@@ -222,10 +242,14 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
-    SamplerState st = a.state[b];
+    // fs_slow requested with the state (no branch around the load: any valid address)
+    const int fsv = *(a.fs_slow ? a.fs_slow + b : &a.state[b].done);
+    SamplerState st;
+    SamplerRow pr;
+    load_row(a, b, st, pr);
+    const int slow = a.fs_slow ? fsv : 1;
     if (st.done) return;
-    if (a.fs_slow && !a.fs_slow[b]) return;   // finished by sampler_fast_kernel this step
-    const SamplerRow pr = a.rows[b];
+    if (!slow) return;   // finished by sampler_fast_kernel this step
     const int V = a.V;
     const bf16_t* lg = a.logits + (long)b * a.ldl;
 
@@ -616,10 +640,12 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
     bf16_t raw[FEPT];
 #pragma unroll
     for (int j = 0; j < FEPT; ++j) raw[j] = lg[max(0, min(i0 + tid + FT * j, i1 - 1))];
-    SamplerState st = a.state[b];
+    asm volatile("" ::: "memory");   // the logit requests go out before the row state is read
+    SamplerState st;
+    SamplerRow pr;
+    load_row(a, b, st, pr);
     if (st.done) return;
     T5G_TS_COMMIT();
-    const SamplerRow pr = a.rows[b];
     int kk = pr.top_k;
     if (pr.top_k_list_len > 0) kk = a.top_k_list[pr.top_k_list_off + min(pr.top_k_list_len - 1, st.cur_num_gen)];
     const bool fast = kk > 0 && kk <= FS_KMAX && !(pr.min_p > 0.f && pr.min_p < 1.f);
