@@ -1,8 +1,10 @@
 """The decode MLP half as one persistent launch (csrc/fused.hip: cross-attention residual
 norm -> gate/up GeGLU -> down, with in-launch hand-offs) against the same step as three
 launches (resid_norm + the two register-X GEMVs): tokens and every logit row bitwise equal,
-at the true 2b-2b widths (d 2304, FFN 9216; 2 + 2 layers), for 1, 8 and 32 rows (one and two
-16-row MFMA tiles), and across repeated calls (the hand-off counters reset themselves)."""
+at the true 2b-2b widths (d 2304, FFN 9216; 2 + 2 layers), for 1, 8, 12 and 16 rows (the
+whole-layer launch, one 16-row MFMA tile: 16 rows = 128 attention workers, the most it takes)
+and 32 rows (the MLP-half launch, two tiles), and across repeated calls (the hand-off
+counters reset themselves)."""
 import numpy as np
 import pytest
 import torch
@@ -43,7 +45,7 @@ def _utts(cfg, n, seed):
     return utts
 
 
-@pytest.mark.parametrize("B", [1, 8, 32])
+@pytest.mark.parametrize("B", [1, 8, 12, 16, 32])
 def test_fused_mlp_bitwise_equal_to_three_launches(B):
     _need_gpu()
     from t5gemma_tts_amd.engine import SamplingParams
