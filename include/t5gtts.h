@@ -287,12 +287,19 @@ int t5g_attention_decode(const t5g_attn_decode_args* args, void* stream);
  * the single-block kernel when a row's top-k / survivor set exceeds it; 1 the single-block
  * kernel only. Both pick the same tokens (tests/test_gpu_sampler.py). */
 int t5g_engine_set_sampler_path(t5g_engine* e, int32_t single_block);
-/* Decode MLP half (cross-attention residual norm -> gate/up GeGLU -> down) as one persistent
- * launch with in-launch hand-offs (fused.hip) instead of three launches; bitwise equal.
- * Default on (fast path only: parity mode runs the exact-order kernels). Replaces the
- * reference's T5GemmaMLP call + residual (hf_export/modeling_t5gemma_voice.py:309-323,
- * [tf] modeling_t5gemma.py:81-97); no reference-side equivalent switch. */
+/* Decode step layout (fast path; parity mode runs the exact-order kernels): each decoder
+ * layer after its self attention -- o-projection, norm, cross-q, PM cross attention,
+ * cross-o, norm, gate/up GeGLU, down, norm, the next layer's q|k|v -- as ONE persistent
+ * launch with in-launch hand-offs (fused.hip; 1-16 rows; 17-32 rows fuse the MLP half) or as
+ * per-op launches; bitwise equal. Default on. Computes the reference's PMDecoderLayer
+ * (hf_export/modeling_t5gemma_voice.py:256-323, [tf] modeling_t5gemma.py:81-97); no
+ * reference-side equivalent switch. */
 int t5g_engine_set_fused(t5g_engine* e, int32_t enable);
+/* Test hook: store `code` (non-zero) in the fused launch's sticky timeout word, as a
+ * hand-off that gave up waiting would: every later in-launch wait gives up at once, the next
+ * t5g_read_tokens returns T5G_EHANDOFF and clears the counters (tests/test_gpu_fused.py:
+ * engine.generate then reruns the call on the per-op launches, same tokens). */
+int t5g_engine_poison_handoff(t5g_engine* e, uint32_t code);
 /* Average device time (us, hipEvents on `stream`) of the fused decode-MLP launch at B rows,
  * rotating over the decoder layers (bench.py roofline leg; no reference equivalent). */
 int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us);

@@ -129,6 +129,7 @@ SIGNATURES = {
     "t5g_engine_set_exact": (C.c_int, [_P, _I, _P, _I]),
     "t5g_engine_set_sampler_path": (C.c_int, [_P, _I]),
     "t5g_engine_set_fused": (C.c_int, [_P, _I]),
+    "t5g_engine_poison_handoff": (C.c_int, [_P, C.c_uint32]),
     "t5g_time_decode_mlp": (C.c_int, [_P, _I, _I, _P, C.POINTER(_F)]),
     "t5g_exact_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
     "t5g_exact_attention": (C.c_int, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),

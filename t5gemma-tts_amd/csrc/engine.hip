@@ -1229,6 +1229,14 @@ extern "C" int t5g_read_tokens(t5g_engine* e, int32_t* out, int32_t B, void* str
     return T5G_OK;
 }
 
+extern "C" int t5g_engine_poison_handoff(t5g_engine* e, uint32_t code) {
+    if (!e || !code || !e->fsync) return T5G_EINVAL;
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(e->fsync, &code, sizeof(unsigned), hipMemcpyHostToDevice));
+    HIPCHK(hipDeviceSynchronize());
+    return T5G_OK;
+}
+
 extern "C" int t5g_engine_set_fused(t5g_engine* e, int32_t enable) {
     if (!e) return T5G_EINVAL;
     if (e->fused_mlp != (enable != 0)) {
