@@ -17,6 +17,9 @@ def main():
     R = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     Bs = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [12, 16, 8]
     cfg, eng = _mid_engine(32)
+    if os.environ.get("DET_SAMPLER_SINGLE"):   # the single-block sampler kernel only
+        from t5gemma_tts_amd import _lib
+        _lib.check(_lib.lib().t5g_engine_set_sampler_path(eng.h, 1), "set_sampler_path")
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
     for B in Bs:
         utts = _utts(cfg, B, 40 + B)
