@@ -243,8 +243,12 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
 }
 
 // ---------------------------------------------------------------------------
+// The engine's own encoder / prefill GEMMs run the register ring (pf_reg defaults to true):
+// in the engine the LDS-staged kernel made the last token tile's sums vary from run to run
+// (tools/diag_det_logits.py); the register ring does not. t5g_gemm's
+// T5G_GEMM_PREFILL still selects the LDS kernel (probes, PMC passes).
 static int gemm(const bf16_t* X, int ldx, int M, const void* W, int N, int K, int splits, const void* bias,
-                void* Y, int ldy, int epi, hipStream_t st, bool prefill = false, bool pf_reg = false) {
+                void* Y, int ldy, int epi, hipStream_t st, bool prefill = false, bool pf_reg = true) {
     GemmArgs a;
     memset(&a, 0, sizeof(a));
     a.prefill = prefill ? (pf_reg ? 2 : 1) : 0;

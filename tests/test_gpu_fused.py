@@ -46,9 +46,9 @@ def _utts(cfg, n, seed):
 
 
 _RARE = pytest.mark.xfail(strict=False, reason=(
-    "known issue: at 12 and 16 rows a rare run-to-run token difference in the batch's last row "
-    "(about 1 run in 8, per-op and fused layouts alike, tools/diag_fused_det.py); under "
-    "investigation, DESIGN.md section 4.1"))
+    "a rare run-to-run token difference in the batch's last row at 12 / 16 rows, traced to the "
+    "LDS-staged prefill GEMM (the engine now runs the register ring; DESIGN.md section 4.1); "
+    "kept non-strict until more runs confirm the fix"))
 
 
 @pytest.mark.parametrize("B", [1, 8, pytest.param(12, marks=_RARE), pytest.param(16, marks=_RARE), 32])
