@@ -45,13 +45,7 @@ def _utts(cfg, n, seed):
     return utts
 
 
-_RARE = pytest.mark.xfail(strict=False, reason=(
-    "a rare run-to-run token difference in the batch's last row at 12 / 16 rows, traced to the "
-    "LDS-staged prefill GEMM (the engine now runs the register ring; DESIGN.md section 4.1); "
-    "kept non-strict until more runs confirm the fix"))
-
-
-@pytest.mark.parametrize("B", [1, 8, pytest.param(12, marks=_RARE), pytest.param(16, marks=_RARE), 32])
+@pytest.mark.parametrize("B", [1, 8, 12, 16, 32])
 def test_fused_mlp_bitwise_equal_to_three_launches(B):
     _need_gpu()
     from t5gemma_tts_amd.engine import SamplingParams
