@@ -326,6 +326,23 @@ int t5g_engine_set_exact(t5g_engine* e, int32_t enable, const uint16_t* gelu_lut
 int t5g_exact_linear(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K,
                      int32_t kb32, const void* bias_dev, const void* gelu_lut_dev, void* Y_dev, int32_t ldy,
                      int32_t epi, void* stream);
+/* The same exact-order Linear on the f32-input MFMA kernels the engine's parity mode runs
+ * (csrc/xmm.hip: v_mfma_f32_16x16x4_f32 chains = the reference's E/O chunk chains); same
+ * arguments and results as t5g_exact_linear, bit for bit. */
+int t5g_xmm_linear(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K,
+                   int32_t kb32, const void* bias_dev, const void* gelu_lut_dev, void* Y_dev, int32_t ldy,
+                   int32_t epi, void* stream);
+/* The parity Linears' operand layouts (csrc/xmm.hip): the E16 image of a P16-packed weight
+ * (bytes = t5g_packed_bytes(N, K)), the X16 image of bf16 rows X [M][ldx] (K columns,
+ * ceil(M / 16) * 16 * K elements). */
+int t5g_pack_e16(const void* p16_dev, void* e16_dev, int64_t bytes, void* stream);
+int t5g_to_x16(const void* X_dev, int32_t ldx, int32_t M, int32_t K, void* Y16_dev, void* stream);
+/* hipEvent-timed f32-MFMA Linear launches on E16 weights W16_list[i % n_w] (rotated to
+ * stream from HBM as in a decode step); epi as t5g_gemm, | 0x1000: Y is an X16 output.
+ * Average microseconds per launch in *avg_us (kernel probes, bench roofline). */
+int t5g_time_xmm(const void* X16_dev, int32_t M, const void* const* W16_list, int32_t n_w, int32_t N, int32_t K,
+                 int32_t epi, const void* bias_dev, void* Y_dev, int32_t ldy, int32_t iters, void* stream,
+                 float* avg_us);
 /* Single exact-order SDPA call on caller buffers (parity tests): one reference call per row b
  * with q_len[b] queries (q rows packed, q_row / q_pos per query) over kv_len[b] keys of a
  * [B][n_kv_heads][cap][head_dim] cache, torch 2.10 CPU flash-attention numerics incl. its
@@ -334,6 +351,30 @@ int t5g_exact_attention(const void* q_dev, int32_t Mq, const int32_t* q_row_dev,
                         const int32_t* q_len_dev, const void* k_cache_dev, const void* v_cache_dev, int32_t cap,
                         const int32_t* kv_len_dev, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
                         int32_t causal, int32_t window, float scale, int32_t threads, void* out_dev, void* stream);
+
+/* --- parity-mode noise on the device (csrc/noise.hip) --------------------------------
+ * The reference's torch.multinomial draws V exponential variates per step from torch's CPU
+ * generator (MT19937; hf_export/modeling_t5gemma_voice.py:133-138, SURVEY a14' 6). Replaces
+ * drawing them with torch on the host (engine.reference_noise):
+ * t5g_mt_stream: one MT19937 stream per row from init_dev [B][625] (624 state words + the
+ * outputs of that state already consumed, 1..624 -- torch's `left` = 625 - pos), outputs
+ * [0, n_out) of row b to out_dev[b * out_stride ...] (uint32), and if snap_dev != NULL the
+ * generator after every snap_every outputs (s < n_snap) to snap_dev [B][n_snap][625].
+ * Step s of a row uses outputs [2 V s, 2 V (s + 1)): draw i = (out[2i] << 32 | out[2i+1]).
+ * t5g_mt_exponential: q = bf16(float(-log1p(-u))) of n draws (raw pairs) into bf16 q_dev
+ * (tests: equal to torch's exponential_). t5g_engine_set_noise_mt: the engine's parity
+ * sampler reads its draws from raw_dev [max_batch][steps][2 V] (NULL: off). */
+int t5g_mt_stream(const uint32_t* init_dev, int32_t B, int64_t n_out, int64_t out_stride, uint32_t* out_dev,
+                  int64_t snap_every, int32_t n_snap, uint32_t* snap_dev, void* stream);
+int t5g_mt_exponential(const uint32_t* raw_dev, int64_t n, void* q_dev, void* stream);
+int t5g_engine_set_noise_mt(t5g_engine* e, const uint32_t* raw_dev, int32_t steps);
+/* Host build of the sampler's sparse emulation of torch.sort's tie order (csrc/sort_emu.h;
+ * replaces the reference's torch.sort in top_k_top_p_filtering, :107-108, for the order of
+ * the survivors only): S survivors at ascending slots pos[] with values val[] in an array of
+ * n otherwise -inf entries; on return the three arrays are ordered by final slot (pos[] the
+ * final slots). T5G_EUNSUPPORTED where the emulation does not follow std::sort (heapsort
+ * fallback, NaN); pure host function. */
+int t5g_sort_emu(int32_t n, int32_t S, int32_t* pos, float* val, int32_t* tag);
 
 #ifdef __cplusplus
 }

@@ -132,7 +132,15 @@ SIGNATURES = {
     "t5g_engine_poison_handoff": (C.c_int, [_P, C.c_uint32]),
     "t5g_time_decode_mlp": (C.c_int, [_P, _I, _I, _P, C.POINTER(_F)]),
     "t5g_exact_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
+    "t5g_xmm_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
+    "t5g_pack_e16": (C.c_int, [_P, _P, _L, _P]),
+    "t5g_to_x16": (C.c_int, [_P, _I, _I, _I, _P, _P]),
+    "t5g_time_xmm": (C.c_int, [_P, _I, C.POINTER(_P), _I, _I, _I, _I, _P, _P, _I, _I, _P, C.POINTER(_F)]),
     "t5g_exact_attention": (C.c_int, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
+    "t5g_mt_stream": (C.c_int, [_P, _I, _L, _L, _P, _L, _I, _P, _P]),
+    "t5g_mt_exponential": (C.c_int, [_P, _L, _P, _P]),
+    "t5g_engine_set_noise_mt": (C.c_int, [_P, _P, _I]),
+    "t5g_sort_emu": (C.c_int, [_I, _I, _P, _P, _P]),
 }
 
 # parity mode: the reference host's bf16 nn.GELU() (erf) table (tools/cpu_order/make_gelu_table.py)

@@ -16,8 +16,8 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "lib", "libt5gtts.so")
-SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "fused.hip", "exact.hip", "xc2.hip", "xc2enc.hip", "whisper.hip", "host_sampler.cpp"]
-HEADERS = ["common.h", "t5g_kernels.h", "xc2_common.h", "exact_math.h", "ref_ksplit.h"]
+SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "fused.hip", "exact.hip", "xmm.hip", "xattn.hip", "noise.hip", "xc2.hip", "xc2enc.hip", "whisper.hip", "host_sampler.cpp"]
+HEADERS = ["common.h", "t5g_kernels.h", "xc2_common.h", "exact_math.h", "ref_ksplit.h", "sort_emu.h"]
 ARCH = os.environ.get("T5G_ARCH", "gfx950")
 # -ffp-contract=off: HIP's default (fast-honor-pragmas) fuses a*b+c into one fma even
 # through __fmul_rn / __fsub_rn, which changes roundings the reference's CPU kernels keep
@@ -46,8 +46,9 @@ def _compile(src: str, force: bool, dbg: bool = False) -> str:
         return o
     cmd = [_hipcc()] + FLAGS + (["-DT5G_DBG_TS=1"] if dbg else []) + ["-c", s, "-o", o]
     if src.endswith(".cpp"):
-        cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-I",
-               os.path.join(REPO, "include"), "-c", s, "-o", o]
+        # host-only C++ (the parity host sampler, the host build of csrc/sort_emu.h): g++
+        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-I",
+               os.path.join(REPO, "include"), "-I", CSRC, "-c", s, "-o", o]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
@@ -71,6 +72,21 @@ def build(force: bool = False, verbose: bool = True, dbg: bool = False) -> str:
         if verbose:
             print(f"[t5gtts] built {lib}")
     return lib
+
+
+ORACLE_SRC = os.path.join(REPO, "oracle", "sort_order.cpp")
+ORACLE_LIB = os.path.join(REPO, "oracle", "lib", "liboracle_sort.so")
+
+
+def build_oracle(force: bool = False) -> str:
+    """Compile the oracle's C++ restatements (test infrastructure, g++) into oracle/lib/."""
+    os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
+    if force or not os.path.exists(ORACLE_LIB) or os.path.getmtime(ORACLE_LIB) < os.path.getmtime(ORACLE_SRC):
+        r = subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", ORACLE_LIB, ORACLE_SRC],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"oracle build failed:\n{r.stderr[-4000:]}")
+    return ORACLE_LIB
 
 
 if __name__ == "__main__":

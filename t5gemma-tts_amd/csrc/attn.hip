@@ -100,8 +100,6 @@ int rope_store(const RopeArgs& a, hipStream_t st) {
 // exp on each block's 16-multiple prefix, lane-ordered sums, bf16 P before P.V, output
 // scaled by 1/l; a causal row t sees its q-block's key range (sdpa_qsplit). ``eager``
 // mirrors eager_attention_forward (bf16 scores, tanh softcap, bf16 normalised probs).
-constexpr int SDPA_KV_BLOCK = 512;
-constexpr int SDPA_MAX_BLOCKS = 8;   // kv_cap <= 4096
 
 template <int D, int G, bool EAGER>
 __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {

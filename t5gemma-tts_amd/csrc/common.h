@@ -47,6 +47,16 @@ __device__ __forceinline__ f32x2 rbf2(f32x2 x) {
     return (f32x2){__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
 }
 
+// Parity-mode noise: q of one multinomial draw from its two raw MT19937 outputs (hi
+// first), as torch's CPU exponential_ (lambda 1) makes it: 53-bit uniform u, then
+// -log1p(-u) in double, cast to float, then to bf16 (noise.hip)
+__device__ __forceinline__ float mt_exp_q(uint32_t hi, uint32_t lo) {
+    const uint64_t r = ((uint64_t)hi << 32) | lo;
+    const double u = (double)(r & ((1ull << 53) - 1)) * 0x1.0p-53;
+    const double x = -1.0 * log1p(-u);
+    return rbf((float)x);
+}
+
 // sc1 (write-through store / L1-bypassing load) accessors for in-launch cross-workgroup
 // hand-offs (relaxed agent-scope atomics lower to global_store / global_load ... sc1; the
 // gfx950 form the file header describes)

@@ -88,6 +88,8 @@ struct t5g_engine {
     int B = 0;            // rows of the current call
     const bf16_t* noise = nullptr;
     int noise_steps = 0;
+    const uint32_t* noise_mt = nullptr;   // parity mode: raw MT19937 outputs [B][noise_mt_steps][2 V] (noise.hip)
+    int noise_mt_steps = 0;
     // graphs of one and of GRAPH_STEPS decode iterations (a replay boundary costs
     // ~10 us; back-to-back iterations inside one graph only the kernel boundaries)
     hipGraph_t graph = nullptr, graph_n = nullptr;
@@ -104,6 +106,16 @@ struct t5g_engine {
     int exact_threads = REF_KSPLIT_THREADS;
     uint16_t* ksplit_dev = nullptr;     // ref_ksplit.h tables [REF_KSPLIT_NSHAPES][REF_KSPLIT_MAX_M]
     uint16_t* gelu_lut_dev = nullptr;   // [65536] bf16 -> bf16 nn.GELU() of the reference host
+    // parity mode's Linears on the f32 MFMA (xmm.hip): E16 copies of the packed weights
+    // (made once, at the first t5g_engine_set_exact) and X16 activation buffers
+    struct XLayer {
+        bf16_t *qkv, *o, *gate_up, *down, *cross_q, *cross_kv, *cross_o;
+    };
+    std::vector<XLayer> enc_x, dec_x;
+    bf16_t *head1_x = nullptr, *head2_x = nullptr;
+    bf16_t *xn16 = nullptr, *att16 = nullptr, *act16 = nullptr, *mem16 = nullptr;   // packed tokens
+    bf16_t *dxn16 = nullptr, *datt16 = nullptr, *dact16 = nullptr, *dhh16 = nullptr;   // decode rows
+    bool xmm_ready = false;
 };
 
 template <typename T>
@@ -318,9 +330,36 @@ static const uint16_t* ksplit_tab(const t5g_engine* e, int N, int K) {
     return nullptr;   // shapes never split by the reference host (K <= 256 in the probes)
 }
 
+// Exact Linear on the f32 MFMA: X16 operand, E16 weights; Y row-major and / or Y16.
 // nref_a / nref_b: the reference Linear's output width for packed columns < / >= nsplit_col
 // (q | k,v share one packed matrix here but are separate F.linear calls there)
-static int xlin(t5g_engine* e, const bf16_t* X, int ldx, int M, const void* W, int N, int K, const void* bias,
+static int xlin16(t5g_engine* e, const bf16_t* X16, int M, const bf16_t* W16, int N, int K, const void* bias,
+                  void* Y, int ldy, bf16_t* Y16, int epi, const int* tok_row, const int* row_len, int nref_a,
+                  int nref_b, int nsplit_col, hipStream_t st) {
+    XmmArgs a;
+    memset(&a, 0, sizeof(a));
+    a.X16 = X16;
+    a.M = M;
+    a.W = W16;
+    a.N = N;
+    a.NG = ng_pad(N);
+    a.KB = K / 32;
+    a.bias = (const bf16_t*)bias;
+    a.Y = Y;
+    a.ldy = ldy;
+    a.Y16 = Y16;
+    a.tok_row = tok_row;
+    a.row_len = row_len;
+    a.kb_a = ksplit_tab(e, nref_a, K);
+    a.kb_b = nref_b ? ksplit_tab(e, nref_b, K) : nullptr;
+    a.nsplit_col = nsplit_col;
+    a.kb_len = REF_KSPLIT_MAX_M;
+    a.gelu_lut = e->gelu_lut_dev;
+    return xmm(a, epi, st);
+}
+
+// VALU exact Linear (exact.hip), kept for the A/B entry point t5g_exact_linear
+[[maybe_unused]] static int xlin(t5g_engine* e, const bf16_t* X, int ldx, int M, const void* W, int N, int K, const void* bias,
                 void* Y, int ldy, int epi, const int* tok_row, const int* row_len, int nref_a, int nref_b,
                 int nsplit_col, hipStream_t st) {
     ExactLinArgs a;
@@ -347,7 +386,7 @@ static int xlin(t5g_engine* e, const bf16_t* X, int ldx, int M, const void* W, i
 
 static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const int* q_pos, const int* q_len,
                  const bf16_t* K, const bf16_t* Vc, int cap, const int* kv_len, int causal, int window, bf16_t* O,
-                 hipStream_t st) {
+                 bf16_t* O16, hipStream_t st) {
     const t5g_config& c = e->c;
     ExactAttnArgs a;
     memset(&a, 0, sizeof(a));
@@ -371,6 +410,12 @@ static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const
     a.threads = e->exact_threads;
     a.O = O;
     a.ldo = e->q_dim;
+    a.O16 = O16;
+    // decode rows (one query each): the scores + P.V launches of xattn.hip
+    if (!q_pos && !q_len) {
+        const int rc = exact_attention_decode(a, e->asbuf, e->ambuf, cap, st);
+        if (rc != -3) return rc;   // -3: a head shape the decode kernels are not built for
+    }
     return exact_attention(a, st);
 }
 
@@ -406,6 +451,7 @@ static int encode_exact(t5g_engine* e, int ntok, const int32_t* ids, const int32
     const int* rl = e->enc_len;   // the reference encodes one utterance: M = its text length
     for (int l = 0; l < c.n_enc_layers; ++l) {
         const t5g_layer_weights& L = e->enc[l];
+        const t5g_engine::XLayer& X = e->enc_x[l];
         NormArgs n = xnorm_args(ntok, d, c.rms_eps);
         if (l == 0) {
             n.ids = ids;
@@ -420,9 +466,10 @@ static int encode_exact(t5g_engine* e, int ntok, const int32_t* ids, const int32
         n.pre_w = (const bf16_t*)L.norms[0];
         n.resid_out = e->h;
         n.normed_out = e->xn;
+        n.normed_x16 = e->xn16;
         RC(resid_norm(n, st));
-        RC(xlin(e, e->xn, d, ntok, L.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, EPI_BF16, tok_row, rl, e->q_dim,
-                e->kv_dim, e->q_dim, st));
+        RC(xlin16(e, e->xn16, ntok, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
+                  e->q_dim, e->kv_dim, e->q_dim, st));
         RopeArgs r = xrope_args(ntok, D, pos, e->w.inv_freq, tok_row, tok_t, nullptr);
         r.X = e->qkv;
         r.ldx = e->qkv_dim;
@@ -437,8 +484,9 @@ static int encode_exact(t5g_engine* e, int ntok, const int32_t* ids, const int32
         r.c_bstride = r.c_hstride * c.n_kv_heads;
         RC(rope_store(r, st));
         RC(xattn(e, e->q, ntok, tok_row, tok_t, rl, e->enc_k, e->enc_v, c.max_text, rl, 0,
-                 c.enc_sliding[l] ? c.sliding_window : 0, e->att, st));
-        RC(xlin(e, e->att, e->q_dim, ntok, L.o, d, e->q_dim, nullptr, e->tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+                 c.enc_sliding[l] ? c.sliding_window : 0, e->att, e->att16, st));
+        RC(xlin16(e, e->att16, ntok, X.o, d, e->q_dim, nullptr, e->tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0,
+                  st));
         n = xnorm_args(ntok, d, c.rms_eps);
         n.delta = e->tmp;
         n.post_w = (const bf16_t*)L.norms[1];
@@ -446,9 +494,11 @@ static int encode_exact(t5g_engine* e, int ntok, const int32_t* ids, const int32
         n.pre_w = (const bf16_t*)L.norms[4];
         n.resid_out = e->h;
         n.normed_out = e->xn;
+        n.normed_x16 = e->xn16;
         RC(resid_norm(n, st));
-        RC(xlin(e, e->xn, d, ntok, L.gate_up, 2 * f, d, nullptr, e->act, f, EPI_GEGLU, tok_row, rl, f, 0, 0, st));
-        RC(xlin(e, e->act, f, ntok, L.down, d, f, nullptr, e->tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+        RC(xlin16(e, e->xn16, ntok, X.gate_up, 2 * f, d, nullptr, nullptr, f, e->act16, EPI_GEGLU, tok_row, rl, f, 0,
+                  0, st));
+        RC(xlin16(e, e->act16, ntok, X.down, d, f, nullptr, e->tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0, st));
     }
     NormArgs n = xnorm_args(ntok, d, c.rms_eps);
     n.delta = e->tmp;
@@ -457,10 +507,11 @@ static int encode_exact(t5g_engine* e, int ntok, const int32_t* ids, const int32
     n.pre_w = (const bf16_t*)e->w.enc_final_norm;
     n.resid_out = e->h;
     n.normed_out = e->mem;
+    n.normed_x16 = e->mem16;
     RC(resid_norm(n, st));
     for (int l = 0; l < c.n_dec_layers; ++l) {
-        RC(xlin(e, e->mem, d, ntok, e->dec[l].cross_kv, 2 * e->kv_dim, d, nullptr, e->qkv, 2 * e->kv_dim, EPI_BF16,
-                tok_row, rl, e->kv_dim, e->kv_dim, e->kv_dim, st));
+        RC(xlin16(e, e->mem16, ntok, e->dec_x[l].cross_kv, 2 * e->kv_dim, d, nullptr, e->qkv, 2 * e->kv_dim, nullptr,
+                  EPI_BF16, tok_row, rl, e->kv_dim, e->kv_dim, e->kv_dim, st));
         RopeArgs r = xrope_args(ntok, D, pos, e->w.inv_freq, tok_row, tok_t, nullptr);
         r.X = e->qkv;
         r.ldx = 2 * e->kv_dim;
@@ -483,9 +534,11 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
     const int d = c.hidden, f = c.intermediate, D = c.head_dim;
     bf16_t* h = decode ? e->dh : e->h;
     bf16_t* xn = decode ? e->dxn : e->xn;
+    bf16_t* xn16 = decode ? e->dxn16 : e->xn16;
     bf16_t* q = decode ? e->dq : e->q;
     bf16_t* att = decode ? e->datt : e->att;
-    bf16_t* act = decode ? e->dact : e->act;
+    bf16_t* att16 = decode ? e->datt16 : e->att16;
+    bf16_t* act16 = decode ? e->dact16 : e->act16;
     bf16_t* tmp = e->tmp;
     const int* rl = decode ? nullptr : e->kv_len;
     const int* qlen = decode ? nullptr : e->kv_len;
@@ -497,11 +550,12 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         n.pre_w = (const bf16_t*)pre_w;
         n.resid_out = h;
         n.normed_out = xn;
+        n.normed_x16 = xn16;
         return resid_norm(n, st);
     };
-    bool qkv_done = false;   // the previous layer's fused block projected this layer's q|k|v
     for (int l = 0; l < c.n_dec_layers; ++l) {
         const t5g_layer_weights& L = e->dec[l];
+        const t5g_engine::XLayer& X = e->dec_x[l];
         if (l == 0) {
             NormArgs n = xnorm_args(M, d, c.rms_eps);
             n.ids = ids;
@@ -511,11 +565,12 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
             n.pre_w = (const bf16_t*)L.norms[0];
             n.resid_out = h;
             n.normed_out = xn;
+            n.normed_x16 = xn16;
             RC(resid_norm(n, st));
         }
         // self attention
-        RC(xlin(e, xn, d, M, L.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, EPI_BF16, tok_row, rl, e->q_dim,
-                e->kv_dim, e->q_dim, st));
+        RC(xlin16(e, xn16, M, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
+                  e->q_dim, e->kv_dim, e->q_dim, st));
         RopeArgs r = xrope_args(M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
         r.X = e->qkv;
         r.ldx = e->qkv_dim;
@@ -530,11 +585,12 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         r.c_bstride = r.c_hstride * c.n_kv_heads;
         RC(rope_store(r, st));
         RC(xattn(e, q, M, tok_row, tok_t, qlen, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1,
-                 c.dec_sliding[l] ? c.sliding_window : 0, att, st));
-        RC(xlin(e, att, e->q_dim, M, L.o, d, e->q_dim, nullptr, tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+                 c.dec_sliding[l] ? c.sliding_window : 0, att, att16, st));
+        RC(xlin16(e, att16, M, X.o, d, e->q_dim, nullptr, tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0, st));
         RC(norm(L.norms[1], L.norms[2]));
         // PM cross attention
-        RC(xlin(e, xn, d, M, L.cross_q, e->q_dim, d, nullptr, q, e->q_dim, EPI_BF16, tok_row, rl, e->q_dim, 0, 0, st));
+        RC(xlin16(e, xn16, M, X.cross_q, e->q_dim, d, nullptr, q, e->q_dim, nullptr, EPI_BF16, tok_row, rl, e->q_dim, 0,
+                  0, st));
         r = xrope_args(M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
         r.X = q;
         r.ldx = e->q_dim;
@@ -543,25 +599,77 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         r.Qout = q;
         r.ldq = e->q_dim;
         RC(rope_store(r, st));
-        RC(xattn(e, q, M, tok_row, tok_t, qlen, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, st));
-        RC(xlin(e, att, e->q_dim, M, L.cross_o, d, e->q_dim, nullptr, tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+        RC(xattn(e, q, M, tok_row, tok_t, qlen, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, att16, st));
+        RC(xlin16(e, att16, M, X.cross_o, d, e->q_dim, nullptr, tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0, st));
         RC(norm(L.norms[3], L.norms[4]));
-        // GeGLU MLP
-        RC(xlin(e, xn, d, M, L.gate_up, 2 * f, d, nullptr, act, f, EPI_GEGLU, tok_row, rl, f, 0, 0, st));
-        RC(xlin(e, act, f, M, L.down, d, f, nullptr, tmp, d, EPI_BF16, tok_row, rl, d, 0, 0, st));
+        // GeGLU MLP: act straight into the down projection's operand order
+        RC(xlin16(e, xn16, M, X.gate_up, 2 * f, d, nullptr, nullptr, f, act16, EPI_GEGLU, tok_row, rl, f, 0, 0, st));
+        RC(xlin16(e, act16, M, X.down, d, f, nullptr, tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0, st));
         const bool last = l == c.n_dec_layers - 1;
         RC(norm(L.norms[5], last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]));
     }
     return T5G_OK;
 }
 
-static int head_exact(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st) {
+// xn_rows16: the final-normed rows in X16 (decode: dxn16; prefill: the gathered last rows)
+static int head_exact(t5g_engine* e, const bf16_t* xn_rows16, int B, hipStream_t st) {
     const t5g_config& c = e->c;
     const int d = c.hidden;
-    RC(xlin(e, xn_rows, d, B, e->w.head1, d, d, e->w.head1_bias, e->dhh, d, EPI_BIAS_GELU, nullptr, nullptr, d, 0, 0,
-            st));
-    RC(xlin(e, e->dhh, d, B, e->w.head2, e->V, d, e->w.head2_bias, e->logits, e->logits_ld, EPI_BIAS_BF16, nullptr,
-            nullptr, e->V, 0, 0, st));
+    RC(xlin16(e, xn_rows16, B, e->head1_x, d, d, e->w.head1_bias, nullptr, d, e->dhh16, EPI_BIAS_GELU, nullptr,
+              nullptr, d, 0, 0, st));
+    RC(xlin16(e, e->dhh16, B, e->head2_x, e->V, d, e->w.head2_bias, e->logits, e->logits_ld, nullptr, EPI_BIAS_BF16,
+              nullptr, nullptr, e->V, 0, 0, st));
+    return T5G_OK;
+}
+
+// E16 copies of every packed weight + the X16 activation buffers (first switch to parity mode)
+static int xmm_prepare(t5g_engine* e) {
+    if (e->xmm_ready) return T5G_OK;
+    const t5g_config& c = e->c;
+    const int d = c.hidden, f = c.intermediate;
+    hipStream_t st = nullptr;
+    auto copy = [&](const void* p16, int N, int K, bf16_t** out) -> int {
+        const int64_t bytes = (int64_t)ng_pad(N) * 16 * K * 2;
+        RC(alloc(e, out, bytes / 2));
+        RC(pack_e16((const bf16_t*)p16, *out, (long)bytes, st));
+        return T5G_OK;
+    };
+    e->enc_x.assign(c.n_enc_layers, t5g_engine::XLayer{});
+    e->dec_x.assign(c.n_dec_layers, t5g_engine::XLayer{});
+    for (int l = 0; l < c.n_enc_layers; ++l) {
+        const t5g_layer_weights& L = e->enc[l];
+        t5g_engine::XLayer& X = e->enc_x[l];
+        RC(copy(L.qkv, e->qkv_dim, d, &X.qkv));
+        RC(copy(L.o, d, e->q_dim, &X.o));
+        RC(copy(L.gate_up, 2 * f, d, &X.gate_up));
+        RC(copy(L.down, d, f, &X.down));
+    }
+    for (int l = 0; l < c.n_dec_layers; ++l) {
+        const t5g_layer_weights& L = e->dec[l];
+        t5g_engine::XLayer& X = e->dec_x[l];
+        RC(copy(L.qkv, e->qkv_dim, d, &X.qkv));
+        RC(copy(L.o, d, e->q_dim, &X.o));
+        RC(copy(L.gate_up, 2 * f, d, &X.gate_up));
+        RC(copy(L.down, d, f, &X.down));
+        RC(copy(L.cross_q, e->q_dim, d, &X.cross_q));
+        RC(copy(L.cross_kv, 2 * e->kv_dim, d, &X.cross_kv));
+        RC(copy(L.cross_o, d, e->q_dim, &X.cross_o));
+    }
+    RC(copy(e->w.head1, d, d, &e->head1_x));
+    RC(copy(e->w.head2, e->V, d, &e->head2_x));
+    const int64_t T16 = ((int64_t)e->max_tok + 15) / 16 * 16;
+    const int64_t B16 = ((int64_t)c.max_batch + 15) / 16 * 16;
+    const int64_t X16T = ((int64_t)c.max_batch * c.max_text + 15) / 16 * 16;
+    RC(alloc(e, &e->xn16, T16 * d));
+    RC(alloc(e, &e->att16, T16 * e->q_dim));
+    RC(alloc(e, &e->act16, T16 * f));
+    RC(alloc(e, &e->mem16, X16T * d));
+    RC(alloc(e, &e->dxn16, B16 * d));
+    RC(alloc(e, &e->datt16, B16 * e->q_dim));
+    RC(alloc(e, &e->dact16, B16 * f));
+    RC(alloc(e, &e->dhh16, B16 * d));
+    HIPCHK(hipDeviceSynchronize());
+    e->xmm_ready = true;
     return T5G_OK;
 }
 
@@ -574,6 +682,7 @@ extern "C" int t5g_engine_set_exact(t5g_engine* e, int32_t enable, const uint16_
     }
     if (threads != REF_KSPLIT_THREADS) return T5G_EUNSUPPORTED;   // the only measured K-split table
     if (e->c.softcap > 0.f) return T5G_EUNSUPPORTED;   // eager attention (softcap): not restated
+    RC(xmm_prepare(e));
     if (!e->ksplit_dev) {
         RC(alloc(e, &e->ksplit_dev, (int64_t)REF_KSPLIT_NSHAPES * REF_KSPLIT_MAX_M));
         HIPCHK(hipMemcpy(e->ksplit_dev, ref_ksplit_kb32, sizeof(ref_ksplit_kb32), hipMemcpyHostToDevice));
@@ -1040,11 +1149,11 @@ static DecGemmArgs dec_args(int M, const void* W, int N, int K, void* Y, int ldy
 
 // one decoder step + predict head for the e->B rows fed by the sampler buffers
 static int head(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st);
-static int head_exact(t5g_engine* e, const bf16_t* xn_rows, int B, hipStream_t st);
+static int head_exact(t5g_engine* e, const bf16_t* xn_rows16, int B, hipStream_t st);
 static int decode_forward(t5g_engine* e, hipStream_t st) {
     if (e->exact) {
         RC(decoder_pass_exact(e, e->B, e->next_token, nullptr, nullptr, e->next_pos, true, st));
-        return head_exact(e, e->dxn, e->B, st);
+        return head_exact(e, e->dxn16, e->B, st);
     }
     int rc = decoder_pass(e, e->B, e->next_token, nullptr, nullptr, e->next_pos, true, st);
     if (rc) return rc;
@@ -1097,7 +1206,11 @@ extern "C" int t5g_prefill(t5g_engine* e, int32_t B, int32_t ntok, const int32_t
     n.out_rows = e->last_rows;
     n.resid_out = e->dxn;
     RC(resid_norm(n, st));
-    return e->exact ? head_exact(e, e->dxn, B, st) : head(e, e->dxn, B, st);
+    if (e->exact) {
+        RC(to_x16(e->dxn, c.hidden, B, c.hidden, e->dxn16, st));
+        return head_exact(e, e->dxn16, B, st);
+    }
+    return head(e, e->dxn, B, st);
 }
 
 extern "C" int t5g_sampler_setup(t5g_engine* e, int32_t B, const t5g_sampler_row* rows, const t5g_sampler_state* init,
@@ -1125,6 +1238,26 @@ extern "C" int t5g_sampler_setup(t5g_engine* e, int32_t B, const t5g_sampler_row
     return T5G_OK;
 }
 
+extern "C" int t5g_engine_set_noise_mt(t5g_engine* e, const uint32_t* raw, int32_t steps) {
+    if (!e || (raw && steps <= 0)) return T5G_EINVAL;
+    if (!raw) steps = 0;
+    if (e->noise_mt != raw || e->noise_mt_steps != steps) drop_graphs(e);   // baked into the captured graphs
+    e->noise_mt = raw;
+    e->noise_mt_steps = steps;
+    return T5G_OK;
+}
+
+extern "C" int t5g_mt_stream(const uint32_t* init, int32_t B, int64_t n_out, int64_t out_stride, uint32_t* out,
+                             int64_t snap_every, int32_t n_snap, uint32_t* snap, void* stream) {
+    RC(mt_stream(init, B, (long)n_out, (long)out_stride, out, (long)snap_every, n_snap, snap, (hipStream_t)stream));
+    return T5G_OK;
+}
+
+extern "C" int t5g_mt_exponential(const uint32_t* raw, int64_t n, void* q, void* stream) {
+    RC(mt_exponential(raw, (long)n, (bf16_t*)q, (hipStream_t)stream));
+    return T5G_OK;
+}
+
 static SamplerArgs sampler_args(t5g_engine* e, const bf16_t* logits, int ld, int B) {
     SamplerArgs s;
     memset(&s, 0, sizeof(s));
@@ -1138,6 +1271,8 @@ static SamplerArgs sampler_args(t5g_engine* e, const bf16_t* logits, int ld, int
     s.silence = e->silence;
     s.noise = e->noise;
     s.noise_steps = e->noise_steps;
+    s.noise_mt = e->noise_mt;
+    s.noise_mt_steps = e->noise_mt_steps;
     s.eos = e->c.eos;
     s.eos_guard = e->c.eos_guard;
     s.budget_extra = e->c.budget_extra;
@@ -1544,10 +1679,6 @@ extern "C" int t5g_exact_linear(const void* X, int32_t ldx, int32_t M, const voi
                                 int32_t kb32, const void* bias, const void* gelu_lut, void* Y, int32_t ldy, int32_t epi,
                                 void* stream) {
     if (!X || !Wp || !Y || M <= 0 || N <= 0 || K <= 0 || K % 32 || kb32 < 0) return T5G_EINVAL;
-    static thread_local uint16_t* kb_dev = nullptr;   // a one-entry split table
-    if (!kb_dev && hipMalloc(&kb_dev, sizeof(uint16_t)) != hipSuccess) return T5G_EHIP;
-    const uint16_t kb = (uint16_t)kb32;
-    if (kb32 > 0) HIPCHK(hipMemcpyAsync(kb_dev, &kb, sizeof(kb), hipMemcpyHostToDevice, (hipStream_t)stream));
     ExactLinArgs a;
     memset(&a, 0, sizeof(a));
     a.X = (const bf16_t*)X;
@@ -1560,11 +1691,95 @@ extern "C" int t5g_exact_linear(const void* X, int32_t ldx, int32_t M, const voi
     a.bias = (const bf16_t*)bias;
     a.Y = Y;
     a.ldy = ldy;
-    a.kb_a = kb32 > 0 ? kb_dev : nullptr;
-    a.kb_len = 1;
+    a.kb_fixed = kb32;
     a.gelu_lut = (const uint16_t*)gelu_lut;
     RC(exact_linear(a, epi, (hipStream_t)stream));
-    if (kb32 > 0) HIPCHK(hipStreamSynchronize((hipStream_t)stream));   // kb is a host temporary
+    return T5G_OK;
+}
+
+extern "C" int t5g_pack_e16(const void* p16, void* e16, int64_t bytes, void* stream) {
+    RC(pack_e16((const bf16_t*)p16, (bf16_t*)e16, (long)bytes, (hipStream_t)stream));
+    return T5G_OK;
+}
+
+extern "C" int t5g_to_x16(const void* X, int32_t ldx, int32_t M, int32_t K, void* Y16, void* stream) {
+    RC(to_x16((const bf16_t*)X, ldx, M, K, (bf16_t*)Y16, (hipStream_t)stream));
+    return T5G_OK;
+}
+
+// hipEvent-timed xmm launches on E16 weights W16_list[i % n_w] (rotate past the Infinity
+// Cache so every launch streams from HBM, as inside a decode step); epi | 0x1000: also the
+// X16 output (Y16 = Y) instead of row-major
+extern "C" int t5g_time_xmm(const void* X16, int32_t M, const void* const* W16_list, int32_t n_w, int32_t N,
+                            int32_t K, int32_t epi, const void* bias, void* Y, int32_t ldy, int32_t iters,
+                            void* stream, float* avg_us) {
+    if (!X16 || !W16_list || n_w <= 0 || !Y || iters <= 0 || !avg_us || K % 32) return T5G_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    XmmArgs a;
+    memset(&a, 0, sizeof(a));
+    a.X16 = (const bf16_t*)X16;
+    a.M = M;
+    a.N = N;
+    a.NG = ng_pad(N);
+    a.KB = K / 32;
+    a.bias = (const bf16_t*)bias;
+    if (epi & 0x1000) a.Y16 = (bf16_t*)Y;
+    else a.Y = Y;
+    a.ldy = ldy;
+    epi &= 0xff;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    a.W = (const bf16_t*)W16_list[0];
+    RC(xmm(a, epi, st));
+    HIPCHK(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i) {
+        a.W = (const bf16_t*)W16_list[i % n_w];
+        RC(xmm(a, epi, st));
+    }
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    *avg_us = ms * 1000.f / iters;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return T5G_OK;
+}
+
+// The same Linear on the f32-MFMA kernels (xmm.hip): X converted to X16 and the packed W
+// to E16 in temporaries (test / probe entry point; the engine keeps both resident)
+extern "C" int t5g_xmm_linear(const void* X, int32_t ldx, int32_t M, const void* Wp, int32_t N, int32_t K,
+                              int32_t kb32, const void* bias, const void* gelu_lut, void* Y, int32_t ldy, int32_t epi,
+                              void* stream) {
+    if (!X || !Wp || !Y || M <= 0 || N <= 0 || K <= 0 || K % 32 || kb32 < 0) return T5G_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const long wbytes = (long)ng_pad(N) * 16 * K * 2;
+    const long xbytes = (long)((M + 15) / 16) * 16 * K * 2;
+    bf16_t *w16 = nullptr, *x16 = nullptr;
+    HIPCHK(hipMallocAsync((void**)&w16, (size_t)wbytes, st));
+    HIPCHK(hipMallocAsync((void**)&x16, (size_t)xbytes, st));
+    int rc = pack_e16((const bf16_t*)Wp, w16, wbytes, st);
+    if (!rc) rc = to_x16((const bf16_t*)X, ldx, M, K, x16, st);
+    if (!rc) {
+        XmmArgs a;
+        memset(&a, 0, sizeof(a));
+        a.X16 = x16;
+        a.M = M;
+        a.W = w16;
+        a.N = N;
+        a.NG = ng_pad(N);
+        a.KB = K / 32;
+        a.bias = (const bf16_t*)bias;
+        a.Y = Y;
+        a.ldy = ldy;
+        a.kb_fixed = kb32;
+        a.gelu_lut = (const uint16_t*)gelu_lut;
+        rc = xmm(a, epi, st);
+    }
+    hipFreeAsync(w16, st);
+    hipFreeAsync(x16, st);
+    RC(rc);
     return T5G_OK;
 }
 

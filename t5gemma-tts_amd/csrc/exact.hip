@@ -88,6 +88,7 @@ __device__ __forceinline__ void exact_lin_store(const ExactLinArgs& a, int m, in
 
 // The K-split chunk size (32-element chunks per part) of row m for packed column n.
 __device__ __forceinline__ int exact_lin_kbc(const ExactLinArgs& a, int m, int n) {
+    if (a.kb_fixed > 0) return a.kb_fixed;
     const int mu = a.row_len ? a.row_len[a.tok_row ? a.tok_row[m] : m] : 1;
     const uint16_t* tab = (a.kb_b && n >= a.nsplit_col) ? a.kb_b : a.kb_a;
     int kbc = tab ? tab[min(max(mu, 1), a.kb_len) - 1] : a.KB;
@@ -604,8 +605,11 @@ __global__ __launch_bounds__(256) void exact_attn_kernel(ExactAttnArgs a) {
         m = mn;
         __syncthreads();
     }
-    if (tid < XA_DS && d0 + tid < D)
-        a.O[(long)qi * a.ldo + h * D + d0 + tid] = f2bf(__fmul_rn(dst, __fdiv_rn(1.0f, l)));
+    if (tid < XA_DS && d0 + tid < D) {
+        const bf16_t o = f2bf(__fmul_rn(dst, __fdiv_rn(1.0f, l)));
+        a.O[(long)qi * a.ldo + h * D + d0 + tid] = o;
+        if (a.O16) a.O16[x16_off(qi, h * D + d0 + tid, a.ldo / 32)] = o;
+    }
 }
 
 int exact_attention(const ExactAttnArgs& a, hipStream_t st) {

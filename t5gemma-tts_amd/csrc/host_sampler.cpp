@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "sort_emu.h"
 #include "t5gtts.h"
 
 namespace {
@@ -162,4 +163,15 @@ extern "C" int t5g_host_sample(const uint16_t* logits, int32_t V, const t5g_samp
     *st_out = st;
     *token_out = token;
     return T5G_OK;
+}
+
+// Host build of the device sampler's sparse std::sort emulation (csrc/sort_emu.h), for the
+// CPU tests: S survivors at slots pos[] (ascending) with values val[] in an array of n
+// otherwise -inf entries; on return pos[] / val[] / tag[] are ordered by final slot.
+extern "C" int t5g_sort_emu(int32_t n, int32_t S, int32_t* pos, float* val, int32_t* tag) {
+    if (n <= 0 || S < 0 || S > n || (S > 0 && (!pos || !val || !tag))) return T5G_EINVAL;
+    for (int i = 1; i < S; ++i)
+        if (pos[i] <= pos[i - 1] || pos[i] >= n) return T5G_EINVAL;
+    t5g::SortEmu E{n, S, pos, val, tag, 0};
+    return t5g::se_sort(E) ? T5G_EUNSUPPORTED : T5G_OK;
 }

@@ -186,7 +186,14 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
     if (a.resid_out && active) *(u32x4*)(a.resid_out + orow * d + 8 * c) = pack8(v);
     if (has_pre) {
         rms8<EXACT>(v, active, d, w_pre, a.eps, red[1], sq);
-        if (active) *(u32x4*)(a.normed_out + orow * d + 8 * c) = pack8(v);
+        if (active) {
+            const u32x4 pk = pack8(v);
+            *(u32x4*)(a.normed_out + orow * d + 8 * c) = pk;
+            if (a.normed_x16) {   // the next exact Linear's operand order (xmm.hip): pair j -> slot q = j
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) *(uint32_t*)(a.normed_x16 + x16_off(orow, 8 * c + 2 * jj, d / 32)) = pk[jj];
+            }
+        }
     }
     T5G_TS(2);
 }

@@ -26,6 +26,7 @@
 // every transform above rounds to bf16, so nothing is lost; thread t owns pairs
 // t + 1024 * jp, i.e. elements 2 * (t + 1024 * jp) + {0, 1}.
 #include "common.h"
+#include "sort_emu.h"
 #include "t5g_kernels.h"
 
 namespace t5g {
@@ -161,6 +162,10 @@ __device__ __forceinline__ float draw_q(const SamplerArgs& a, const SamplerRow& 
                                         int i) {
     // parity mode: the step's reference draws (steps past the uploaded ones -- never reached
     // when the host sizes the stream to the row budget + 1 -- reuse the last, in bounds)
+    if (a.noise_mt) {
+        const uint32_t* r = a.noise_mt + ((long)b * a.noise_mt_steps + min(st.cur_num_gen, a.noise_mt_steps - 1)) * 2L * a.V;
+        return mt_exp_q(r[2 * i], r[2 * i + 1]);
+    }
     if (a.noise) return bf2f(a.noise[((long)b * a.noise_steps + min(st.cur_num_gen, a.noise_steps - 1)) * a.V + i]);
     (void)b;
     const uint32_t u = philox((uint32_t)i, (uint32_t)st.cur_num_gen, 0u, pr.seed_lo, pr.seed_hi);
@@ -173,6 +178,16 @@ __device__ __forceinline__ float draw_q(const SamplerArgs& a, const SamplerRow& 
 // Stop rules + per-row state update (:753-786, :806-832); one thread.
 __device__ void finish_row(const SamplerArgs& a, const SamplerRow& pr, SamplerState st, int b, int token, int amax,
                            int ambiguous, int eff_len) {
+    if (ambiguous & 4) {
+        // parity mode, a tie order the device could not reproduce: the row STALLS (done = 2)
+        // without committing the step -- no token, no state advance, so later steps of the
+        // graph recompute the same logits for it -- until the host re-runs the step with
+        // std::sort (t5g_host_sample) and writes the state back
+        st.done = 2;
+        if (a.flags) a.flags[b] = ambiguous | (amax == a.eos ? 2 : 0);
+        a.state[b] = st;
+        return;
+    }
     bool force = (token == a.eos) || (amax == a.eos);
     if (a.text_guard > 0) force = force || (eff_len > max(1, st.first_input_len) * a.text_guard);
     bool budget = st.target_total >= 0 &&
@@ -192,7 +207,7 @@ __device__ void finish_row(const SamplerArgs& a, const SamplerRow& pr, SamplerSt
     st.cur_num_gen += 1;
     st.current_length += 1;
     st.last_token = token;
-    st.ambiguous_steps += ambiguous;
+    st.ambiguous_steps += ambiguous & 1;
     if (token == a.eos) {
         st.done = 1;
     } else {
@@ -511,8 +526,9 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
             for (int j = 0; j < SPER; ++j)
                 if (x.get(j) < vc) x.set(j, -INFINITY);
             if (keep < gsz) {
-                // production tie-break: keep the `keep` lowest indices of the tie group
-                ambiguous = 1;
+                // production tie-break: keep the `keep` lowest indices of the tie group; in
+                // parity mode (reference noise) the row stalls for the host's std::sort
+                ambiguous = (a.noise_mt || a.noise) ? 1 | 4 : 1;
                 if (tid == 0) sh_int[7] = 0;
                 __syncthreads();
 #pragma unroll
@@ -552,8 +568,6 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
             if (v > -INFINITY) ls += expf(v - m);
         }
         const float inv = 1.0f / block_sum(ls, redv);
-        const bf16_t* nz =
-            a.noise ? a.noise + ((long)b * a.noise_steps + min(st.cur_num_gen, a.noise_steps - 1)) * V : nullptr;
         float bv = -1.f;
         int bi = 0x7fffffff;
 #pragma unroll
@@ -564,7 +578,7 @@ __global__ __launch_bounds__(SN) void sampler_kernel(SamplerArgs a) {
             if (xv == -INFINITY) continue;  // p = 0 -> r = 0 can never beat a survivor
             const float p = rbf(expf(xv - m) * inv);
             float r = 0.f;
-            if (p > 0.f) r = rbf(p / (nz ? bf2f(nz[i]) : draw_q(a, pr, st, b, i)));
+            if (p > 0.f) r = rbf(p / draw_q(a, pr, st, b, i));
             if (r > bv || (r == bv && i < bi)) { bv = r; bi = i; }
         }
         token = block_argmax(bv, bi, redv, redi);
@@ -880,19 +894,79 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
         nkeep = sh_int[0];
         ambiguous = sh_int[1];
     }
-    // ---- 7. softmax over the kept survivors + multinomial-as-argmax(p / q)
+    // ---- 7. softmax over the kept survivors + multinomial-as-argmax(p / q). The normaliser
+    // depends only on how many survivors are kept (a cut group's members are equal), so the
+    // r of every survivor up to the end of the cut group is known before the group's order
     float ls = 0.f;
     if (tid < nkeep && cv[tid] > -INFINITY) ls = expf(cv[tid] - m);
     const float inv = 1.0f / block_sum(ls, redv);
+    const float vc = cv[nkeep - 1];
+    int g1 = nkeep;   // end of the cut group (ambiguous: the group runs past nkeep)
+    if (ambiguous) {
+        if (tid == 0) {
+            int e1 = nkeep;
+            while (e1 < ns && cv[e1] == vc) ++e1;
+            int e0 = nkeep - 1;
+            while (e0 > 0 && cv[e0 - 1] == vc) --e0;
+            sh_int[2] = e1;
+            sh_int[3] = e0;
+        }
+        __syncthreads();
+        g1 = sh_int[2];
+    }
+    auto r_of = [&](int q) -> float {
+        const float p = rbf(expf(cv[q] - m) * inv);
+        return p > 0.f ? rbf(p / draw_q(a, pr, st, b, ci[q])) : 0.f;
+    };
+    float rq = -1.f;
+    if (tid < g1 && cv[tid] > -INFINITY) rq = r_of(tid);
+    if (ambiguous && (a.noise_mt || a.noise)) {
+        // parity mode: which members of the cut group are kept matters only if one of them
+        // can win -- beat the best survivor above the group
+        const int g0 = sh_int[3];
+        int iw = tid < g0 ? ci[tid] : 0x7fffffff, ig = (tid >= g0 && tid < g1) ? ci[tid] : 0x7fffffff;
+        const float rw = block_argmax_v(tid < g0 ? rq : -2.f, iw, redv, redi);
+        const float rg = block_argmax_v((tid >= g0 && tid < g1) ? rq : -2.f, ig, redv, redi);
+        if (rg > rw || (rg == rw && ig < iw)) {
+            // the kept members are those torch.sort puts first: follow its std::sort on the
+            // survivors (csrc/sort_emu.h), one thread. Survivors by token index (= initial
+            // slot): spos / sval / stag (cv / ci slot)
+            int* spos = (int*)&wh[0][0];
+            int* stag = (int*)&wh[1][0];
+            float* sval = sv;
+            int nf = 0;   // finite survivors (a -inf tail sorts among the -inf entries)
+            while (nf < ns && cv[nf] > -INFINITY) ++nf;
+            if (tid < nf) {
+                const int i = ci[tid];
+                int r = 0;
+                for (int q = 0; q < nf; ++q) r += ci[q] < i;
+                spos[r] = i;
+                sval[r] = cv[tid];
+                stag[r] = tid;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                SortEmu E{V, nf, spos, sval, stag, 0};
+                if (se_sort(E) || vc == -INFINITY) {
+                    sh_int[1] = 1 | 4;   // not reproducible here: stall for the host
+                } else {
+                    // the cut group [g0, g1) of cv / ci, reordered by final slot
+                    int k = 0;
+                    for (int q = 0; q < nf; ++q)
+                        if (sval[q] == vc) si[k++] = ci[stag[q]];
+                    for (int q = 0; q < k; ++q) ci[g0 + q] = si[q];
+                }
+            }
+            __syncthreads();
+            ambiguous = sh_int[1];
+            if (tid >= g0 && tid < g1 && cv[tid] > -INFINITY) rq = r_of(tid);   // the group's new order
+        }
+    }
     float rbv = -1.f;
     int rbi = 0x7fffffff;
     if (tid < nkeep && cv[tid] > -INFINITY) {
-        const int i = ci[tid];
-        const float p = rbf(expf(cv[tid] - m) * inv);
-        float r = 0.f;
-        if (p > 0.f) r = rbf(p / draw_q(a, pr, st, b, i));
-        rbv = r;
-        rbi = i;
+        rbv = rq;
+        rbi = ci[tid];
     }
     int token = rbi;
     block_argmax_v(rbv, token, redv, redi);

@@ -140,6 +140,7 @@ struct NormArgs {
     float* rope_tab;         // [M][rope_D]
     int rope_D;
     int exact;               // parity mode: the reference's CPU sum order (delta / ids sources)
+    bf16_t* normed_x16;      // optional: normed_out again in the X16 layout (xmm.hip)
 };
 int resid_norm(const NormArgs& a, hipStream_t st);
 
@@ -223,9 +224,43 @@ struct ExactLinArgs {
     const uint16_t* kb_a;
     const uint16_t* kb_b;
     int nsplit_col, kb_len;
+    int kb_fixed;             // > 0: every row splits K into parts of kb_fixed chunks (no tables)
     const uint16_t* gelu_lut; // EPI_BIAS_GELU: bf16 -> bf16 nn.GELU() table (null: exact_math.h)
 };
 int exact_linear(const ExactLinArgs& a, int epi, hipStream_t st);
+
+// exact-order Linear on the f32 MFMA (xmm.hip): X and Y16 in the X16 layout, W in E16
+struct XmmArgs {
+    const bf16_t* X16;        // [ceil(M / 16)][KB][16][4][8] bf16 (xmm_to_x16 / producers)
+    int M;
+    const bf16_t* W;          // E16 packed, NG row groups x KB fragments
+    int N, NG, KB;
+    const bf16_t* bias;
+    void* Y;                  // row-major bf16 / fp32 [M][ldy] (GEGLU: bf16 [M][N/2]) or null
+    int ldy;
+    bf16_t* Y16;              // optional: the bf16 output again in the X16 layout (next Linear's X)
+    const int* tok_row;       // K split as ExactLinArgs
+    const int* row_len;
+    const uint16_t* kb_a;
+    const uint16_t* kb_b;
+    int nsplit_col, kb_len;
+    int kb_fixed;             // > 0: every row splits K into parts of kb_fixed chunks (no tables)
+    const uint16_t* gelu_lut;
+};
+int xmm(const XmmArgs& a, int epi, hipStream_t st);
+int pack_e16(const bf16_t* p16, bf16_t* e16, long bytes, hipStream_t st);
+int to_x16(const bf16_t* X, int ldx, int M, int K, bf16_t* Y, hipStream_t st);
+// X16 element offset of (row m, column k) of a matrix with KB chunks of 32 per row: per
+// 16-row tile and chunk a 1 KiB block in the B-operand lane order of v_mfma_f32_16x16x4_f32
+// (lane l = 16 q + j, j = row in the tile), lane l's 16 bytes the element pairs 4t + q,
+// t = 0..3, of row j
+__host__ __device__ inline long x16_off(long m, int k, int KB) {
+    const int kb = k >> 5, e = k & 31, p = e >> 1, t = p >> 2, q = p & 3;
+    return ((((m >> 4) * KB + kb) * 4 + q) * 16 + (m & 15)) * 8 + t * 2 + (e & 1);
+}
+// torch CPU SDPA kv blocks (common.h sdpa_*): keys per block, blocks per row (kv_cap <= 4096)
+constexpr int SDPA_KV_BLOCK = 512;
+constexpr int SDPA_MAX_BLOCKS = 8;
 
 struct ExactAttnArgs {
     const bf16_t* Q;          // [Mq][ldq] RoPE'd queries
@@ -243,8 +278,12 @@ struct ExactAttnArgs {
     int threads;              // the reference host's torch thread count (aten need_pack)
     bf16_t* O;
     int ldo;
+    bf16_t* O16;              // optional: the output again in the X16 layout (K = ldo)
 };
 int exact_attention(const ExactAttnArgs& a, hipStream_t st);
+// decode (one query per row, at its last key): scores + P.V launches (xattn.hip) on the
+// scratch sbuf [Mq][Hq][cap] / mbuf [Mq][Hkv][ceil(cap / 64)][G]
+int exact_attention_decode(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, hipStream_t st);
 
 // ---- sampler -------------------------------------------------------------------
 struct SamplerRow {           // per-utterance parameters (device)
@@ -281,6 +320,8 @@ struct SamplerArgs {
     const int* silence;
     const bf16_t* noise;      // parity mode: [B][noise_steps][V] bf16 or null (Philox)
     int noise_steps;
+    const uint32_t* noise_mt; // parity mode: raw MT19937 outputs [B][noise_mt_steps][2 V] (noise.hip)
+    int noise_mt_steps;
     int eos, eos_guard;       // eos id, encodec_sr // 5
     float budget_extra;       // int(encodec_sr) * extra_cutoff
     int text_guard;           // text_guard_frames_per_token
@@ -308,5 +349,12 @@ constexpr int FS_CAP = 128;   // candidates per slice
 constexpr int FS_KMAX = 64;   // largest top-k the fast path takes
 constexpr int FS_SMAX = 256;  // largest top-k survivor set (ties) the fast path takes
 size_t sampler_fast_ws_bytes(int B);
+
+// ---- parity-mode noise (noise.hip) ------------------------------------------------
+// init [B][625]: MT19937 words + consumed position; raw outputs [B][out_stride] (n_out per
+// row); optional snapshots of the generator every snap_every outputs [B][n_snap][625]
+int mt_stream(const uint32_t* init, int B, long n_out, long out_stride, uint32_t* out, long snap_every, int n_snap,
+              uint32_t* snap, hipStream_t st);
+int mt_exponential(const uint32_t* raw, long n, bf16_t* q, hipStream_t st);
 int sample(const SamplerArgs& a, hipStream_t st);
 }  // namespace t5g

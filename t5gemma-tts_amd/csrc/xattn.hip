@@ -1,0 +1,228 @@
+// Exact-order decode attention (parity mode, one query per row): two launches instead of
+// exact.hip's one workgroup per (row, q head, 32-dim slice) that recomputed every score
+// eight times.
+//
+// The reference's decode step calls F.scaled_dot_product_attention with one query
+// ([tf] T5GemmaSelfAttention :264-304, PMCrossAttention :167-253); aten's CPU flash
+// attention then runs oneDNN's gemv for q.k and P.V:
+//   q.k: 16 lane accumulators, lane l taking the pair (2l, 2l+1) of every 32-element chunk,
+//        odd product first, then l + l^8, adjacent pairs, adjacent pairs, the last pair;
+//   softmax per 512-key block against the running max (common.h sdpa_*);
+//   P.V: groups of 8 keys, each a fresh pair-ordered chain (odd key first), added in
+//        group order onto the (rescaled) output.
+// * xattn_scores_kernel: one wave per (row, kv head, 64-key chunk); a lane per key computes
+//   the scores of the G query heads in the gemv order (the 16 accumulators in registers,
+//   the q rows broadcast from LDS), writes them and the chunk maxima.
+// * xattn_pv_kernel: per (row, kv head, 32-dim slice): running maxima from the chunk
+//   maxima, exact p of each block, aten's block sums, the 8-key group chains of its slice
+//   in parallel (16 group lanes x 16 dimension pairs), then the group sums folded in order
+//   by one thread per (head, dimension); output x 1/l, also written in the X16 layout of
+//   the o-projection (xmm.hip).
+#include "common.h"
+#include "t5g_kernels.h"
+
+namespace t5g {
+
+constexpr int XD_CH = 64;    // keys per scores workgroup
+constexpr int XD_DZ = 32;    // output dims per P.V workgroup
+
+// keys [lo, hi) of a decode query (the sdpa call's keys: a sliding-window layer whose
+// cache is at least `window` long sees its last `window` keys, DynamicSlidingWindowLayer)
+__device__ __forceinline__ void xd_range(const ExactAttnArgs& a, int row, int& lo, int& hi) {
+    hi = a.kv_len[row];
+    lo = (a.window > 0 && a.causal && hi >= a.window) ? hi - a.window : 0;
+}
+
+template <int G, int XD_D>
+__global__ __launch_bounds__(64) void xattn_scores_kernel(ExactAttnArgs a, float* sbuf, float* mbuf, int cap,
+                                                          int nsplit) {
+    __shared__ float qs[G][XD_D];
+    const int qi = blockIdx.x, kvh = blockIdx.y, ch = blockIdx.z, lane = threadIdx.x;
+    const int row = a.q_row ? a.q_row[qi] : qi;
+    int lo, hi;
+    xd_range(a, row, lo, hi);
+    const int c0 = lo + ch * XD_CH;
+    if (c0 >= hi) return;
+    const int key = c0 + lane;
+    const bool valid = key < hi;
+    const bf16_t* kr = a.K + row * a.kv_bstride + kvh * a.kv_hstride + (long)(valid ? key : c0) * XD_D;
+    u32x4 kv[XD_D / 8];
+#pragma unroll
+    for (int j = 0; j < XD_D / 8; ++j) kv[j] = *(const u32x4*)(kr + 8 * j);
+    // the G query rows of this kv head (GQA: heads kvh * G + g), broadcast from LDS
+    for (int i = lane; i < G * XD_D / 2; i += 64) {
+        const int g = i / (XD_D / 2), p = i % (XD_D / 2);
+        const uint32_t w = *(const uint32_t*)(a.Q + (long)qi * a.ldq + (kvh * G + g) * XD_D + 2 * p);
+        qs[g][2 * p] = bf_lo(w);
+        qs[g][2 * p + 1] = bf_hi(w);
+    }
+    __syncthreads();
+    float sc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        float acc[16];
+#pragma unroll
+        for (int l2 = 0; l2 < 16; ++l2) acc[l2] = 0.f;
+#pragma unroll
+        for (int cb = 0; cb < XD_D / 32; ++cb) {
+            const int c = cb * 32;
+#pragma unroll
+            for (int l2 = 0; l2 < 16; ++l2) {
+                const uint32_t kw = kv[cb * 4 + (l2 >> 2)][l2 & 3];
+                acc[l2] = fmaf(qs[g][c + 2 * l2 + 1], bf_hi(kw), acc[l2]);
+                acc[l2] = fmaf(qs[g][c + 2 * l2], bf_lo(kw), acc[l2]);
+            }
+        }
+        float v8[8], v4[4];
+#pragma unroll
+        for (int l2 = 0; l2 < 8; ++l2) v8[l2] = __fadd_rn(acc[l2], acc[l2 + 8]);
+#pragma unroll
+        for (int l2 = 0; l2 < 4; ++l2) v4[l2] = __fadd_rn(v8[2 * l2], v8[2 * l2 + 1]);
+        sc[g] = __fmul_rn(__fadd_rn(__fadd_rn(v4[0], v4[1]), __fadd_rn(v4[2], v4[3])), a.scale);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const float s = valid ? sc[g] : -INFINITY;
+        if (valid) sbuf[((long)qi * a.Hq + kvh * G + g) * cap + (key - lo)] = s;
+        const float mx = wave_max(s);
+        if (lane == 0) mbuf[(((long)qi * a.Hkv + kvh) * nsplit + ch) * G + g] = mx;
+    }
+}
+
+template <int G, int XD_D>
+__global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const float* sbuf, const float* mbuf,
+                                                       int cap, int nsplit) {
+    constexpr int BLK = SDPA_KV_BLOCK;           // 512
+    constexpr int NGRP = BLK / 8;                // 8-key groups per block
+    constexpr int DP = XD_DZ / 2;                // dimension pairs per workgroup
+    constexpr int GL = 256 / DP;                 // group lanes (16)
+    __shared__ float pex[G][BLK + 16];           // exact p (block sums)
+    __shared__ float pbf[G][BLK];                // bf16-rounded p (P.V)
+    __shared__ float tmp[NGRP][G][XD_DZ];        // group chain sums of the block
+    __shared__ float mrun[G][SDPA_MAX_BLOCKS];
+    __shared__ float et_s[G], l_s[G];
+    const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int row = a.q_row ? a.q_row[qi] : qi;
+    int lo, hi;
+    xd_range(a, row, lo, hi);
+    const int span = max(hi - lo, 0);
+    if (span == 0) return;
+    const int nch = (span + XD_CH - 1) / XD_CH;
+    const int nblk = (span + BLK - 1) / BLK;
+    const float* sb = sbuf + ((long)qi * a.Hq + kvh * G) * cap;
+    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride + (long)lo * XD_D + z * XD_DZ;
+    if (wave < G) {   // running max through each block, from the chunk maxima
+        const int g = wave;
+        float run = -INFINITY;
+        for (int b = 0; b < nblk; ++b) {
+            float cm = -INFINITY;
+            for (int c = b * (BLK / XD_CH) + lane; c < min(nch, (b + 1) * (BLK / XD_CH)); c += 64)
+                cm = fmaxf(cm, mbuf[(((long)qi * a.Hkv + kvh) * nsplit + c) * G + g]);
+            run = fmaxf(run, wave_max(cm));
+            if (lane == 0) mrun[g][b] = run;
+        }
+        if (lane < 16) pex[g][BLK + lane] = 0.f;
+    }
+    const int dp = tid % DP, gl = tid / DP;      // P.V role: dimension pair, group lane
+    float l = 0.f, m_old = -INFINITY;            // wave g < G: head g's running sum
+    float dst = 0.f;                             // folder (g, dim) = tid < G * XD_DZ
+    const int fg = tid / XD_DZ, fd = tid % XD_DZ;
+    __syncthreads();
+    for (int b = 0; b < nblk; ++b) {
+        const int bs = b * BLK, blen = min(BLK, span - bs);
+        // exact p of the block's keys
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float mb = mrun[g][b];
+            for (int pos = tid; pos < BLK; pos += 256) {
+                const float p = pos < blen ? sdpa_p(__fsub_rn(sb[(long)g * cap + bs + pos], mb), pos, blen) : 0.f;
+                pex[g][pos] = p;
+                pbf[g][pos] = rbf(p);
+            }
+        }
+        __syncthreads();
+        if (wave < G) {
+            const int g = wave;
+            const float ts = sdpa_block_sum_lds<BLK>(pex[g], blen, lane);
+            const float mb = mrun[g][b];
+            const float et = sdpa_block_rescale(m_old, mb);
+            l = fmaf(et, l, ts);
+            m_old = mb;
+            if (lane == 0) et_s[g] = et;
+        }
+        // 8-key group chains of the slice: lane gl takes groups gl, gl + 16, ... (pairs, odd
+        // key first; keys past the block count 0 and add nothing: the chain stops there)
+        const int ngrp = (blen + 7) / 8;
+        for (int gi = gl; gi < ngrp; gi += GL) {
+            const int k0 = gi * 8, cn = min(8, blen - k0);
+            uint32_t vw[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                vw[j] = *(const uint32_t*)(Vb + (long)(bs + k0 + (j < cn ? j : 0)) * XD_D + 2 * dp);
+            float t0[G], t1[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                t0[g] = 0.f;
+                t1[g] = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; j += 2) {
+                    if (j < cn) {
+                        if (j + 1 < cn) {
+                            const float p1 = pbf[g][k0 + j + 1];
+                            t0[g] = fmaf(p1, bf_lo(vw[j + 1]), t0[g]);
+                            t1[g] = fmaf(p1, bf_hi(vw[j + 1]), t1[g]);
+                        }
+                        const float p0 = pbf[g][k0 + j];
+                        t0[g] = fmaf(p0, bf_lo(vw[j]), t0[g]);
+                        t1[g] = fmaf(p0, bf_hi(vw[j]), t1[g]);
+                    }
+                }
+                tmp[gi][g][2 * dp] = t0[g];
+                tmp[gi][g][2 * dp + 1] = t1[g];
+            }
+        }
+        __syncthreads();
+        if (tid < G * XD_DZ) {
+            float acc = bs == 0 ? 0.f : __fmul_rn(dst, et_s[fg]);
+            for (int gi = 0; gi < ngrp; ++gi) acc = __fadd_rn(acc, tmp[gi][fg][fd]);
+            dst = acc;
+        }
+        __syncthreads();   // pex / pbf / tmp / et_s are rewritten by the next block
+    }
+    if (wave < G && lane == 0) l_s[wave] = l;
+    __syncthreads();
+    if (tid < G * XD_DZ) {
+        const int col = (kvh * G + fg) * XD_D + z * XD_DZ + fd;
+        const bf16_t o = f2bf(__fmul_rn(dst, __fdiv_rn(1.0f, l_s[fg])));
+        a.O[(long)qi * a.ldo + col] = o;
+        if (a.O16) a.O16[x16_off(qi, col, a.ldo / 32)] = o;
+    }
+}
+
+// decode attention (one query per row, gemv numerics) on the scores scratch sbuf
+// [Mq][Hq][cap] and chunk maxima mbuf [Mq][Hkv][nsplit][G]
+template <int G, int D>
+static void launch_xd(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, int nsplit, hipStream_t st) {
+    const dim3 gs((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)nsplit), gp((unsigned)a.Mq, (unsigned)a.Hkv, D / XD_DZ);
+    hipLaunchKernelGGL((xattn_scores_kernel<G, D>), gs, dim3(64), 0, st, a, sbuf, mbuf, cap, nsplit);
+    hipLaunchKernelGGL((xattn_pv_kernel<G, D>), gp, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
+}
+
+int exact_attention_decode(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, hipStream_t st) {
+    if (a.Mq <= 0) return 0;
+    if (!a.Q || !a.K || !a.V || !a.kv_len || !a.O || !sbuf || !mbuf || a.Hq % a.Hkv) return -1;
+    if (a.q_pos || a.q_len) return -1;   // one query per row, at its last key
+    const int G = a.Hq / a.Hkv;
+    const int nsplit = (cap + XD_CH - 1) / XD_CH;
+    if ((cap + SDPA_KV_BLOCK - 1) / SDPA_KV_BLOCK > SDPA_MAX_BLOCKS) return -1;
+    if (G == 2 && a.D == 256) launch_xd<2, 256>(a, sbuf, mbuf, cap, nsplit, st);
+    else if (G == 2 && a.D == 128) launch_xd<2, 128>(a, sbuf, mbuf, cap, nsplit, st);
+    else if (G == 2 && a.D == 64) launch_xd<2, 64>(a, sbuf, mbuf, cap, nsplit, st);
+    else if (G == 1 && a.D == 256) launch_xd<1, 256>(a, sbuf, mbuf, cap, nsplit, st);
+    else if (G == 1 && a.D == 64) launch_xd<1, 64>(a, sbuf, mbuf, cap, nsplit, st);
+    else return -3;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace t5g

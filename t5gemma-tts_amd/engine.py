@@ -24,6 +24,7 @@ import torch
 
 from . import _lib
 from .config import VoiceConfig
+from .noise import DeviceNoise
 from .weights import check_state_dict
 
 BF16 = torch.bfloat16
@@ -209,6 +210,7 @@ class T5GemmaTTSEngine:
         ld = C.c_int32()
         self._logits_ptr = self.L.t5g_logits_ptr(h, C.byref(ld))
         self.logits_ld = ld.value
+        self._noise = DeviceNoise(self.V, self.device)
 
     def set_fused(self, enable: bool) -> None:
         """Decode MLP half (norm -> gate/up -> down) as one persistent launch (default) or as
@@ -265,8 +267,9 @@ class T5GemmaTTSEngine:
                  generators: Optional[Sequence[torch.Generator]] = None, exact: Optional[bool] = None):
         """Run inference_tts on a batch. ``parity=True`` is the reference-reproduction mode:
         the exact-order kernels (logits bit-identical to the reference host's CPU run), the
-        reference's CPU RNG stream, and host resolution of tie-ambiguous top-p steps (one
-        host sync per step). The stream of row i is ``torch.manual_seed(seeds[i])`` or, with
+        reference's CPU RNG stream (MT19937 on the device, csrc/noise.hip) and torch.sort's
+        tie order for top-p cuts inside tie groups (csrc/sort_emu.h; the host's std::sort for
+        the rare step the device cannot reproduce), in graph-replayed chunks. The stream of row i is ``torch.manual_seed(seeds[i])`` or, with
         ``generators``, the continuation of ``generators[i]`` (e.g. ``torch.default_generator``
         after ``seed_everything``), which is then advanced by exactly the draws the reference
         would have made. ``exact`` (default: = parity) selects the kernel set on its own.
@@ -297,14 +300,14 @@ class T5GemmaTTSEngine:
                     g.set_state(st_)
             out = self._generate_once(utts, params, seeds, generators, parity, use_graph, chunk, record_logits, stream)
         if generators is not None:
-            for g, row in zip(generators, out["gen"]):
-                consume_noise(g, len(row), self.V)
+            # where the reference's loop leaves torch's generator: after len(gen) draws of V
+            self._noise.advance_generators(generators, [len(row) for row in out["gen"]])
         return out
 
     def _generate_once(self, utts, params, seeds, generators, parity, use_graph, chunk, record_logits, stream):
         ctx = self._prepare(utts, params, generators if generators is not None else seeds, parity, stream)
         if parity:
-            self._run_parity(ctx, stream, record_logits)
+            self._run_parity(ctx, stream, record_logits, chunk, use_graph)
         else:
             while not self._decode_chunk(ctx, chunk, use_graph, stream):
                 pass
@@ -332,6 +335,7 @@ class T5GemmaTTSEngine:
         silence: List[int] = []
         y_rows = []
         max_steps = 1
+        budgets: List[int] = []
         for b, u in enumerate(utts):
             x = [int(v) for v in u.x]
             if len(x) == 0:
@@ -385,6 +389,7 @@ class T5GemmaTTSEngine:
                 if budget < 1:
                     raise ValueError(f"row {b}: prompt {cur_len} leaves no room in max_audio {self.max_audio}")
             max_steps = max(max_steps, budget)
+            budgets.append(budget)
             p = params[b]
             r = rows[b]
             if isinstance(p.top_k, (list, tuple)):
@@ -406,12 +411,17 @@ class T5GemmaTTSEngine:
         d_aid, d_arow, d_at = (torch.tensor(v, **i32) for v in (aid, arow, at))
         d_apos = torch.cat(apos).to(dev)
         d_alen, d_last = torch.tensor(alen, **i32), torch.tensor(last, **i32)
-        noise = None
-        if parity:
-            # one stream step per sampler call: up to the row budget, plus the step at which a
-            # cap (time budget or, without tgt_y_lens, the cache capacity) forces EOS
-            noise = torch.stack([reference_noise(s, max_steps + 1, self.V) for s in seeds[:B]]).to(dev)
         L = self.L
+        if parity:
+            # the reference's multinomial draws, one stream step per sampler call (up to the row
+            # budget, plus the step at which a cap forces EOS): MT19937 streams generated on a
+            # side stream (csrc/noise.hip) while the encoder and prefill run
+            self._noise.generate(seeds[:B], max_steps + 1, self.max_gen + 1,
+                                 snapshots=isinstance(seeds[0], torch.Generator))
+            _lib.check(L.t5g_engine_set_noise_mt(self.h, C.c_void_p(self._noise.raw.data_ptr()), self.max_gen + 1),
+                       "set_noise_mt")
+        else:
+            _lib.check(L.t5g_engine_set_noise_mt(self.h, None, 0), "set_noise_mt")
         # the host tensors above were filled on torch's current stream: order them first
         torch.cuda.current_stream(dev).synchronize()
         _lib.check(L.t5g_encode(self.h, B, len(ids), _ptr(d_ids), _ptr(d_trow), _ptr(d_tt), _ptr(d_tpos),
@@ -421,8 +431,10 @@ class T5GemmaTTSEngine:
         tk = (C.c_int32 * max(1, len(topk_list)))(*topk_list)
         sl = (C.c_int32 * max(1, len(silence)))(*silence)
         _lib.check(L.t5g_sampler_setup(self.h, B, rows, states, tk, len(topk_list), sl, len(silence),
-                                       _ptr(noise), max_steps + 1 if parity else 0, stream), "sampler_setup")
-        return {"B": B, "rows": rows, "tk": tk, "sl": sl, "noise": noise, "y_rows": y_rows,
+                                       None, 0, stream), "sampler_setup")
+        if parity:
+            self._noise.wait()   # the first sampler call reads the draws
+        return {"B": B, "rows": rows, "tk": tk, "sl": sl, "y_rows": y_rows, "budgets": budgets,
                 "max_steps": max_steps, "steps": 0, "ambiguous_fixed": 0, "rec": None,
                 "cur": (_lib.SamplerState * B)(), "keep": (d_ids, d_trow, d_tt, d_tpos, d_tlen, d_aid, d_arow, d_at,
                                                           d_apos, d_alen, d_last)}
@@ -444,44 +456,60 @@ class T5GemmaTTSEngine:
             raise RuntimeError("decode did not terminate within the time budget")
         return False
 
-    def _run_parity(self, ctx, stream, record_logits: bool) -> None:
-        L, B, cfg = self.L, ctx["B"], self.cfg
-        rows, tk, sl, noise = ctx["rows"], ctx["tk"], ctx["sl"], ctx["noise"]
-        eos = cfg.eog_inference
+    def _run_parity(self, ctx, stream, record_logits: bool, chunk: int, use_graph: bool) -> None:
+        """The AR loop in parity mode: graph-replayed chunks of sampler + exact decoder steps,
+        with the reference's draws and torch.sort's tie order on the device. A row whose tie
+        order the device cannot reproduce (csrc/sort_emu.h bails out, or the single-block
+        sampler path) stalls without committing its step (state.done == 2); after the chunk
+        the host re-runs that step with std::sort (t5g_host_sample), writes the state back
+        and runs one decoder step so the row's next logits follow its token.
+        record_logits: one step per chunk, every sampled logits row kept."""
+        L, B = self.L, ctx["B"]
+        rows, tk, sl = ctx["rows"], ctx["tk"], ctx["sl"]
+        eos = self.cfg.eog_inference
         rec = [] if record_logits else None
         cur = ctx["cur"]
+        budget = ctx["budgets"]
         _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
-        flags = (C.c_int32 * B)()
-        nxt = (_lib.SamplerState * B)()
-        while not all(cur[b].done for b in range(B)):
+        limit = ctx["max_steps"] + 2
+        while True:
+            active = [b for b in range(B) if cur[b].done != 1]
+            if not active:
+                break
+            stalled = [b for b in active if cur[b].done == 2]
+            if stalled:
+                lg = self.logits(B).cpu()
+                for b in stalled:
+                    st_in = _lib.SamplerState()
+                    C.memmove(C.byref(st_in), C.byref(cur[b]), C.sizeof(st_in))
+                    st_in.done = 0
+                    nz = self._noise.q_row(b, st_in.cur_num_gen)
+                    out_st = _lib.SamplerState()
+                    tok = C.c_int32()
+                    _lib.check(L.t5g_host_sample(
+                        _ptr(lg[b].contiguous()), self.V, C.byref(rows[b]), tk, sl, C.byref(st_in), _ptr(nz), eos,
+                        self._cfg.eos_guard, self._cfg.budget_extra, self._cfg.text_guard,
+                        self._cfg.progress_scale, self.max_gen, self.max_audio, C.byref(out_st), C.byref(tok)),
+                        "host_sample")
+                    out_st.ambiguous_steps = st_in.ambiguous_steps + 1
+                    _lib.check(L.t5g_write_state(self.h, C.byref(out_st), b, st_in.cur_num_gen, tok.value, stream),
+                               "write_state")
+                    ctx["ambiguous_fixed"] += 1
+                    limit += 1
+                # the resolved rows' next logits (the other rows recompute theirs: same inputs)
+                _lib.check(L.t5g_step_only(self.h, stream), "step")
+                _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
+                continue
             if rec is not None:
                 rec.append(self.logits(B).clone())
-            _lib.check(L.t5g_sample_only(self.h, B, C.c_void_p(self._logits_ptr), self.logits_ld, stream), "sample")
-            _lib.check(L.t5g_read_step(self.h, nxt, flags, B, stream), "read_step")
-            fixed = False
-            for b in range(B):
-                if cur[b].done or not (flags[b] & 1):
-                    continue
-                lg = self.logits(B)[b].contiguous().cpu()
-                nz = noise[b, cur[b].cur_num_gen].contiguous().cpu()
-                out_st = _lib.SamplerState()
-                tok = C.c_int32()
-                _lib.check(L.t5g_host_sample(
-                    _ptr(lg), self.V, C.byref(rows[b]), tk, sl, C.byref(cur[b]), _ptr(nz), eos,
-                    self._cfg.eos_guard, self._cfg.budget_extra, self._cfg.text_guard,
-                    self._cfg.progress_scale, self.max_gen, self.max_audio, C.byref(out_st), C.byref(tok)),
-                    "host_sample")
-                out_st.ambiguous_steps = cur[b].ambiguous_steps + 1
-                _lib.check(L.t5g_write_state(self.h, C.byref(out_st), b, cur[b].cur_num_gen, tok.value,
-                                             stream), "write_state")
-                ctx["ambiguous_fixed"] += 1
-                fixed = True
-            if fixed:
-                _lib.check(L.t5g_read_state(self.h, nxt, B, stream), "read_state")
-            C.memmove(cur, nxt, C.sizeof(cur))
-            ctx["steps"] += 1
-            if not all(cur[b].done for b in range(B)):
-                _lib.check(L.t5g_step_only(self.h, stream), "step")
+                n = 1
+            else:
+                n = max(1, min(chunk, max(budget[b] + 1 - cur[b].cur_num_gen for b in active)))
+            _lib.check(L.t5g_decode(self.h, n, 1 if use_graph else 0, stream), "decode")
+            ctx["steps"] += n
+            _lib.check(L.t5g_read_state(self.h, cur, B, stream), "read_state")
+            if ctx["steps"] > limit + chunk:
+                raise RuntimeError("parity decode did not terminate within the time budget")
         ctx["rec"] = rec
 
     def _collect(self, ctx, stream):

@@ -57,9 +57,13 @@ def _hdr(shape, g):
     (8, 18432, 2304, 0, 3), (2, 65541, 2304, 0, 1), (17, 300, 128, 0, 0), (9, 256, 128, 0, 3),
     # split-K launches (<= 8 rows, < 256 row tiles): K parts, bias, GEGLU, a ragged last tile
     (8, 2304, 9216, 2304, 3), (7, 1024, 9216, 3072, 1), (1, 1028, 2304, 0, 1), (6, 2304, 9216, 4608, 4),
+    # f32-MFMA shapes: 17-32 decode rows (two row tiles), prefill tiles of 4 x 16 rows
+    (32, 2304, 9216, 4608, 0), (24, 18432, 2304, 0, 3), (100, 4096, 2304, 768, 0), (160, 2304, 2304, 0, 4),
 ])
-def test_exact_linear_bitwise_vs_cpu_order(M, N, K, kb, epi):
-    """t5g_exact_linear == oracle.cpu_order.linear (the reference host's F.linear order)."""
+@pytest.mark.parametrize("fn", ["t5g_exact_linear", "t5g_xmm_linear"])
+def test_exact_linear_bitwise_vs_cpu_order(M, N, K, kb, epi, fn):
+    """t5g_exact_linear (VALU chains) and t5g_xmm_linear (the engine's f32-MFMA chains) ==
+    oracle.cpu_order.linear (the reference host's F.linear order)."""
     _need_gpu()
     from oracle import cpu_order
     from t5gemma_tts_amd import _lib
@@ -73,7 +77,9 @@ def test_exact_linear_bitwise_vs_cpu_order(M, N, K, kb, epi):
     lut = torch.frombuffer(bytearray(_lib.gelu_erf_table()), dtype=torch.int16).cuda()
     n_out = N // 2 if epi == 3 else N
     Y = torch.zeros(M, n_out, dtype=torch.float32 if epi == 4 else BF16, device="cuda")
-    rc = L.t5g_exact_linear(C.c_void_p(Xd.data_ptr()), K, M, C.c_void_p(Wp.data_ptr()), N, K, kb // 32,
+    if fn == "t5g_exact_linear" and M > 256:
+        pytest.skip("VALU kernel: the engine no longer runs it on prefill shapes")
+    rc = getattr(L, fn)(C.c_void_p(Xd.data_ptr()), K, M, C.c_void_p(Wp.data_ptr()), N, K, kb // 32,
                             C.c_void_p(bd.data_ptr()), C.c_void_p(lut.data_ptr()), C.c_void_p(Y.data_ptr()), n_out,
                             epi, _st())
     assert rc == 0
