@@ -70,6 +70,24 @@ def make_batch(cfg, n: int, seed: int, T_x: int = T_X, T_p: int = T_P):
     return rows
 
 
+def cpu_model() -> str:
+    """The host CPU (model name of /proc/cpuinfo, and the logical CPUs the process may use)."""
+    name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 0
+    return f"{name} ({n} logical CPUs visible)"
+
+
 def cpu_baseline(cfg, sd_gpu, utt, n_budget: int):
     """The CPU oracle (the reference's algorithm in PyTorch CPU ops, pinned bitwise to the
     reference's golden vectors) on one utterance of the workload, batch 1 as the reference.
@@ -123,6 +141,7 @@ def cpu_baseline(cfg, sd_gpu, utt, n_budget: int):
     steps = a * n_budget + b * sum(L0 + i for i in range(n_budget))
     total = t_pre + steps
     return {"value": round(n_budget / total, 3), "unit": "audio tokens/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"1 utterance of this workload (T_x {len(x)}, T_p {len(y)}), batch 1 (reference semantics): "
                       f"encoder + prefill {t_pre:.1f} s timed; decode step times at cache lengths "
                       + ", ".join(f"{int(l)}: {t * 1e3:.0f} ms" for l, t in pts)
@@ -137,6 +156,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--parity-steps", type=int, default=1,
+                    help="timed generate() calls of the parity (drop-in default) path reported in the line's "
+                         "`parity` object (0: skip)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
                     help="BASELINE config: c2 / c3 (default) / c4 / c5 (= --e2e)")
     ap.add_argument("--parity", action="store_true",
@@ -194,7 +216,7 @@ def main():
     torch.manual_seed(1234)
     sd = synthetic_weights(cfg, seed=1234, device=str(dev))
     n_tok_row = DUR_FRAMES + int(cfg.extra_budget) + 1
-    eng = T5GemmaTTSEngine(cfg, sd, device=str(dev), max_batch=B, max_text=64,
+    eng = T5GemmaTTSEngine(cfg, sd, device=str(dev), max_batch=B, max_text=128,   # the engine default
                            max_audio=wl_tp + 1 + n_tok_row + 8, max_gen=n_tok_row + 4)
     if args.no_fused:
         eng.set_fused(False)
@@ -211,22 +233,35 @@ def main():
     G = B * world
     rows = costs = None
     if rank == 0:
-        rows = [[len(x), tgt] + x + y for x, y, tgt in make_batch(cfg, G, seed=20251226, T_x=wl_tx, T_p=wl_tp)]
+        # [len(x), tgt, global request index] + x + y: the index seeds the row, so a request
+        # samples the same tokens whatever rank / slot it is sharded to
+        rows = [[len(x), tgt, gi] + x + y
+                for gi, (x, y, tgt) in enumerate(make_batch(cfg, G, seed=20251226, T_x=wl_tx, T_p=wl_tp))]
         costs = [r[1] for r in rows]
     params = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3,
                             eos_disabled=not (args.natural_eos or args.parity))
+    # the drop-in default path accepts EOS as the reference does
+    params_parity = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3, eos_disabled=False)
+    parity_stats = {"tokens": 0, "host_resolved": 0, "tie_cuts": 0}
+
+    def request_seed(step_i: int, gidx: int) -> int:
+        return 1000 * step_i + gidx
     speed_lines = []
     gen_tokens = [0]
     audio_frames = [0]
 
-    def generate(shard, i):
-        utts = [Utterance(x=r[2:2 + r[0]], y=r[2 + r[0]:], tgt_y_len=r[1]) for r in shard]
+    def generate(shard, i, parity=None):
+        parity = args.parity if parity is None else parity
+        utts = [Utterance(x=r[3:3 + r[0]], y=r[3 + r[0]:], tgt_y_len=r[1]) for r in shard]
         t_call = time.perf_counter()
-        out = eng.generate(utts, params, seeds=[1000 * i + rank * B + b for b in range(len(utts))], chunk=64,
-                           parity=args.parity)
+        out = eng.generate(utts, params_parity if parity else params, seeds=[request_seed(i, r[2]) for r in shard],
+                           chunk=64, parity=parity)
         n_gen = sum(len(g) for g in out["gen"])
         gen_tokens[0] += n_gen
-        if args.parity:
+        if parity:
+            parity_stats["tokens"] += n_gen
+            parity_stats["host_resolved"] += out["ambiguous_fixed"]
+            parity_stats["tie_cuts"] += sum(out["ambiguous"])
             # the reference's own report (inference_tts_utils.py:308-321)
             dt_call = time.perf_counter() - t_call
             speed_lines.append(f"[Speed] {n_gen / dt_call:.2f} tokens/s | RTF: {n_gen / 50.0 / dt_call:.2f}x | "
@@ -273,6 +308,31 @@ def main():
     else:
         tokens_all, frames_all, dt_max = float(tokens), float(audio_frames[0]), dt
     value = tokens_all / dt_max
+
+    # ---- the drop-in default path (parity mode: token-exact to the reference) on the same
+    # workload, timed after the headline region: one untimed warm-up, PARITY_STEPS timed
+    parity_line = None
+    if world == 1 and not args.e2e and not args.parity and args.parity_steps > 0:
+        saved = gen_tokens[0]
+        generate(rows, 50, parity=True)   # warm-up: exact weight images, graphs
+        torch.cuda.synchronize(dev)
+        for k in parity_stats:
+            parity_stats[k] = 0
+        tp0 = time.perf_counter()
+        for i in range(args.parity_steps):
+            generate(rows, 200 + i, parity=True)
+        torch.cuda.synchronize(dev)
+        dtp = time.perf_counter() - tp0
+        gen_tokens[0] = saved
+        parity_line = {
+            "value": round(parity_stats["tokens"] / dtp, 2), "unit": "audio tokens/s",
+            "ms_per_step": round(dtp / args.parity_steps * 1e3, 2), "steps": args.parity_steps,
+            "tokens": parity_stats["tokens"], "rtf_audio_s_per_wall_s": round(parity_stats["tokens"] / 50.0 / dtp, 3),
+            "top_p_tie_cuts": parity_stats["tie_cuts"], "host_resolved_steps": parity_stats["host_resolved"],
+            "mode": "parity (the drop-in default of inference_tts): exact-order kernels (logits bitwise the "
+                    "reference CPU run's), the reference's MT19937 multinomial draws generated on the GPU, "
+                    "torch.sort tie order on the GPU, EOS accepted; same workload and rows",
+        }
 
     # ---- roofline of the dominant kernel: the fused decode-MLP launch (norm + gate/up +
     # down, 127 MB of weights per layer), or the gate/up GEMV when the MLP runs unfused
@@ -362,6 +422,10 @@ def main():
                 "rtf_audio_s_per_wall_s": round(value / 50.0, 3),
                 "roofline": roof, "cpu_baseline": cpu,
             }
+            if parity_line is not None:
+                if cpu is not None:
+                    parity_line["vs_cpu_baseline"] = round(parity_line["value"] / cpu["value"], 1)
+                line["parity"] = parity_line
             if speed_lines:
                 line["reference_speed_lines"] = speed_lines[-args.steps:]
         print(json.dumps(line), flush=True)

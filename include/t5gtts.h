@@ -295,6 +295,10 @@ int t5g_engine_set_sampler_path(t5g_engine* e, int32_t single_block);
  * (hf_export/modeling_t5gemma_voice.py:256-323, [tf] modeling_t5gemma.py:81-97); no
  * reference-side equivalent switch. */
 int t5g_engine_set_fused(t5g_engine* e, int32_t enable);
+/* Host hint: the longest text (encoder length) of the batch the next t5g_encode / t5g_decode
+ * calls run (0: assume max_text). The persistent decode launch reads at most 64 cross keys
+ * per row, so it is chosen when the batch's texts fit, whatever the engine's max_text. */
+int t5g_engine_set_text_max(t5g_engine* e, int32_t n);
 /* Test hook: store `code` (non-zero) in the fused launch's sticky timeout word, as a
  * hand-off that gave up waiting would: every later in-launch wait gives up at once, the next
  * t5g_read_tokens returns T5G_EHANDOFF and clears the counters (tests/test_gpu_fused.py:
@@ -317,7 +321,7 @@ int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void* stream, f
  * exact-erf form, equal except on 24 inputs in [-5.4, -3.1]); threads: the reference
  * host's torch thread count (8, the only measured K-split table; others -> EUNSUPPORTED).
  * enable = 0 returns to the fast kernels. Per-utterance token counts (text, prompt + 1)
- * must not exceed 512 in parity mode (the measured table). Synchronous. */
+ * must not exceed 1024 in parity mode (the measured table, csrc/ref_ksplit.h). Synchronous. */
 int t5g_engine_set_exact(t5g_engine* e, int32_t enable, const uint16_t* gelu_lut, int32_t threads);
 /* Single exact-order Linear on caller buffers (parity tests): Y = X . W^T on a packed W in
  * the reference's order (32-element E/O chunk chains, chunk sums folded; K split into

@@ -129,6 +129,7 @@ SIGNATURES = {
     "t5g_engine_set_exact": (C.c_int, [_P, _I, _P, _I]),
     "t5g_engine_set_sampler_path": (C.c_int, [_P, _I]),
     "t5g_engine_set_fused": (C.c_int, [_P, _I]),
+    "t5g_engine_set_text_max": (C.c_int, [_P, _I]),
     "t5g_engine_poison_handoff": (C.c_int, [_P, C.c_uint32]),
     "t5g_time_decode_mlp": (C.c_int, [_P, _I, _I, _P, C.POINTER(_F)]),
     "t5g_exact_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
@@ -164,7 +165,7 @@ def gelu_erf_table():
 # the K-split table of the reference host's F.linear was measured for this many threads
 # and per-utterance token counts up to EXACT_MAX_TOKENS (csrc/ref_ksplit.h)
 EXACT_THREADS = 8
-EXACT_MAX_TOKENS = 512
+EXACT_MAX_TOKENS = 1024
 
 _lib = None
 

@@ -86,6 +86,7 @@ struct t5g_engine {
     float* asbuf = nullptr;   // decode attention scores of rows > 64 keys [B][Hq][max(max_audio, max_text)]
     float* ambuf = nullptr;   // decode attention chunk maxima [B][Hkv][nsplit][G]
     int B = 0;            // rows of the current call
+    int text_max = 0;     // longest text of the current call (host hint; 0: max_text)
     const bf16_t* noise = nullptr;
     int noise_steps = 0;
     const uint32_t* noise_mt = nullptr;   // parity mode: raw MT19937 outputs [B][noise_mt_steps][2 V] (noise.hip)
@@ -890,6 +891,7 @@ static FusedMlpArgs fused_block_args(t5g_engine* e, int M, int l) {
     fa.ck = e->ck[l];
     fa.cv = e->cv[l];
     fa.kv_cap = c.max_text;
+    fa.text_max = e->text_max > 0 ? e->text_max : c.max_text;
     fa.enc_len = e->enc_len;
     fa.rope_tab = e->rope_tab;
     fa.q_dim = e->q_dim;
@@ -1350,22 +1352,26 @@ extern "C" int t5g_read_state(t5g_engine* e, t5g_sampler_state* out, int32_t B, 
     return T5G_OK;
 }
 
+// The fused launches' sticky timeout word: non-zero when an in-launch hand-off gave up
+// (outputs of those launches invalid). Cleared with the counters; T5G_EHANDOFF then.
+static int check_handoff(t5g_engine* e, hipStream_t st) {
+    unsigned tmo = 0;
+    HIPCHK(hipMemcpyAsync(&tmo, e->fsync, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (!tmo) return T5G_OK;
+    fprintf(stderr, "[t5gtts] fused decode hand-off timed out (code %u)\n", tmo);
+    hipMemsetAsync(e->fsync, 0, (FM_LINE + (size_t)FM_SET_WORDS * e->c.n_dec_layers) * sizeof(unsigned), st);
+    hipStreamSynchronize(st);
+    return T5G_EHANDOFF;
+}
+
 extern "C" int t5g_read_tokens(t5g_engine* e, int32_t* out, int32_t B, void* stream) {
     if (!e || !out || B <= 0 || B > e->c.max_batch) return T5G_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipMemcpyAsync(out, e->out_tokens, (size_t)B * e->c.max_gen * sizeof(int), hipMemcpyDeviceToHost, st));
-    unsigned tmo = 0;
-    HIPCHK(hipMemcpyAsync(&tmo, e->fsync, sizeof(unsigned), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (tmo) {
-        // an in-launch hand-off of the fused MLP gave up waiting (a workgroup was not
-        // resident): the outputs are garbage; clear the counters for the next call
-        fprintf(stderr, "[t5gtts] fused MLP hand-off timed out (code %u)\n", tmo);
-        hipMemsetAsync(e->fsync, 0, (FM_LINE + (size_t)FM_SET_WORDS * e->c.n_dec_layers) * sizeof(unsigned), st);
-        hipStreamSynchronize(st);
-        return T5G_EHANDOFF;
-    }
-    return T5G_OK;
+    // an in-launch hand-off of the fused launch gave up waiting (a workgroup was not
+    // resident): the outputs are garbage; the counters are cleared for the next call
+    return check_handoff(e, st);
 }
 
 extern "C" int t5g_engine_poison_handoff(t5g_engine* e, uint32_t code) {
@@ -1373,6 +1379,15 @@ extern "C" int t5g_engine_poison_handoff(t5g_engine* e, uint32_t code) {
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(e->fsync, &code, sizeof(unsigned), hipMemcpyHostToDevice));
     HIPCHK(hipDeviceSynchronize());
+    return T5G_OK;
+}
+
+extern "C" int t5g_engine_set_text_max(t5g_engine* e, int32_t n) {
+    if (!e || n < 0 || n > e->c.max_text) return T5G_EINVAL;
+    const int before = e->text_max > 0 ? e->text_max : e->c.max_text;
+    const int after = n > 0 ? n : e->c.max_text;
+    if ((before <= 64) != (after <= 64)) drop_graphs(e);   // the decode layout baked into the graphs follows it
+    e->text_max = n;
     return T5G_OK;
 }
 
@@ -1529,7 +1544,7 @@ extern "C" int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, 
     *avg_us = ms * 1000.f / iters;
     hipEventDestroy(e0);
     hipEventDestroy(e1);
-    return T5G_OK;
+    return check_handoff(e, st);
 }
 
 // hipEvent-timed fused decode-MLP launches (bench.py roofline leg): layers rotated, so every
@@ -1561,7 +1576,7 @@ extern "C" int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void
     hipEventDestroy(e1);
     if (rc) return rc == -1 ? T5G_EUNSUPPORTED : T5G_EHIP;
     *avg_us = ms * 1000.f / (float)n;
-    return T5G_OK;
+    return check_handoff(e, st);   // a timed launch that gave up would report a false rate
 }
 
 // work = scores | chunk maxima (fp32)

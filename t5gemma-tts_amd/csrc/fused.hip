@@ -924,7 +924,7 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
             most(a.NGgu, nw) > 5 || (a.Wqkv && most(a.NGqkv, nw / 2) > 3))
             return -1;
         if (a.D != 256 || a.Hq * a.D != a.q_dim || a.Hq % a.Hkv || a.Hq > 8 ||
-            a.NGq * 16 != a.q_dim || a.NGo * 16 != a.d || a.kv_cap > 64 || a.M * a.Hq > nw || !a.o_slabs ||
+            a.NGq * 16 != a.q_dim || a.NGo * 16 != a.d || a.text_max > 64 || a.text_max > a.kv_cap || a.M * a.Hq > nw || !a.o_slabs ||
             !a.post1_w || !a.pre1_w || !a.xn1 || !a.Wq || !a.qslab || !a.ck || !a.cv || !a.enc_len || !a.rope_tab ||
             !a.att || !a.Wo || !a.oslab)
             return -1;
@@ -935,15 +935,18 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
         static_assert(FB_GU_KB == FM_NW * 6 && FB_GU_KB % 3 == 0 && FB_LDS <= FM_LDS_MAX, "gate/up LDS unit");
         if (a.d != FB_D) return -1;
         const size_t shm = FB_LDS;
-        static bool attr_b = false;
-        if (!attr_b) {
+        // function attributes and the occupancy check are per device (an engine per GPU in
+        // one process must not skip the second device's hipFuncSetAttribute)
+        if (dev < 0 || dev >= 64) return -1;
+        static bool attr_b[64] = {};
+        if (!attr_b[dev]) {
             (void)hipFuncSetAttribute((const void*)fused_block_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)FM_LDS_MAX);
             int occ = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fused_block_kernel<true>, FM_NW * 64, shm) !=
                     hipSuccess || occ < 1)
                 return -1;
-            attr_b = true;
+            attr_b[dev] = true;
         }
         if (!launch) return 0;
         hipLaunchKernelGGL(fused_block_kernel<true>, dim3((unsigned)nb), dim3(FM_NW * 64), shm, st, a);
@@ -955,12 +958,13 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
     // the norm): the last ones
     a.norm_b0 = nb - a.M;
     auto* fn = MT == 1 ? fused_mlp_kernel<1> : fused_mlp_kernel<2>;
-    static bool attr[2] = {false, false};
-    if (!attr[MT - 1]) {
+    if (dev < 0 || dev >= 64) return -1;
+    static bool attr[64][2] = {};
+    if (!attr[dev][MT - 1]) {
         (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FM_LDS_MAX);
         int occ = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, FM_NW * 64, shm) != hipSuccess || occ < 1) return -1;
-        attr[MT - 1] = true;
+        attr[dev][MT - 1] = true;
     }
     if (!launch) return 0;
     hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(FM_NW * 64), shm, st, a);

@@ -460,9 +460,15 @@ __global__ __launch_bounds__(256) void gemm_pf_kernel(GemmArgs a) {
 // one barrier per k-step. Fragments are fetched once per block instead of once per wave
 // pair, which is what bounded the register form (load issue, not MFMA). The two
 // accumulator chains and every sum are those of gemm_pf_kernel: outputs bitwise equal.
+// lgkmcnt(0) too: this wave's ds_reads of the previous k-step's stage must have completed
+// before the barrier, because right after it some wave's stage() DMA-writes that same slot.
+// With only vmcnt the compiler may sink the MFMAs (and the lgkmcnt wait before them) past
+// the barrier; an out-of-range LDS-DMA piece (a token tile's rows >= M) completes at once
+// and could overwrite the slot while the read is still pending -- the round-3 run-to-run
+// difference of the last token tile.
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" : : "n"(N) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" : : "n"(N) : "memory");
 }
 template <int EPI, int NBUF>
 __global__ __launch_bounds__(256, 2) void gemm_pfl_kernel(GemmArgs a) {

@@ -85,6 +85,7 @@ struct FusedMlpArgs {
     const bf16_t* cv;
     int kv_cap;
     const int* enc_len;       // [B] text lengths (keys of each row)
+    int text_max;             // the batch's longest text (the cross-attention stage reads <= 64 keys)
     const float* rope_tab;    // [B][D] this step's PM-RoPE cos | sin
     int q_dim, Hq, Hkv, D;
     float scale;

@@ -213,8 +213,10 @@ class T5GemmaTTSEngine:
         self._noise = DeviceNoise(self.V, self.device)
 
     def set_fused(self, enable: bool) -> None:
-        """Decode MLP half (norm -> gate/up -> down) as one persistent launch (default) or as
-        three launches; the two are bitwise equal (csrc/fused.hip)."""
+        """Fast-path decode layer after the self attention (o-proj, norm, cross-q, cross
+        attention, cross-o, norm, gate/up, down, norm, the next q|k|v) as one persistent
+        launch (default; 17-32 rows: the MLP half) or as per-op launches; bitwise equal
+        (csrc/fused.hip)."""
         _lib.check(self.L.t5g_engine_set_fused(self.h, 1 if enable else 0), "set_fused")
 
     def close(self):
@@ -277,9 +279,13 @@ class T5GemmaTTSEngine:
         if generators is not None and not parity:
             raise ValueError("generators= drives the reference RNG stream: parity=True only")
         if exact is None:
-            # the exact-order kernels restate the sdpa attention path; eager (softcap)
-            # configurations keep the fast kernels under parity=True
-            exact = parity and self.cfg.backbone.softcap == 0.0
+            exact = parity
+        if exact and self.cfg.backbone.softcap != 0.0:
+            # the exact-order kernels restate the sdpa attention path only; an eager (softcap)
+            # checkpoint would not be reproduced bit for bit -- refuse instead of degrading
+            raise ValueError("parity mode restates the reference's sdpa attention path; this configuration uses "
+                             "eager attention with a logit softcap (attn_implementation='eager'), which is not "
+                             "restated bit for bit: run with parity=False (fast kernels, tolerance parity)")
         if exact:
             for u in utts:
                 n_y = len(u.y) + 1
@@ -293,12 +299,19 @@ class T5GemmaTTSEngine:
             out = self._generate_once(utts, params, seeds, generators, parity, use_graph, chunk, record_logits, stream)
         except _lib.FusedHandoffError:
             # the fused decode launch could not have all its workgroups resident (another
-            # process on this GPU): rerun on the per-op launches, which compute the same bits
+            # process on this GPU): rerun this call on the per-op launches (the same bits),
+            # then restore the persistent launch for the next calls
+            import warnings
+            warnings.warn("fused decode launch gave up waiting (GPU shared?): call rerun on the per-op launches")
             self.set_fused(False)
             if gen_state is not None:
                 for g, st_ in zip(generators, gen_state):
                     g.set_state(st_)
-            out = self._generate_once(utts, params, seeds, generators, parity, use_graph, chunk, record_logits, stream)
+            try:
+                out = self._generate_once(utts, params, seeds, generators, parity, use_graph, chunk, record_logits,
+                                          stream)
+            finally:
+                self.set_fused(True)
         if generators is not None:
             # where the reference's loop leaves torch's generator: after len(gen) draws of V
             self._noise.advance_generators(generators, [len(row) for row in out["gen"]])
@@ -412,6 +425,7 @@ class T5GemmaTTSEngine:
         d_apos = torch.cat(apos).to(dev)
         d_alen, d_last = torch.tensor(alen, **i32), torch.tensor(last, **i32)
         L = self.L
+        _lib.check(L.t5g_engine_set_text_max(self.h, max(tlen)), "set_text_max")
         if parity:
             # the reference's multinomial draws, one stream step per sampler call (up to the row
             # budget, plus the step at which a cap forces EOS): MT19937 streams generated on a
@@ -561,7 +575,7 @@ class T5GemmaVoiceForConditionalGeneration:
 
     @torch.inference_mode()
     def inference_tts(self, x, x_lens, y, tgt_y_lens, top_k=-100, top_p=1.0, min_p=0.0, temperature=1.0,
-                      stop_repetition=3, silence_tokens=None, multi_trial=None, parity=True, seeds=None,
+                      stop_repetition=3, silence_tokens=None, multi_trial=None, parity=None, seeds=None,
                       **kwargs):
         """Reference signature and RNG contract (:565-862). With the defaults the noise of
         every step is drawn from torch's global CPU generator exactly as the reference's
@@ -572,6 +586,16 @@ class T5GemmaVoiceForConditionalGeneration:
         unless ``seeds`` is given. Batch > 1 (not allowed by the reference, :594) gives
         row i its own stream: ``seeds[i]``, or a seed drawn from the global generator."""
         cfg = self.config
+        if parity is None:
+            # the drop-in default: token-exact parity where it is restated (sdpa attention);
+            # an eager / softcap checkpoint runs the fast kernels, and says so once
+            parity = cfg.backbone.softcap == 0.0
+            if not parity and not getattr(self, "_warned_eager", False):
+                import warnings
+                warnings.warn("eager (softcap) attention checkpoint: inference_tts runs the fast kernels "
+                              "(logits within tolerance of the reference, tokens may differ); the bit-exact "
+                              "parity mode covers the sdpa attention path")
+                self._warned_eager = True
         if multi_trial:
             import warnings
             warnings.warn("multi_trial is not supported and will be ignored")   # :585-586

@@ -301,6 +301,68 @@ def gen_long_golden(RT, out="golden_long", seed=13, n_cases=2):
     np.savez_compressed(os.path.join(HERE, f"{out}.npz"), **arrays)
 
 
+def gen_cases_golden(RT, out, cases, cfg_kw, seed=13):
+    """Full-depth 2b-2b reference runs of explicit cases (tokens, top-64 logits and a sha of
+    every full logit row per step), e.g. one row of a BASELINE workload."""
+    import hashlib
+    cfg = named_config("2b2b", **cfg_kw)
+    with tempfile.TemporaryDirectory(dir=os.environ.get("GOLDEN_TMP", "/tmp")) as td:
+        m, sd = build_reference_model(RT, cfg, seed, td, lowmem=True)
+        arrays = {}
+        for ci, c in enumerate(cases):
+            res, gen, logs, dt = run_case(RT, m, cfg, c)
+            c["res"], c["gen"] = res, gen
+            c["ref_seconds"] = round(dt, 4)
+            c["n_steps"] = int(logs.shape[0])
+            top = torch.topk(logs.float(), 64, dim=-1)
+            arrays[f"top_vals_{ci}"] = bf16_bits(top.values.to(torch.bfloat16))
+            arrays[f"top_idx_{ci}"] = top.indices.numpy().astype(np.int32)
+            c["logit_sha"] = [hashlib.sha256(bf16_bits(r).tobytes()).hexdigest()[:16] for r in logs]
+            print(f"[{out}] case {ci}: T_x={len(c['x'])} T_p={len(c['y'])} gen={len(gen)} ({dt:.2f}s)", flush=True)
+        digest = state_dict_digest(sd)
+    meta = {"config": "2b2b", "config_kw": cfg_kw, "weight_seed": seed, "weight_sha256": digest,
+            "torch": torch.__version__, "threads": torch.get_num_threads(), "cases": cases}
+    with open(os.path.join(HERE, f"{out}.json"), "w") as f:
+        json.dump(meta, f)
+    np.savez_compressed(os.path.join(HERE, f"{out}.npz"), **arrays)
+
+
+def _row_case(x, y, tgt, seed, **kw):
+    c = dict(x=[int(v) for v in x], y=[int(v) for v in y], tgt=int(tgt), seed=int(seed), top_k=30, top_p=0.9,
+             min_p=0.0, temperature=0.8, stop_repetition=3, silence_tokens=[])
+    c.update(kw)
+    return c
+
+
+def gen_config_goldens(RT, which):
+    """Rows of the BASELINE workloads (bench.py make_batch, seed 20251226) run to their full
+    budget by the reference, plus a long voice-clone prompt:
+    * c2: configs[1] batch 1, T_x 32, no prompt, top-k 30 / p 0.9 / T 0.8, 10 s target;
+    * c4: configs[3] a T_x 36 no-prompt row;
+    * c1: configs[0] greedy (top_k 1, T 1.0), T_x 16, no prompt, 3 s target;
+    * longprompt: T_x 60, a 600-code prompt + y_sep (T_p 601, the prefill a 602-token
+      call), 16 steps -- past the 512-token K-split table of round 3."""
+    sys.path.insert(0, REPO)
+    from bench import make_batch
+    cfg = named_config("2b2b", extra_cutoff=5.0)
+    if "c2" in which:
+        x, y, tgt = make_batch(cfg, 1, seed=20251226, T_x=32, T_p=0)[0]
+        gen_cases_golden(RT, "golden_c2", [_row_case(x, y, tgt, 4000)], {"extra_cutoff": 5.0})
+    if "c4" in which:
+        x, y, tgt = make_batch(cfg, 1, seed=20251226, T_x=36, T_p=0)[0]
+        gen_cases_golden(RT, "golden_c4", [_row_case(x, y, tgt, 4100)], {"extra_cutoff": 5.0})
+    if "c1" in which:
+        x, y, _ = make_batch(cfg, 1, seed=20251226, T_x=16, T_p=0)[0]
+        gen_cases_golden(RT, "golden_c1", [_row_case(x, y, 150, 4200, top_k=1, top_p=1.0, temperature=1.0)],
+                         {"extra_cutoff": 5.0})
+    if "longprompt" in which:
+        steps = 16
+        kw = {"extra_cutoff": (steps - 2) / 50.0}
+        cfgl = named_config("2b2b", **kw)
+        x, y, _ = make_batch(cfgl, 1, seed=20251226, T_x=60, T_p=601)[0]
+        gen_cases_golden(RT, "golden_longprompt", [_row_case(x, y, len(y) + 1, 4300)], kw)
+
+
 def gen_sampler_golden(RU, out="golden_sampler", V=65541, n=48):
     """Per-step sampler cases at the real vocab: reference topk_sampling +
     torch.multinomial under torch.manual_seed(seed). Logits regenerable from
@@ -359,6 +421,9 @@ if __name__ == "__main__":
         gen_full_golden(RT)
     if "long" in todo:
         gen_long_golden(RT)
+    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt")]
+    if cfg_todo:
+        gen_config_goldens(RT, cfg_todo)
     if "mid" in todo:
         gen_model_golden(RT, "mid", {}, seed=11, n_cases=2, out="golden_mid", store_logits="top",
                          max_tx=40, tgt_frames=(4, 8))

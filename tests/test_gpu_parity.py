@@ -282,7 +282,10 @@ def test_tiny_engine_vs_reference_golden(name):
     divergences = []
     for ci, c in enumerate(meta["cases"]):
         u = Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"])
-        out = eng.generate([u], _params(c), seeds=[c["seed"]], parity=True, record_logits=True)
+        # eager (softcap) configurations: the reference RNG and sampler with the fast kernels
+        # (parity mode's exact-order kernels restate the sdpa path and refuse eager)
+        out = eng.generate([u], _params(c), seeds=[c["seed"]], parity=True, record_logits=True,
+                           exact=False if name == "golden_tiny_eager" else None)
         w, ex = teacher_forced_check(cfg, sd, u, _oparams(c), c["seed"], out, rtol=0.02)
         worst = max(worst, w)
         rows_exact += ex

@@ -83,6 +83,9 @@ SHAPES = {
     # (N, K): q, k/v, o, gate/up, down, head1, head2 of T5Gemma-2b-2b
     "2b2b": [(2048, 2304), (1024, 2304), (2304, 2048), (9216, 2304), (2304, 9216), (2304, 2304), (65541, 2304)],
     "tiny": [(128, 128), (64, 128), (128, 128), (256, 128), (128, 256), (69, 128)],
+    # the decoder / encoder layer shapes only: the calls made with one utterance's prompt or
+    # text (M > 512 for long reference clips); the head is called on one row
+    "2b2b_layers": [(2048, 2304), (1024, 2304), (2304, 2048), (9216, 2304), (2304, 9216)],
 }
 
 
@@ -90,12 +93,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--shapes", default="2b2b")
-    ap.add_argument("--ms", default="1,2,8,13,20,32,40,42,43,48,60,64,65,100,128,152,200,256,257,300,512")
+    ap.add_argument("--ms", default="1,2,8,13,20,32,40,42,43,48,60,64,65,100,128,152,200,256,257,300,512",
+                    help="comma list, or lo-hi for a range")
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
     for N, K in SHAPES[args.shapes]:
         cands = sorted({K} | {K // d for d in (2, 3, 4, 6, 8, 9, 12, 16) if K % d == 0 and (K // d) % 32 == 0}, reverse=True)
-        for M in [int(v) for v in args.ms.split(",")]:
+        if "-" in args.ms:
+            lo, hi = (int(v) for v in args.ms.split("-"))
+            ms = list(range(lo, hi + 1))
+        else:
+            ms = [int(v) for v in args.ms.split(",")]
+        for M in ms:
             hits = probe(M, N, K, cands)
             print(json.dumps({"N": N, "K": K, "M": M, "threads": args.threads, "Kb": hits}), flush=True)
 
