@@ -70,6 +70,18 @@ def make_batch(cfg, n: int, seed: int, T_x: int = T_X, T_p: int = T_P):
     return rows
 
 
+def request_rows(cfg, G: int, T_x: int, T_p: int):
+    """The step's global request batch (drawn on rank 0): [len(x), tgt, global index] + x + y.
+    The global index seeds the request (request_seed), so a request samples the same
+    tokens whatever rank / slot run_sharded gives it."""
+    return [[len(x), tgt, gi] + x + y for gi, (x, y, tgt) in enumerate(make_batch(cfg, G, seed=20251226, T_x=T_x, T_p=T_p))]
+
+
+def request_seed(step_i: int, gidx: int) -> int:
+    """Sampling seed of global request gidx in step step_i (independent of the sharding)."""
+    return 1000 * step_i + gidx
+
+
 def cpu_model() -> str:
     """The host CPU (model name of /proc/cpuinfo, and the logical CPUs the process may use)."""
     name = "unknown"
@@ -233,10 +245,7 @@ def main():
     G = B * world
     rows = costs = None
     if rank == 0:
-        # [len(x), tgt, global request index] + x + y: the index seeds the row, so a request
-        # samples the same tokens whatever rank / slot it is sharded to
-        rows = [[len(x), tgt, gi] + x + y
-                for gi, (x, y, tgt) in enumerate(make_batch(cfg, G, seed=20251226, T_x=wl_tx, T_p=wl_tp))]
+        rows = request_rows(cfg, G, wl_tx, wl_tp)
         costs = [r[1] for r in rows]
     params = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3,
                             eos_disabled=not (args.natural_eos or args.parity))
@@ -244,8 +253,6 @@ def main():
     params_parity = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3, eos_disabled=False)
     parity_stats = {"tokens": 0, "host_resolved": 0, "tie_cuts": 0}
 
-    def request_seed(step_i: int, gidx: int) -> int:
-        return 1000 * step_i + gidx
     speed_lines = []
     gen_tokens = [0]
     audio_frames = [0]

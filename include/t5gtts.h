@@ -332,7 +332,8 @@ int t5g_exact_linear(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_d
                      int32_t epi, void* stream);
 /* The same exact-order Linear on the f32-input MFMA kernels the engine's parity mode runs
  * (csrc/xmm.hip: v_mfma_f32_16x16x4_f32 chains = the reference's E/O chunk chains); same
- * arguments and results as t5g_exact_linear, bit for bit. */
+ * arguments and results as t5g_exact_linear, bit for bit. epi | 0x2000 (M <= 32, kb32 <
+ * K / 32): the decode part mode -- Y receives each K part's fp32 fold, [parts][M][N]. */
 int t5g_xmm_linear(const void* X_dev, int32_t ldx, int32_t M, const void* Wp_dev, int32_t N, int32_t K,
                    int32_t kb32, const void* bias_dev, const void* gelu_lut_dev, void* Y_dev, int32_t ldy,
                    int32_t epi, void* stream);

@@ -116,6 +116,7 @@ struct t5g_engine {
     bf16_t *head1_x = nullptr, *head2_x = nullptr;
     bf16_t *xn16 = nullptr, *att16 = nullptr, *act16 = nullptr, *mem16 = nullptr;   // packed tokens
     bf16_t *dxn16 = nullptr, *datt16 = nullptr, *dact16 = nullptr, *dhh16 = nullptr;   // decode rows
+    float* dpart = nullptr;   // decode down projection: fp32 K-part values [4][B16][hidden]
     bool xmm_ready = false;
 };
 
@@ -359,6 +360,41 @@ static int xlin16(t5g_engine* e, const bf16_t* X16, int M, const bf16_t* W16, in
     return xmm(a, epi, st);
 }
 
+// The reference's K part (chunks) of Linear (N, K) called with M rows; KB when not split
+static int ksplit_host(int N, int K, int M) {
+    for (int i = 0; i < REF_KSPLIT_NSHAPES; ++i)
+        if (ref_ksplit_shapes[i].N == N && ref_ksplit_shapes[i].K == K && M >= 1 && M <= ref_ksplit_max_m[i]) {
+            const int v = ref_ksplit_kb32[i][M - 1];
+            return v > 0 ? v : K / 32;
+        }
+    return K / 32;
+}
+
+// Decode rows (each a reference call of M = 1): when the reference splits K at M = 1, one
+// workgroup per (group, part) writes the parts' fp32 values to e->dpart and the number of
+// parts is returned in *nparts (the consumer norm folds them); otherwise a plain bf16 Linear
+// into Y (*nparts = 0).
+static int xlin16_dec_parts(t5g_engine* e, const bf16_t* X16, int M, const bf16_t* W16, int N, int K, void* Y,
+                            int ldy, const int* tok_row, int* nparts, hipStream_t st) {
+    const int kbc = ksplit_host(N, K, 1), KB = K / 32;
+    *nparts = 0;
+    if (kbc >= KB || M > 32 || (KB + kbc - 1) / kbc > 4 || N > e->c.hidden)
+        return xlin16(e, X16, M, W16, N, K, nullptr, Y, ldy, nullptr, EPI_BF16, tok_row, nullptr, N, 0, 0, st);
+    XmmArgs a;
+    memset(&a, 0, sizeof(a));
+    a.X16 = X16;
+    a.M = M;
+    a.W = W16;
+    a.N = N;
+    a.NG = ng_pad(N);
+    a.KB = KB;
+    a.part_out = e->dpart;
+    a.part_kbc = kbc;
+    RC(xmm(a, EPI_F32, st));
+    *nparts = (KB + kbc - 1) / kbc;
+    return T5G_OK;
+}
+
 // VALU exact Linear (exact.hip), kept for the A/B entry point t5g_exact_linear
 [[maybe_unused]] static int xlin(t5g_engine* e, const bf16_t* X, int ldx, int M, const void* W, int N, int K, const void* bias,
                 void* Y, int ldy, int epi, const int* tok_row, const int* row_len, int nref_a, int nref_b,
@@ -567,12 +603,19 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
             n.resid_out = h;
             n.normed_out = xn;
             n.normed_x16 = xn16;
+            if (decode) {   // and the step's RoPE table (exact cos / sin), in the same launch
+                n.rope_pos = pos;
+                n.rope_inv_freq = e->w.inv_freq;
+                n.rope_tab = e->rope_tab;
+                n.rope_D = D;
+            }
             RC(resid_norm(n, st));
         }
         // self attention
         RC(xlin16(e, xn16, M, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
                   e->q_dim, e->kv_dim, e->q_dim, st));
         RopeArgs r = xrope_args(M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
+        r.rope_tab = decode ? e->rope_tab : nullptr;
         r.X = e->qkv;
         r.ldx = e->qkv_dim;
         r.nq = c.n_heads;
@@ -593,6 +636,7 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         RC(xlin16(e, xn16, M, X.cross_q, e->q_dim, d, nullptr, q, e->q_dim, nullptr, EPI_BF16, tok_row, rl, e->q_dim, 0,
                   0, st));
         r = xrope_args(M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
+        r.rope_tab = decode ? e->rope_tab : nullptr;
         r.X = q;
         r.ldx = e->q_dim;
         r.nq = c.n_heads;
@@ -605,9 +649,29 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         RC(norm(L.norms[3], L.norms[4]));
         // GeGLU MLP: act straight into the down projection's operand order
         RC(xlin16(e, xn16, M, X.gate_up, 2 * f, d, nullptr, nullptr, f, act16, EPI_GEGLU, tok_row, rl, f, 0, 0, st));
-        RC(xlin16(e, act16, M, X.down, d, f, nullptr, tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0, st));
         const bool last = l == c.n_dec_layers - 1;
-        RC(norm(L.norms[5], last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]));
+        if (decode) {
+            int np = 0;
+            RC(xlin16_dec_parts(e, act16, M, X.down, d, f, tmp, d, tok_row, &np, st));
+            NormArgs n = xnorm_args(M, d, c.rms_eps);
+            if (np) {
+                n.part = e->dpart;
+                n.nsplit = np;
+                n.ldp = d;
+            } else {
+                n.delta = tmp;
+            }
+            n.post_w = (const bf16_t*)L.norms[5];
+            n.resid = h;
+            n.pre_w = (const bf16_t*)(last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]);
+            n.resid_out = h;
+            n.normed_out = xn;
+            n.normed_x16 = xn16;
+            RC(resid_norm(n, st));
+        } else {
+            RC(xlin16(e, act16, M, X.down, d, f, nullptr, tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0, st));
+            RC(norm(L.norms[5], last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]));
+        }
     }
     return T5G_OK;
 }
@@ -669,6 +733,7 @@ static int xmm_prepare(t5g_engine* e) {
     RC(alloc(e, &e->datt16, B16 * e->q_dim));
     RC(alloc(e, &e->dact16, B16 * f));
     RC(alloc(e, &e->dhh16, B16 * d));
+    RC(alloc(e, &e->dpart, 4 * B16 * d));
     HIPCHK(hipDeviceSynchronize());
     e->xmm_ready = true;
     return T5G_OK;
@@ -1741,6 +1806,7 @@ extern "C" int t5g_time_xmm(const void* X16, int32_t M, const void* const* W16_l
     if (epi & 0x1000) a.Y16 = (bf16_t*)Y;
     else a.Y = Y;
     a.ldy = ldy;
+    a.timing_var = (epi & 0x4000) ? 1 : ((epi & 0x8000) ? 2 : 0);   // decode-kernel timing variants
     epi &= 0xff;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
@@ -1786,11 +1852,16 @@ extern "C" int t5g_xmm_linear(const void* X, int32_t ldx, int32_t M, const void*
         a.NG = ng_pad(N);
         a.KB = K / 32;
         a.bias = (const bf16_t*)bias;
-        a.Y = Y;
-        a.ldy = ldy;
-        a.kb_fixed = kb32;
+        if (epi & 0x2000) {   // K parts of kb32 chunks: Y = fp32 part values [parts][M][N]
+            a.part_out = (float*)Y;
+            a.part_kbc = kb32;
+        } else {
+            a.Y = Y;
+            a.ldy = ldy;
+            a.kb_fixed = kb32;
+        }
         a.gelu_lut = (const uint16_t*)gelu_lut;
-        rc = xmm(a, epi, st);
+        rc = xmm(a, epi & 0xff, st);
     }
     hipFreeAsync(w16, st);
     hipFreeAsync(x16, st);

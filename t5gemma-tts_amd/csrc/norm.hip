@@ -69,8 +69,15 @@ __device__ __forceinline__ float ref_sumsq(const float (&v)[8], bool active, int
         const int size_ilp = nvec / 4;
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
         int i = 0;
+        // each level-0 row of 16 is read into registers first (one LDS round trip, not 16
+        // dependent ones), then added in order
         while (i + 16 <= size_ilp) {
-            for (int q = 0; q < 16; ++q, ++i) a0 = __fadd_rn(a0, sq[(i * 4 + k) * 8 + j]);
+            float t[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t[q] = sq[((i + q) * 4 + k) * 8 + j];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) a0 = __fadd_rn(a0, t[q]);
+            i += 16;
             a1 = __fadd_rn(a1, a0);
             a0 = 0.f;
             if (i & 0xF0) continue;
@@ -80,7 +87,14 @@ __device__ __forceinline__ float ref_sumsq(const float (&v)[8], bool active, int
             a3 = __fadd_rn(a3, a2);
             a2 = 0.f;
         }
-        for (; i < size_ilp; ++i) a0 = __fadd_rn(a0, sq[(i * 4 + k) * 8 + j]);
+        {
+            float t[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t[q] = sq[(min(i + q, max(size_ilp - 1, 0)) * 4 + k) * 8 + j];
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (i + q < size_ilp) a0 = __fadd_rn(a0, t[q]);
+        }
         a0 = __fadd_rn(__fadd_rn(__fadd_rn(a0, a1), a2), a3);
         if (k == 0)
             for (int t = size_ilp * 4; t < nvec; ++t) a0 = __fadd_rn(a0, sq[t * 8 + j]);
@@ -165,8 +179,8 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
         for (int s = 0; s < NS; ++s) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                v[j] += p[s][0][j];
-                v[4 + j] += p[s][1][j];
+                v[j] = __fadd_rn(v[j], p[s][0][j]);
+                v[4 + j] = __fadd_rn(v[4 + j], p[s][1][j]);
             }
         }
 #pragma unroll
@@ -221,10 +235,15 @@ int resid_norm(const NormArgs& a_in, hipStream_t st) {
 #define T5G_NORM(NS_, SRC_) \
     hipLaunchKernelGGL((resid_norm_kernel<NS_, SRC_>), g, b, 0, st, a, has_post, has_resid, has_pre)
     if (a.exact) {
-        // parity mode: the reference's CPU sum order (part slabs are not used there)
-        if (src == 2 || a.d > 8 * 1024) return -1;
+        // parity mode: the reference's CPU sum order. Part slabs: the K parts of an exact
+        // Linear (xmm part_out), v = bf16((0 + p0) + p1 ...) = the reference's fold of parts
+        if (a.d > 8 * 1024 || (src == 2 && a.nsplit > 4)) return -1;
         if (src == 0) hipLaunchKernelGGL((resid_norm_kernel<0, 0, true>), g, b, 0, st, a, has_post, has_resid, has_pre);
-        else hipLaunchKernelGGL((resid_norm_kernel<0, 1, true>), g, b, 0, st, a, has_post, has_resid, has_pre);
+        else if (src == 1) hipLaunchKernelGGL((resid_norm_kernel<0, 1, true>), g, b, 0, st, a, has_post, has_resid, has_pre);
+        else if (a.nsplit == 1) hipLaunchKernelGGL((resid_norm_kernel<1, 2, true>), g, b, 0, st, a, has_post, has_resid, has_pre);
+        else if (a.nsplit == 2) hipLaunchKernelGGL((resid_norm_kernel<2, 2, true>), g, b, 0, st, a, has_post, has_resid, has_pre);
+        else if (a.nsplit == 3) hipLaunchKernelGGL((resid_norm_kernel<3, 2, true>), g, b, 0, st, a, has_post, has_resid, has_pre);
+        else hipLaunchKernelGGL((resid_norm_kernel<4, 2, true>), g, b, 0, st, a, has_post, has_resid, has_pre);
     } else if (src == 0) T5G_NORM(0, 0);
     else if (src == 1) T5G_NORM(0, 1);
     else switch (a.nsplit) {

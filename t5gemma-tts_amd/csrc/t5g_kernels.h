@@ -247,6 +247,12 @@ struct XmmArgs {
     int nsplit_col, kb_len;
     int kb_fixed;             // > 0: every row splits K into parts of kb_fixed chunks (no tables)
     const uint16_t* gelu_lut;
+    // decode rows whose K parts are all part_kbc chunks: one workgroup per (group, part),
+    // each writes its part's fp32 fold to part_out[part][M][N] (the consumer adds them in
+    // order from 0, as the reference's fold of parts; resid_norm's part source)
+    float* part_out;
+    int part_kbc;
+    int timing_var;           // t5g_time_xmm only: 1 decode kernel without the fold, 2 without the MFMA
 };
 int xmm(const XmmArgs& a, int epi, hipStream_t st);
 int pack_e16(const bf16_t* p16, bf16_t* e16, long bytes, hipStream_t st);

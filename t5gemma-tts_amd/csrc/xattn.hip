@@ -129,8 +129,17 @@ __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const fl
     float dst = 0.f;                             // folder (g, dim) = tid < G * XD_DZ
     const int fg = tid / XD_DZ, fd = tid % XD_DZ;
     __syncthreads();
+    constexpr int GPL = NGRP / GL;               // 8-key groups per lane and block (4)
     for (int b = 0; b < nblk; ++b) {
         const int bs = b * BLK, blen = min(BLK, span - bs);
+        // V words of this lane's groups gl + GL t, issued first: they fly during the exact
+        // p and the block sums (keys past the block re-read its last key, unused)
+        uint32_t vw[GPL][8];
+#pragma unroll
+        for (int t = 0; t < GPL; ++t)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                vw[t][j] = *(const uint32_t*)(Vb + (long)(bs + min((gl + GL * t) * 8 + j, blen - 1)) * XD_D + 2 * dp);
         // exact p of the block's keys
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -154,12 +163,11 @@ __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const fl
         // 8-key group chains of the slice: lane gl takes groups gl, gl + 16, ... (pairs, odd
         // key first; keys past the block count 0 and add nothing: the chain stops there)
         const int ngrp = (blen + 7) / 8;
-        for (int gi = gl; gi < ngrp; gi += GL) {
-            const int k0 = gi * 8, cn = min(8, blen - k0);
-            uint32_t vw[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                vw[j] = *(const uint32_t*)(Vb + (long)(bs + k0 + (j < cn ? j : 0)) * XD_D + 2 * dp);
+        for (int t = 0; t < GPL; ++t) {
+            const int gi = gl + GL * t;
+            if (gi >= ngrp) break;
+            const int k0 = gi * 8, cn = min(8, blen - k0);
             float t0[G], t1[G];
 #pragma unroll
             for (int g = 0; g < G; ++g) {
@@ -170,12 +178,12 @@ __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const fl
                     if (j < cn) {
                         if (j + 1 < cn) {
                             const float p1 = pbf[g][k0 + j + 1];
-                            t0[g] = fmaf(p1, bf_lo(vw[j + 1]), t0[g]);
-                            t1[g] = fmaf(p1, bf_hi(vw[j + 1]), t1[g]);
+                            t0[g] = fmaf(p1, bf_lo(vw[t][j + 1]), t0[g]);
+                            t1[g] = fmaf(p1, bf_hi(vw[t][j + 1]), t1[g]);
                         }
                         const float p0 = pbf[g][k0 + j];
-                        t0[g] = fmaf(p0, bf_lo(vw[j]), t0[g]);
-                        t1[g] = fmaf(p0, bf_hi(vw[j]), t1[g]);
+                        t0[g] = fmaf(p0, bf_lo(vw[t][j]), t0[g]);
+                        t1[g] = fmaf(p0, bf_hi(vw[t][j]), t1[g]);
                     }
                 }
                 tmp[gi][g][2 * dp] = t0[g];
@@ -185,7 +193,15 @@ __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const fl
         __syncthreads();
         if (tid < G * XD_DZ) {
             float acc = bs == 0 ? 0.f : __fmul_rn(dst, et_s[fg]);
-            for (int gi = 0; gi < ngrp; ++gi) acc = __fadd_rn(acc, tmp[gi][fg][fd]);
+            // 16 group sums read per batch (one LDS round trip), then added in order
+            for (int g0 = 0; g0 < ngrp; g0 += 16) {
+                float t[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) t[u] = tmp[min(g0 + u, NGRP - 1)][fg][fd];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (g0 + u < ngrp) acc = __fadd_rn(acc, t[u]);
+            }
             dst = acc;
         }
         __syncthreads();   // pex / pbf / tmp / et_s are rewritten by the next block

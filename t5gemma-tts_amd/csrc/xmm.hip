@@ -22,11 +22,10 @@
 //
 // Two launch shapes:
 // * xmm_wave_kernel: one wave per (16-output group, RT row tiles), every chunk of K in
-//   order, folds in registers -- prefill / encoder (thousands of tiles) and the wide
-//   decode projections (gate/up: 1 152 groups, the 65 541-row head: 4 097);
-// * xmm_split_kernel: decode projections with fewer groups (N = 2 048 ... 4 096): one
-//   1 024-thread workgroup per group, its 16 waves split the chunks of a stage, chunk sums
-//   go through LDS, 4 waves fold them in order.
+//   order, folds in registers -- prefill / encoder (M > 32: thousands of tiles);
+// * xmm_dec_kernel: decode rows (M <= 32): one 512-thread workgroup per group (and K part
+//   where the reference splits K at M = 1: the down projection), its 8 waves split the
+//   chunks, chunk sums go through LDS, one thread per output folds them in order.
 #include "common.h"
 #include "exact_math.h"
 #include "t5g_kernels.h"
@@ -244,85 +243,141 @@ __global__ __launch_bounds__(256) void xmm_wave_kernel(XmmArgs a) {
     }
 }
 
-// ---- decode, fewer groups: one workgroup per group, 16 waves split each stage's chunks,
-// chunk sums in LDS [chunk][reg][lane], threads 0..255 (element reg = t >> 6, lane = t & 63)
-// fold them in order. RT row tiles (M <= 16 RT).
-template <int RT, int EPI>
-__global__ __launch_bounds__(1024) void xmm_split_kernel(XmmArgs a) {
-    constexpr int NW = 16, SC = RT == 1 ? 96 : 48, CPW = SC / NW;
-    __shared__ float cs[SC][RT][4][64];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int g = blockIdx.x;
-    const int KB = a.KB;
+// ---- decode rows (M <= 32): one 512-thread workgroup per (16-output group, K part) ----
+// The 8 waves take the chunks of a stage round-robin and issue every chunk's operand loads
+// up front (CPW chunks per wave in flight), chunk sums go to LDS as [chunk][row][col]
+// (only the ROWS rows that exist: 8 when M <= 8, so two or more workgroups share a CU),
+// then thread t < 16 ROWS folds element (row t >> 4, col t & 15) over the chunks in order
+// and stores it: consecutive threads write consecutive outputs of a row.
+// PART: the group's chunks [p part_kbc, (p + 1) part_kbc) only, folded from 0 into
+// part_out[p] -- the reference's part value, summed in order by the consumer.
+template <int RT, bool R8>
+struct XDecShape {
+    static constexpr int NW = 8, CPW = RT == 1 ? 9 : 5, SC = NW * CPW;
+    static constexpr int ROWS = R8 ? 8 : 16 * RT, EL = 16 * ROWS;
+    static constexpr int LDS = SC * EL * 4;
+};
+
+template <int RT, bool R8, int EPI, bool PART, int VAR = 0>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void xmm_dec_kernel(XmmArgs a) {
+    using S = XDecShape<RT, R8>;
+    constexpr int NW = S::NW, CPW = S::CPW, SC = S::SC, EL = S::EL;
+    extern __shared__ float cs[];   // [SC][EL]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j = lane & 15, q = lane >> 4;
+    const int g = blockIdx.x, KB = a.KB;
+    const int kb_lo = PART ? (int)blockIdx.y * a.part_kbc : 0;
+    const int kb_hi = PART ? min(kb_lo + a.part_kbc, KB) : KB;
     const u32x4* wp = (const u32x4*)(a.W + (long)g * KB * 512) + lane;
-    const u32x4* xp = (const u32x4*)a.X16 + lane;
-    // folder state: element (reg, lane) of each row tile
-    const bool folder = tid < 256;
-    const int freg = tid >> 6, fl = tid & 63, fj = fl & 15, fq = fl >> 4;
-    XFold f[RT];
-    int kbc[RT];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-        f[r] = XFold{0.f, 0.f, 0};
-        kbc[r] = xmm_kbc(a, min(r * 16 + fj, a.M - 1), g * 16);
-    }
+    // R8: lanes j >= 8 (rows that do not exist) read lane j - 8's operand: half the bytes
+    const u32x4* xp = (const u32x4*)a.X16 + (R8 ? (lane & ~8) : lane);
+    const int frow = tid >> 4, fcol = tid & 15;
+    const bool folder = tid < EL;
+    // decode rows (no per-row lengths) share the K-part length: a scalar, so the fold's part
+    // boundary test is a scalar branch; otherwise each element's own (xfold)
+    const bool uni = PART || a.kb_fixed > 0 || !a.row_len;
+    const int kbc_t = PART ? (1 << 30) : xmm_kbc(a, uni ? 0 : min(frow, a.M - 1), g * 16);
+    const int kbc_u = __builtin_amdgcn_readfirstlane(kbc_t);
+    XFold f{0.f, 0.f, kb_lo};
+    int nb_u = kb_lo;   // uniform fold: the next part's first chunk
     u32x4 wr[CPW], xr[CPW][RT];
     auto load = [&](int s0) {
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
-            const int kb = min(s0 + w + c * NW, KB - 1);
+            const int kb = min(s0 + w + c * NW, kb_hi - 1);
             wr[c] = wp[(long)kb * 64];
 #pragma unroll
             for (int r = 0; r < RT; ++r) xr[c][r] = xp[((long)r * KB + kb) * 64];
         }
     };
-    load(0);
-    for (int s0 = 0; s0 < KB; s0 += SC) {
-        const int n = min(SC, KB - s0);
+    load(kb_lo);
+    for (int s0 = kb_lo; s0 < kb_hi; s0 += SC) {
+        const int n = min(SC, kb_hi - s0);
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             const int cc = w + c * NW;
             if (cc < n) {
 #pragma unroll
                 for (int r = 0; r < RT; ++r) {
-                    const f32x4_t v = xmm_chunk(wr[c], xr[c][r]);
+                    f32x4_t v;
+                    if constexpr (VAR == 2) {   // timing variant: no MFMA
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) cs[cc][r][i][lane] = v[i];
+                        for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(wr[c][i] ^ xr[c][r][i]);
+                    } else {
+                        v = xmm_chunk(wr[c], xr[c][r]);
+                    }
+                    if (!R8 || j < 8) *(f32x4_t*)&cs[cc * EL + (r * 16 + j) * 16 + 4 * q] = v;
                 }
             }
         }
-        if (s0 + SC < KB) load(s0 + SC);   // the next stage's operands fly during the fold
+        if (s0 + SC < kb_hi) load(s0 + SC);   // the next stage's operands fly during the fold
         __syncthreads();
-        if (folder) {
-            // 8 chunk sums requested per batch, then folded in order (the adds are the chain)
+        if (VAR == 1 && folder) {   // timing variant: no fold
+            f.part = cs[tid];
+        } else if (folder && uni) {
+            // 16 chunk sums requested per batch (one LDS round trip), then folded in order
+            for (int c0 = 0; c0 < n; c0 += 16) {
+                float v[16];
 #pragma unroll
-            for (int r = 0; r < RT; ++r)
-                for (int c0 = 0; c0 < n; c0 += 8) {
-                    float v[8];
+                for (int u = 0; u < 16; ++u) v[u] = cs[min(c0 + u, SC - 1) * EL + tid];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) v[u] = cs[min(c0 + u, SC - 1)][r][freg][fl];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u)
-                        if (c0 + u < n) xfold(f[r], s0 + c0 + u, kbc[r], v[u]);
+                for (int u = 0; u < 16; ++u) {
+                    const int kb = s0 + c0 + u;
+                    if (c0 + u >= n) break;
+                    if (kb == nb_u) {   // a new K part (scalar test)
+                        if (kb > 0) f.tot = __fadd_rn(f.tot, f.part);
+                        f.part = __fadd_rn(0.f, v[u]);
+                        nb_u += kbc_u;
+                    } else {
+                        f.part = __fadd_rn(f.part, v[u]);
+                    }
                 }
+            }
+        } else if (folder) {
+            for (int c0 = 0; c0 < n; c0 += 8) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = cs[min(c0 + u, SC - 1) * EL + tid];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (c0 + u < n) xfold(f, s0 + c0 + u, kbc_t, v[u]);
+            }
         }
         __syncthreads();
     }
-    // folders hold element (reg, lane); the epilogue wants lane (q, j) with its 4 regs:
-    // regroup through LDS
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-        if (folder) cs[0][r][freg][fl] = xfold_end(f[r], KB, kbc[r]);
-    __syncthreads();
-    if (w >= 1) return;   // wave 0 stores (whole wave: GEGLU pairs lanes q, q + 2)
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-        float y[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] = cs[0][r][i][lane];
-        (void)fq;
-        xmm_store<EPI>(a, g, lane >> 4, (long)r * 16 + (lane & 15), y);
+    if (!folder) return;
+    const float y = PART ? f.part : xfold_end(f, KB, uni ? kbc_u : kbc_t);
+    const long m = frow;
+    const int n = g * 16 + fcol;
+    if constexpr (PART) {
+        if (m < a.M && n < a.N) a.part_out[((long)blockIdx.y * a.M + m) * a.N + n] = y;
+        return;
     }
+    if constexpr (EPI == EPI_GEGLU) {
+        const float up = xlane<8>(y);   // col + 8 of the same row: the up row of this feature
+        if (fcol >= 8 || m >= a.M) return;
+        const int ft = g * 8 + fcol;
+        if (ft >= a.N / 2) return;
+        const bf16_t v = f2bf(rbf(__fmul_rn(rbf(t5g_exact::gelu_tanh(rbf(y))), rbf(up))));
+        if (a.Y) ((bf16_t*)a.Y)[m * a.ldy + ft] = v;
+        if (a.Y16) a.Y16[x16_off(m, ft, a.N / 64)] = v;
+        return;
+    }
+    if (m >= a.M || n >= a.N) return;
+    if constexpr (EPI == EPI_F32) {
+        ((float*)a.Y)[m * a.ldy + n] = y;
+        return;
+    }
+    float v;
+    if constexpr (EPI == EPI_BF16) {
+        v = rbf(y);
+    } else if constexpr (EPI == EPI_BIAS_BF16) {
+        v = rbf(__fadd_rn(y, bf2f(a.bias[n])));
+    } else {   // EPI_BIAS_GELU: nn.GELU() (erf) on the bf16 Linear output
+        const bf16_t h = f2bf(__fadd_rn(y, bf2f(a.bias[n])));
+        v = bf2f(a.gelu_lut ? a.gelu_lut[h] : f2bf(t5g_exact::gelu_erf(bf2f(h))));
+    }
+    if (a.Y) ((bf16_t*)a.Y)[m * a.ldy + n] = f2bf(v);
+    if (a.Y16) a.Y16[x16_off(m, n, a.N / 32)] = f2bf(v);
 }
 
 template <int RT>
@@ -340,15 +395,41 @@ static int launch_xmm_wave(const XmmArgs& a, int epi, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <int RT>
-static int launch_xmm_split(const XmmArgs& a, int epi, hipStream_t st) {
-    const dim3 grid((unsigned)a.NG), blk(1024);
+template <int RT, bool R8, int EPI, bool PART, int VAR = 0>
+static void launch_dec1(const XmmArgs& a, hipStream_t st) {
+    using S = XDecShape<RT, R8>;
+    auto k = xmm_dec_kernel<RT, R8, EPI, PART, VAR>;
+    if (S::LDS > 64 * 1024) {   // once per device: opt in to more than 64 KiB of LDS
+        static bool done[64];
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (dev >= 0 && dev < 64 && !done[dev]) {
+            (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
+            done[dev] = true;
+        }
+    }
+    const int np = PART ? (a.KB + a.part_kbc - 1) / a.part_kbc : 1;
+    hipLaunchKernelGGL(k, dim3((unsigned)a.NG, (unsigned)np), dim3(512), S::LDS, st, a);
+}
+
+template <int RT, bool R8>
+static int launch_xmm_dec(const XmmArgs& a, int epi, hipStream_t st) {
+    if (a.part_out) {
+        launch_dec1<RT, R8, EPI_F32, true>(a, st);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
+    if (a.timing_var) {
+        if (epi != EPI_BF16) return -1;
+        if (a.timing_var == 1) launch_dec1<RT, R8, EPI_BF16, false, 1>(a, st);
+        else launch_dec1<RT, R8, EPI_BF16, false, 2>(a, st);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
     switch (epi) {
-        case EPI_F32: hipLaunchKernelGGL((xmm_split_kernel<RT, EPI_F32>), grid, blk, 0, st, a); break;
-        case EPI_BF16: hipLaunchKernelGGL((xmm_split_kernel<RT, EPI_BF16>), grid, blk, 0, st, a); break;
-        case EPI_BIAS_BF16: hipLaunchKernelGGL((xmm_split_kernel<RT, EPI_BIAS_BF16>), grid, blk, 0, st, a); break;
-        case EPI_BIAS_GELU: hipLaunchKernelGGL((xmm_split_kernel<RT, EPI_BIAS_GELU>), grid, blk, 0, st, a); break;
-        case EPI_GEGLU: hipLaunchKernelGGL((xmm_split_kernel<RT, EPI_GEGLU>), grid, blk, 0, st, a); break;
+        case EPI_F32: launch_dec1<RT, R8, EPI_F32, false>(a, st); break;
+        case EPI_BF16: launch_dec1<RT, R8, EPI_BF16, false>(a, st); break;
+        case EPI_BIAS_BF16: launch_dec1<RT, R8, EPI_BIAS_BF16, false>(a, st); break;
+        case EPI_BIAS_GELU: launch_dec1<RT, R8, EPI_BIAS_GELU, false>(a, st); break;
+        case EPI_GEGLU: launch_dec1<RT, R8, EPI_GEGLU, false>(a, st); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -356,12 +437,17 @@ static int launch_xmm_split(const XmmArgs& a, int epi, hipStream_t st) {
 
 int xmm(const XmmArgs& a, int epi, hipStream_t st) {
     if (a.M <= 0) return 0;
-    if (!a.X16 || !a.W || (!a.Y && !a.Y16) || a.N <= 0 || a.KB <= 0 || a.NG % 4 || a.NG * 16 < a.N) return -1;
+    if (!a.X16 || !a.W || (!a.Y && !a.Y16 && !a.part_out) || a.N <= 0 || a.KB <= 0 || a.NG % 4 || a.NG * 16 < a.N) return -1;
     if ((epi == EPI_BIAS_BF16 || epi == EPI_BIAS_GELU) && !a.bias) return -1;
     if (epi == EPI_GEGLU && a.N % 64) return -1;
     if (a.Y16 && (epi == EPI_F32 || (epi == EPI_GEGLU ? a.N % 64 : a.N % 32))) return -1;
-    // decode rows with too few groups to fill the chip: split the chunks over 16 waves
-    if (a.M <= 32 && a.NG < 1024) return a.M <= 16 ? launch_xmm_split<1>(a, epi, st) : launch_xmm_split<2>(a, epi, st);
+    if (a.part_out) {   // parts: decode rows only, fp32 part values (no epilogue)
+        if (a.M > 32 || a.part_kbc <= 0 || a.part_kbc >= a.KB || (a.KB + a.part_kbc - 1) / a.part_kbc > 8) return -1;
+    }
+    // decode rows: K of each group over the 8 waves of a workgroup
+    if (a.M <= 8) return launch_xmm_dec<1, true>(a, epi, st);
+    if (a.M <= 16) return launch_xmm_dec<1, false>(a, epi, st);
+    if (a.M <= 32) return launch_xmm_dec<2, false>(a, epi, st);
     if (a.M <= 16) return launch_xmm_wave<1>(a, epi, st);
     if (a.M <= 32) return launch_xmm_wave<2>(a, epi, st);
     return launch_xmm_wave<4>(a, epi, st);

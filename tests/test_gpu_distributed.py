@@ -50,7 +50,7 @@ def _engine():
                                  max_audio=128, max_gen=64)
 
 
-def _worker(rank, world, port, parity, q):
+def _worker(rank, world, port, parity, q, backend="gloo"):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import torch.distributed as dist
@@ -58,12 +58,14 @@ def _worker(rank, world, port, parity, q):
     from t5gemma_tts_amd.distributed import run_sharded
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         cfg, eng = _engine()
-        rows = _requests(cfg) if rank == 0 else None
+        rows = _requests(cfg, n=6 if world > 1 else 4) if rank == 0 else None
         costs = [r[2] for r in rows] if rank == 0 else None
-        out, mine = run_sharded(rows, costs, lambda shard: _generate(eng, shard, parity), torch.device("cpu"),
+        comm = torch.device("cuda:0") if backend == "nccl" else torch.device("cpu")
+        out, mine = run_sharded(rows, costs, lambda shard: _generate(eng, shard, parity), comm,
                                 max_per_rank=4, max_len=64)
         q.put((rank, out, mine))
     finally:
@@ -96,3 +98,23 @@ def test_sharded_engine_equals_unsharded(parity):
         mines += mine
     assert sorted(mines) == list(range(len(rows)))
     assert all(len(r[2]) > 0 for r in res)   # both ranks generated a shard
+
+
+@pytest.mark.timeout(300)
+def test_run_sharded_rccl_world1():
+    """bench.py's RCCL path (backend "nccl" = RCCL, collectives on cuda tensors) at world
+    size 1: the broadcast / all-gather plumbing over the real communicator returns the
+    unsharded ids."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), False, q, "nccl"))
+    p.start()
+    rank, out, mine = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    cfg, eng = _engine()
+    rows = _requests(cfg, n=4)
+    assert out == _generate(eng, rows, False)
+    assert sorted(mine) == list(range(len(rows)))

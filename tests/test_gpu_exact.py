@@ -103,6 +103,37 @@ def test_exact_linear_bitwise_vs_cpu_order(M, N, K, kb, epi, fn):
         int((got.view(torch.int16) != ref.view(torch.int16)).sum())
 
 
+@pytest.mark.parametrize("M,N,K,kb", [
+    (1, 2304, 9216, 4608), (8, 2304, 9216, 4608), (13, 2304, 9216, 4608), (32, 2304, 9216, 3072),
+    (5, 1028, 2304, 1152), (3, 300, 256, 96),
+])
+def test_xmm_decode_parts_bitwise(M, N, K, kb):
+    """The decode part mode (one workgroup per (group, K part), the engine's down projection
+    at M = 1): each part's fp32 fold, added in order from 0 as the consumer norm does, ==
+    the reference order's unrounded sum (oracle.cpu_order.linear_f32 with the same split)."""
+    _need_gpu()
+    from oracle import cpu_order
+    from t5gemma_tts_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(M * 71 + N + kb)
+    X = _hdr((M, K), g)
+    W = _hdr((N, K), g)
+    Wp = _pack(L, W.cuda())
+    Xd = X.cuda()
+    parts = -(-K // kb)
+    Y = torch.full((parts, M, N), float("nan"), dtype=torch.float32, device="cuda")
+    rc = L.t5g_xmm_linear(C.c_void_p(Xd.data_ptr()), K, M, C.c_void_p(Wp.data_ptr()), N, K, kb // 32, None, None,
+                          C.c_void_p(Y.data_ptr()), N, 0x2000 | 4, _st())
+    assert rc == 0
+    torch.cuda.synchronize()
+    p = Y.cpu().numpy()
+    tot = np.zeros((M, N), np.float32)
+    for i in range(parts):
+        tot = (tot + p[i]).astype(np.float32)
+    y32 = cpu_order.linear_f32(X.float().numpy(), W.float().numpy(), kb)
+    assert np.array_equal(tot.view(np.int32), y32.view(np.int32)), int((tot.view(np.int32) != y32.view(np.int32)).sum())
+
+
 # ------------------------------------------------------------------------- SDPA
 @pytest.mark.parametrize("Tq,Tk,causal,window", [
     (1, 1, 1, 0), (1, 60, 0, 0), (1, 152, 1, 0), (1, 903, 1, 0), (1, 600, 1, 0),   # decode (gemv)

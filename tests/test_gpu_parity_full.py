@@ -235,3 +235,59 @@ def test_c3_batch8_exact_vs_reference():
     print(json.dumps(report))
     for r in report.values():
         assert r["tokens_equal"] and r["logit_rows_equal"] == r["steps"], report
+
+
+# (golden, batch, golden row's slot): the reference's full-depth runs of BASELINE rows
+# (tests/golden/make_golden.py gen_config_goldens), each alone and inside a batch of the
+# workload's own size (the other rows: bench.make_batch rows of the same shape)
+CONFIG_GOLDENS = [("golden_c2", 1, 0), ("golden_c1", 1, 0), ("golden_c4", 8, 3), ("golden_c2", 32, 17),
+                  ("golden_longprompt", 1, 0), ("golden_longprompt", 4, 2)]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name,batch,slot", CONFIG_GOLDENS)
+def test_config_golden_exact(name, batch, slot):
+    """Parity mode == the reference's own generate on BASELINE rows run to their full
+    budget: every token and every step's logits row (sha of the bf16 bits), bitwise."""
+    _need_gpu()
+    import hashlib
+    import sys
+    sys.path.insert(0, REPO)
+    from bench import make_batch
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import SamplingParams, T5GemmaTTSEngine, Utterance
+    from t5gemma_tts_amd.weights import state_dict_digest, synthetic_weights
+    path = os.path.join(GOLDEN, name + ".json")
+    if not os.path.exists(path):
+        pytest.fail(f"{name} not generated (tests/golden/make_golden.py --only {name[7:]})")
+    with open(path) as f:
+        meta = json.load(f)
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    assert state_dict_digest(sd) == meta["weight_sha256"]
+    c = meta["cases"][0]
+    others = make_batch(cfg, batch, seed=3131, T_x=len(c["x"]), T_p=max(len(c["y"]) - 1, 0))
+    utts, seeds = [], []
+    for b in range(batch):
+        if b == slot:
+            utts.append(Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"]))
+            seeds.append(c["seed"])
+        else:
+            x, y, tgt = others[b]
+            utts.append(Utterance(x=x, y=y, tgt_y_len=tgt))
+            seeds.append(5000 + b)
+    p = SamplingParams(top_k=c["top_k"], top_p=c["top_p"], min_p=c["min_p"], temperature=c["temperature"],
+                       stop_repetition=c["stop_repetition"])
+    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=batch, max_text=64, max_audio=1024,
+                           max_gen=max(760, len(c["gen"]) + 8))
+    out = eng.generate(utts, p, seeds=seeds, parity=True, record_logits=True)
+    n = len(c["gen"])
+    shas = [hashlib.sha256(lg[slot].cpu().view(torch.int16).numpy().tobytes()).hexdigest()[:16]
+            for lg in out["logits"][:n]]
+    eq = [a == e for a, e in zip(shas, c["logit_sha"])]
+    first_bad = eq.index(False) if not all(eq) else None
+    rep = {"name": name, "batch": batch, "steps": n, "tokens_equal": out["gen"][slot].tolist() == c["gen"],
+           "logit_rows_equal": sum(eq), "first_differing_step": first_bad}
+    _write(f"parity_{name}_b{batch}.json", rep)
+    print(json.dumps(rep))
+    assert rep["tokens_equal"] and rep["logit_rows_equal"] == n, rep
