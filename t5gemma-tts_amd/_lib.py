@@ -116,6 +116,7 @@ SIGNATURES = {
     "t5g_host_sample": (C.c_int, [_P, _I, C.POINTER(SamplerRow), _P, _P, C.POINTER(SamplerState), _P, _I, _I,
                                   _F, _I, _F, _I, _I, C.POINTER(SamplerState), C.POINTER(_I)]),
     "t5g_logits_ptr": (_P, [_P, C.POINTER(_I)]),
+    "t5g_engine_cache_ptr": (_P, [_P, _I, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "t5g_copy_logits": (C.c_int, [_P, _P, _I, _P]),
     "t5g_sample_only": (C.c_int, [_P, _I, _P, _I, _P]),
     "t5g_gemm": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _I, _I, _P]),

@@ -1543,6 +1543,15 @@ extern "C" void* t5g_logits_ptr(t5g_engine* e, int32_t* ld) {
     return e->logits;
 }
 
+extern "C" void* t5g_engine_cache_ptr(t5g_engine* e, int32_t layer, int32_t which, int64_t* head_stride,
+                                      int64_t* row_stride) {
+    if (!e || layer < 0 || layer >= e->c.n_dec_layers || which < 0 || which > 3) return nullptr;
+    const int cap = which < 2 ? e->c.max_audio : e->c.max_text;
+    if (head_stride) *head_stride = (int64_t)cap * e->c.head_dim;
+    if (row_stride) *row_stride = (int64_t)cap * e->c.head_dim * e->c.n_kv_heads;
+    return which == 0 ? e->sk[layer] : which == 1 ? e->sv[layer] : which == 2 ? e->ck[layer] : e->cv[layer];
+}
+
 extern "C" int t5g_copy_logits(t5g_engine* e, void* dst, int32_t B, void* stream) {
     if (!e || !dst || B <= 0 || B > e->c.max_batch) return T5G_EINVAL;
     HIPCHK(hipMemcpyAsync(dst, e->logits, (size_t)B * e->logits_ld * sizeof(bf16_t), hipMemcpyDeviceToDevice,

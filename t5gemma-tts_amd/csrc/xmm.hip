@@ -258,27 +258,63 @@ struct XDecShape {
     static constexpr int LDS = SC * EL * 4;
 };
 
+// Epilogue of folder thread (row m, col fcol of group g): y is the folded value
+template <int EPI, bool PART>
+__device__ __forceinline__ void xdec_store(const XmmArgs& a, int g, int part, long m, int fcol, float y) {
+    const int n = g * 16 + fcol;
+    if constexpr (PART) {
+        if (m < a.M && n < a.N) a.part_out[((long)part * a.M + m) * a.N + n] = y;
+        return;
+    }
+    if constexpr (EPI == EPI_GEGLU) {
+        const float up = xlane<8>(y);   // col + 8 of the same row: the up row of this feature
+        if (fcol >= 8 || m >= a.M) return;
+        const int ft = g * 8 + fcol;
+        if (ft >= a.N / 2) return;
+        const bf16_t v = f2bf(rbf(__fmul_rn(rbf(t5g_exact::gelu_tanh(rbf(y))), rbf(up))));
+        if (a.Y) ((bf16_t*)a.Y)[m * a.ldy + ft] = v;
+        if (a.Y16) a.Y16[x16_off(m, ft, a.N / 64)] = v;
+        return;
+    }
+    if (m >= a.M || n >= a.N) return;
+    if constexpr (EPI == EPI_F32) {
+        ((float*)a.Y)[m * a.ldy + n] = y;
+        return;
+    }
+    float v;
+    if constexpr (EPI == EPI_BF16) {
+        v = rbf(y);
+    } else if constexpr (EPI == EPI_BIAS_BF16) {
+        v = rbf(__fadd_rn(y, bf2f(a.bias[n])));
+    } else {   // EPI_BIAS_GELU: nn.GELU() (erf) on the bf16 Linear output
+        const bf16_t h = f2bf(__fadd_rn(y, bf2f(a.bias[n])));
+        v = bf2f(a.gelu_lut ? a.gelu_lut[h] : f2bf(t5g_exact::gelu_erf(bf2f(h))));
+    }
+    if (a.Y) ((bf16_t*)a.Y)[m * a.ldy + n] = f2bf(v);
+    if (a.Y16) a.Y16[x16_off(m, n, a.N / 32)] = f2bf(v);
+}
+
 template <int RT, bool R8, int EPI, bool PART, int VAR = 0>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void xmm_dec_kernel(XmmArgs a) {
+__global__ __launch_bounds__(512) void xmm_dec_kernel(XmmArgs a) {
     using S = XDecShape<RT, R8>;
     constexpr int NW = S::NW, CPW = S::CPW, SC = S::SC, EL = S::EL;
     extern __shared__ float cs[];   // [SC][EL]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j = lane & 15, q = lane >> 4;
     const int g = blockIdx.x, KB = a.KB;
-    const int kb_lo = PART ? (int)blockIdx.y * a.part_kbc : 0;
+    const int part = PART ? (int)blockIdx.y : 0;
+    const int kb_lo = PART ? part * a.part_kbc : 0;
     const int kb_hi = PART ? min(kb_lo + a.part_kbc, KB) : KB;
     const u32x4* wp = (const u32x4*)(a.W + (long)g * KB * 512) + lane;
     // R8: lanes j >= 8 (rows that do not exist) read lane j - 8's operand: half the bytes
     const u32x4* xp = (const u32x4*)a.X16 + (R8 ? (lane & ~8) : lane);
     const int frow = tid >> 4, fcol = tid & 15;
     const bool folder = tid < EL;
-    // decode rows (no per-row lengths) share the K-part length: a scalar, so the fold's part
-    // boundary test is a scalar branch; otherwise each element's own (xfold)
+    // decode rows (no per-row lengths) share the K-part length; when it covers the
+    // workgroup's chunks every element folds them as one plain chain
     const bool uni = PART || a.kb_fixed > 0 || !a.row_len;
     const int kbc_t = PART ? (1 << 30) : xmm_kbc(a, uni ? 0 : min(frow, a.M - 1), g * 16);
-    const int kbc_u = __builtin_amdgcn_readfirstlane(kbc_t);
+    const bool single = uni && __builtin_amdgcn_readfirstlane(kbc_t) >= kb_hi - kb_lo;
     XFold f{0.f, 0.f, kb_lo};
-    int nb_u = kb_lo;   // uniform fold: the next part's first chunk
     u32x4 wr[CPW], xr[CPW][RT];
     auto load = [&](int s0) {
 #pragma unroll
@@ -313,23 +349,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void x
         __syncthreads();
         if (VAR == 1 && folder) {   // timing variant: no fold
             f.part = cs[tid];
-        } else if (folder && uni) {
-            // 16 chunk sums requested per batch (one LDS round trip), then folded in order
+        } else if (folder && single) {
+            // one K part: part = ((0 + c0) + c1) + ... -- a plain chain (xfold's first step
+            // is fadd(0, c0) too), 16 chunk sums read per LDS round trip
             for (int c0 = 0; c0 < n; c0 += 16) {
                 float v[16];
 #pragma unroll
                 for (int u = 0; u < 16; ++u) v[u] = cs[min(c0 + u, SC - 1) * EL + tid];
+                if (c0 + 16 <= n) {
 #pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const int kb = s0 + c0 + u;
-                    if (c0 + u >= n) break;
-                    if (kb == nb_u) {   // a new K part (scalar test)
-                        if (kb > 0) f.tot = __fadd_rn(f.tot, f.part);
-                        f.part = __fadd_rn(0.f, v[u]);
-                        nb_u += kbc_u;
-                    } else {
-                        f.part = __fadd_rn(f.part, v[u]);
-                    }
+                    for (int u = 0; u < 16; ++u) f.part = __fadd_rn(f.part, v[u]);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 16; ++u)
+                        if (c0 + u < n) f.part = __fadd_rn(f.part, v[u]);
                 }
             }
         } else if (folder) {
@@ -344,40 +377,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void x
         }
         __syncthreads();
     }
-    if (!folder) return;
-    const float y = PART ? f.part : xfold_end(f, KB, uni ? kbc_u : kbc_t);
-    const long m = frow;
-    const int n = g * 16 + fcol;
-    if constexpr (PART) {
-        if (m < a.M && n < a.N) a.part_out[((long)blockIdx.y * a.M + m) * a.N + n] = y;
-        return;
-    }
-    if constexpr (EPI == EPI_GEGLU) {
-        const float up = xlane<8>(y);   // col + 8 of the same row: the up row of this feature
-        if (fcol >= 8 || m >= a.M) return;
-        const int ft = g * 8 + fcol;
-        if (ft >= a.N / 2) return;
-        const bf16_t v = f2bf(rbf(__fmul_rn(rbf(t5g_exact::gelu_tanh(rbf(y))), rbf(up))));
-        if (a.Y) ((bf16_t*)a.Y)[m * a.ldy + ft] = v;
-        if (a.Y16) a.Y16[x16_off(m, ft, a.N / 64)] = v;
-        return;
-    }
-    if (m >= a.M || n >= a.N) return;
-    if constexpr (EPI == EPI_F32) {
-        ((float*)a.Y)[m * a.ldy + n] = y;
-        return;
-    }
-    float v;
-    if constexpr (EPI == EPI_BF16) {
-        v = rbf(y);
-    } else if constexpr (EPI == EPI_BIAS_BF16) {
-        v = rbf(__fadd_rn(y, bf2f(a.bias[n])));
-    } else {   // EPI_BIAS_GELU: nn.GELU() (erf) on the bf16 Linear output
-        const bf16_t h = f2bf(__fadd_rn(y, bf2f(a.bias[n])));
-        v = bf2f(a.gelu_lut ? a.gelu_lut[h] : f2bf(t5g_exact::gelu_erf(bf2f(h))));
-    }
-    if (a.Y) ((bf16_t*)a.Y)[m * a.ldy + n] = f2bf(v);
-    if (a.Y16) a.Y16[x16_off(m, n, a.N / 32)] = f2bf(v);
+    if (folder) xdec_store<EPI, PART>(a, g, part, frow, fcol, (PART || single) ? f.part : xfold_end(f, KB, kbc_t));
 }
 
 template <int RT>
@@ -418,7 +418,7 @@ static int launch_xmm_dec(const XmmArgs& a, int epi, hipStream_t st) {
         launch_dec1<RT, R8, EPI_F32, true>(a, st);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
-    if (a.timing_var) {
+    if (a.timing_var == 1 || a.timing_var == 2) {
         if (epi != EPI_BF16) return -1;
         if (a.timing_var == 1) launch_dec1<RT, R8, EPI_BF16, false, 1>(a, st);
         else launch_dec1<RT, R8, EPI_BF16, false, 2>(a, st);

@@ -59,6 +59,8 @@ def _hdr(shape, g):
     (8, 2304, 9216, 2304, 3), (7, 1024, 9216, 3072, 1), (1, 1028, 2304, 0, 1), (6, 2304, 9216, 4608, 4),
     # f32-MFMA shapes: 17-32 decode rows (two row tiles), prefill tiles of 4 x 16 rows
     (32, 2304, 9216, 4608, 0), (24, 18432, 2304, 0, 3), (100, 4096, 2304, 768, 0), (160, 2304, 2304, 0, 4),
+    # a 602-token prefill (601-code voice prompt): the K splits of the measured table at M = 602
+    (602, 2048, 2304, 1152, 0), (602, 2304, 2048, 1024, 0), (602, 4608, 2304, 768, 3), (602, 2304, 9216, 1536, 0),
 ])
 @pytest.mark.parametrize("fn", ["t5g_exact_linear", "t5g_xmm_linear"])
 def test_exact_linear_bitwise_vs_cpu_order(M, N, K, kb, epi, fn):
@@ -139,6 +141,7 @@ def test_xmm_decode_parts_bitwise(M, N, K, kb):
     (1, 1, 1, 0), (1, 60, 0, 0), (1, 152, 1, 0), (1, 903, 1, 0), (1, 600, 1, 0),   # decode (gemv)
     (60, 60, 0, 0), (33, 33, 0, 0), (152, 152, 1, 0), (152, 60, 0, 0), (200, 200, 1, 0),   # prefill / encoder
     (17, 17, 1, 8), (1, 40, 1, 8), (20, 20, 0, 8),                                       # sliding window
+    (602, 602, 1, 0), (602, 60, 0, 0), (1, 603, 1, 0),                                    # 601-code prompt
 ])
 def test_exact_attention_bitwise_vs_cpu_order(Tq, Tk, causal, window):
     """t5g_exact_attention == oracle.cpu_order.sdpa (aten CPU flash attention + the GEMM it
