@@ -194,6 +194,10 @@ int t5g_host_sample(const uint16_t* logits_bf16, int32_t V, const t5g_sampler_ro
 /* Device pointer of the logits buffer bf16 [max_batch][logits_ld] (debug / parity). */
 void* t5g_logits_ptr(t5g_engine* e, int32_t* logits_ld);
 /* Stream-ordered device copy of the first B logits rows into dst_dev [B][logits_ld]. */
+/* Parity mode: the RoPE cos / sin exception table (data/rope_trig_exc.bin: n sorted
+ * (fp32 angle bits, cos_bf16 | sin_bf16 << 16) pairs, host memory; copied). Angles in it
+ * take the reference host's MKL values, all others the correctly rounded ones. */
+int t5g_engine_set_rope_exc(t5g_engine* e, const uint32_t* tab, int32_t n);
 /* Diagnostics: device pointer of decoder layer `layer`'s cache (which: 0 self K, 1 self V,
  * 2 cross K, 3 cross V), bf16 [max_batch][n_kv_heads][cap][head_dim]; strides in elements. */
 void* t5g_engine_cache_ptr(t5g_engine* e, int32_t layer, int32_t which, int64_t* head_stride,

@@ -117,6 +117,7 @@ SIGNATURES = {
                                   _F, _I, _F, _I, _I, C.POINTER(SamplerState), C.POINTER(_I)]),
     "t5g_logits_ptr": (_P, [_P, C.POINTER(_I)]),
     "t5g_engine_cache_ptr": (_P, [_P, _I, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "t5g_engine_set_rope_exc": (C.c_int, [_P, _P, _I]),
     "t5g_copy_logits": (C.c_int, [_P, _P, _I, _P]),
     "t5g_sample_only": (C.c_int, [_P, _I, _P, _I, _P]),
     "t5g_gemm": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _I, _I, _P]),
@@ -147,6 +148,17 @@ SIGNATURES = {
 
 # parity mode: the reference host's bf16 nn.GELU() (erf) table (tools/cpu_order/make_gelu_table.py)
 GELU_ERF_TABLE = os.path.join(_PKG, "data", "gelu_erf_bf16.bin")
+# RoPE cos / sin angles where the reference host's MKL differs from the correctly rounded
+# value after the bf16 cast (tools/cpu_order/make_rope_table.py); covers every position
+# of an utterance whose estimated total length is <= ROPE_EXC_MAX_LEN
+ROPE_EXC_TABLE = os.path.join(_PKG, "data", "rope_trig_exc.bin")
+ROPE_EXC_MAX_LEN = 4096
+
+
+def rope_exc_table():
+    """The exception table as a uint32 numpy array [n, 2] (angle bits, cos | sin << 16)."""
+    import numpy as np
+    return np.fromfile(ROPE_EXC_TABLE, dtype="<u4").reshape(-1, 2)
 _gelu_tab = None
 
 

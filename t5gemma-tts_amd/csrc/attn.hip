@@ -64,8 +64,8 @@ __global__ __launch_bounds__(256) void rope_store_kernel(RopeArgs a) {
             sn = a.rope_tab[(long)row * D + H2 + i];
         } else {
             const float ang = a.inv_freq[i] * a.pos[m];
-            c = rbf(a.exact_trig ? t5g_exact::rope_cos(ang) : cosf(ang));
-            sn = rbf(a.exact_trig ? t5g_exact::rope_sin(ang) : sinf(ang));
+            c = a.exact_trig ? t5g_exact::rope_trig(ang, 0, a.trig_exc, a.n_trig_exc) : rbf(cosf(ang));
+            sn = a.exact_trig ? t5g_exact::rope_trig(ang, 1, a.trig_exc, a.n_trig_exc) : rbf(sinf(ang));
         }
         o1 = rbf(rbf(x1 * c) + rbf(-x2 * sn));
         o2 = rbf(rbf(x2 * c) + rbf(x1 * sn));

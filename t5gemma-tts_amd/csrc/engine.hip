@@ -117,6 +117,8 @@ struct t5g_engine {
     bf16_t *xn16 = nullptr, *att16 = nullptr, *act16 = nullptr, *mem16 = nullptr;   // packed tokens
     bf16_t *dxn16 = nullptr, *datt16 = nullptr, *dact16 = nullptr, *dhh16 = nullptr;   // decode rows
     float* dpart = nullptr;   // decode down projection: fp32 K-part values [4][B16][hidden]
+    uint32_t* trig_exc = nullptr;   // parity mode: RoPE cos / sin exceptions (t5g_engine_set_rope_exc)
+    int n_trig_exc = 0;
     bool xmm_ready = false;
 };
 
@@ -159,6 +161,7 @@ extern "C" int t5g_engine_destroy(t5g_engine* e) {
     drop_graphs(e);
     if (e->cap_stream) hipStreamDestroy(e->cap_stream);
     for (void* p : e->allocs) hipFree(p);
+    if (e->trig_exc) hipFree(e->trig_exc);
     delete e;
     return T5G_OK;
 }
@@ -466,10 +469,12 @@ static NormArgs xnorm_args(int M, int d, float eps) {
     return n;
 }
 
-static RopeArgs xrope_args(int M, int D, const float* pos, const float* inv_freq, const int* tok_row, const int* tok_t,
-                           const int* kv_len) {
+static RopeArgs xrope_args(const t5g_engine* e, int M, int D, const float* pos, const float* inv_freq,
+                           const int* tok_row, const int* tok_t, const int* kv_len) {
     RopeArgs r;
     memset(&r, 0, sizeof(r));
+    r.trig_exc = e->trig_exc;
+    r.n_trig_exc = e->n_trig_exc;
     r.M = M;
     r.D = D;
     r.pos = pos;
@@ -507,7 +512,7 @@ static int encode_exact(t5g_engine* e, int ntok, const int32_t* ids, const int32
         RC(resid_norm(n, st));
         RC(xlin16(e, e->xn16, ntok, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
                   e->q_dim, e->kv_dim, e->q_dim, st));
-        RopeArgs r = xrope_args(ntok, D, pos, e->w.inv_freq, tok_row, tok_t, nullptr);
+        RopeArgs r = xrope_args(e, ntok, D, pos, e->w.inv_freq, tok_row, tok_t, nullptr);
         r.X = e->qkv;
         r.ldx = e->qkv_dim;
         r.nq = c.n_heads;
@@ -549,7 +554,7 @@ static int encode_exact(t5g_engine* e, int ntok, const int32_t* ids, const int32
     for (int l = 0; l < c.n_dec_layers; ++l) {
         RC(xlin16(e, e->mem16, ntok, e->dec_x[l].cross_kv, 2 * e->kv_dim, d, nullptr, e->qkv, 2 * e->kv_dim, nullptr,
                   EPI_BF16, tok_row, rl, e->kv_dim, e->kv_dim, e->kv_dim, st));
-        RopeArgs r = xrope_args(ntok, D, pos, e->w.inv_freq, tok_row, tok_t, nullptr);
+        RopeArgs r = xrope_args(e, ntok, D, pos, e->w.inv_freq, tok_row, tok_t, nullptr);
         r.X = e->qkv;
         r.ldx = 2 * e->kv_dim;
         r.nk = r.nv = c.n_kv_heads;
@@ -608,13 +613,15 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
                 n.rope_inv_freq = e->w.inv_freq;
                 n.rope_tab = e->rope_tab;
                 n.rope_D = D;
+                n.trig_exc = e->trig_exc;
+                n.n_trig_exc = e->n_trig_exc;
             }
             RC(resid_norm(n, st));
         }
         // self attention
         RC(xlin16(e, xn16, M, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
                   e->q_dim, e->kv_dim, e->q_dim, st));
-        RopeArgs r = xrope_args(M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
+        RopeArgs r = xrope_args(e, M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
         r.rope_tab = decode ? e->rope_tab : nullptr;
         r.X = e->qkv;
         r.ldx = e->qkv_dim;
@@ -635,7 +642,7 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         // PM cross attention
         RC(xlin16(e, xn16, M, X.cross_q, e->q_dim, d, nullptr, q, e->q_dim, nullptr, EPI_BF16, tok_row, rl, e->q_dim, 0,
                   0, st));
-        r = xrope_args(M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
+        r = xrope_args(e, M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
         r.rope_tab = decode ? e->rope_tab : nullptr;
         r.X = q;
         r.ldx = e->q_dim;
@@ -1541,6 +1548,20 @@ extern "C" void* t5g_logits_ptr(t5g_engine* e, int32_t* ld) {
     if (!e) return nullptr;
     if (ld) *ld = e->logits_ld;
     return e->logits;
+}
+
+extern "C" int t5g_engine_set_rope_exc(t5g_engine* e, const uint32_t* tab, int32_t n) {
+    if (!e || n < 0 || (n > 0 && !tab)) return T5G_EINVAL;
+    if (e->trig_exc) {
+        (void)hipFree(e->trig_exc);
+        e->trig_exc = nullptr;
+    }
+    e->n_trig_exc = 0;
+    if (n == 0) return T5G_OK;
+    HIPCHK(hipMalloc(&e->trig_exc, (size_t)n * 8));
+    HIPCHK(hipMemcpy(e->trig_exc, tab, (size_t)n * 8, hipMemcpyHostToDevice));
+    e->n_trig_exc = n;
+    return T5G_OK;
 }
 
 extern "C" void* t5g_engine_cache_ptr(t5g_engine* e, int32_t layer, int32_t which, int64_t* head_stride,

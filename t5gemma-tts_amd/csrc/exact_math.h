@@ -14,11 +14,16 @@
 //   (aten gelu_out_cpu -> ideep). After the bf16 cast its results equal
 //   (x * (1 + erf(x*M_SQRT1_2))) * 0.5 with the exact erf on every bf16 input (overflow at
 //   |x| >= 2^127 included), except that outputs below FLT_MIN come out as zero.
-// * cos / sin of the fp32 RoPE angle (Sleef u10), cast to bf16: equal to the correctly
-//   rounded value after the cast on every angle of the tested workloads.
+// * cos / sin of the fp32 RoPE angle: torch is built with MKL, so the reference's float
+//   cos / sin are MKL VML's vmsCos / vmsSin (VML_HA, ~0.6 ulp, proprietary). After the
+//   bf16 cast they equal the correctly rounded value except on ~2.5e-7 of the angles; the
+//   exceptions over every angle this model's position formulas can produce are listed in
+//   data/rope_trig_exc.bin (tools/cpu_order/make_rope_table.py, made on the reference
+//   host) and looked up here (rope_trig).
 #pragma once
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 #ifndef T5G_HD
 #define T5G_HD __host__ __device__
@@ -50,5 +55,32 @@ T5G_HD inline float gelu_erf(float x) {
 
 T5G_HD inline float rope_cos(float ang) { return (float)cos((double)ang); }
 T5G_HD inline float rope_sin(float ang) { return (float)sin((double)ang); }
+
+// bf16-rounded cos (which = 0) / sin (1) of a RoPE angle as the reference host rounds it:
+// the correctly rounded value unless the angle is in the exception table exc (n sorted
+// (angle bits, cos_bf16 | sin_bf16 << 16) pairs; null: none). Returned as the bf16 value
+// in a float.
+T5G_HD inline float rope_trig(float ang, int which, const uint32_t* exc, int n) {
+    const float cr = which ? rope_sin(ang) : rope_cos(ang);
+    uint32_t key;
+    memcpy(&key, &ang, 4);
+    int lo = 0, hi = exc ? n : 0;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (exc[2 * mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    uint32_t bits;
+    if (exc && lo < n && exc[2 * lo] == key) {
+        bits = (which ? exc[2 * lo + 1] >> 16 : exc[2 * lo + 1] & 0xFFFFu) << 16;
+    } else {   // round to nearest even bf16
+        uint32_t u;
+        memcpy(&u, &cr, 4);
+        bits = ((u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u);
+    }
+    float r;
+    memcpy(&r, &bits, 4);
+    return r;
+}
 
 }  // namespace t5g_exact

@@ -147,8 +147,10 @@ __global__ __launch_bounds__(1024) void resid_norm_kernel(NormArgs a, int has_po
         const int H2 = a.rope_D / 2;
         for (int i = threadIdx.x; i < H2; i += blockDim.x) {
             const float ang = a.rope_inv_freq[i] * a.rope_pos[mi];
-            a.rope_tab[(long)mi * a.rope_D + i] = rbf(EXACT ? t5g_exact::rope_cos(ang) : cosf(ang));
-            a.rope_tab[(long)mi * a.rope_D + H2 + i] = rbf(EXACT ? t5g_exact::rope_sin(ang) : sinf(ang));
+            a.rope_tab[(long)mi * a.rope_D + i] =
+                EXACT ? t5g_exact::rope_trig(ang, 0, a.trig_exc, a.n_trig_exc) : rbf(cosf(ang));
+            a.rope_tab[(long)mi * a.rope_D + H2 + i] =
+                EXACT ? t5g_exact::rope_trig(ang, 1, a.trig_exc, a.n_trig_exc) : rbf(sinf(ang));
         }
     }
     const int m = a.out_rows ? a.out_rows[mi] : mi;

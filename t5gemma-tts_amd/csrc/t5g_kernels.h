@@ -141,6 +141,8 @@ struct NormArgs {
     float* rope_tab;         // [M][rope_D]
     int rope_D;
     int exact;               // parity mode: the reference's CPU sum order (delta / ids sources)
+    const uint32_t* trig_exc;   // parity mode: the RoPE cos / sin exception table (exact_math.h rope_trig)
+    int n_trig_exc;
     bf16_t* normed_x16;      // optional: normed_out again in the X16 layout (xmm.hip)
 };
 int resid_norm(const NormArgs& a, hipStream_t st);
@@ -166,6 +168,8 @@ struct RopeArgs {
     long c_bstride, c_hstride;
     const float* rope_tab;   // optional [rows][D]: bf16-rounded cos (D/2) | sin (D/2) per row
     int exact_trig;          // parity mode: cos / sin as the reference host rounds them (exact_math.h)
+    const uint32_t* trig_exc;   // with the exception table of rope_trig
+    int n_trig_exc;
 };
 int rope_store(const RopeArgs& a, hipStream_t st);
 // (the decode step's per-row table tab[r][i] = bf16(cos(inv_freq[i] * pos[r])),

@@ -20,6 +20,7 @@ import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Union
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -261,6 +262,10 @@ class T5GemmaTTSEngine:
             return
         tab = _lib.gelu_erf_table() if enable else None
         _lib.check(self.L.t5g_engine_set_exact(self.h, 1 if enable else 0, tab, _lib.EXACT_THREADS), "set_exact")
+        if enable and getattr(self, "_rope_exc", None) is None:
+            self._rope_exc = np.ascontiguousarray(_lib.rope_exc_table())
+            _lib.check(self.L.t5g_engine_set_rope_exc(self.h, self._rope_exc.ctypes.data, len(self._rope_exc)),
+                       "set_rope_exc")
         self._exact = bool(enable)
 
     def generate(self, utts: Sequence[Utterance], params: Union[SamplingParams, Sequence[SamplingParams]],
@@ -380,6 +385,9 @@ class T5GemmaTTSEngine:
             else:
                 est = int(cur_len + int(cfg.encodec_sr) * cfg.progress_lookahead_secs)
             est = max(est, cur_len)
+            if getattr(self, "_exact", False) and est > _lib.ROPE_EXC_MAX_LEN:
+                raise ValueError(f"parity mode: estimated length {est} exceeds the RoPE cos / sin table's "
+                                 f"coverage ({_lib.ROPE_EXC_MAX_LEN}, tools/cpu_order/make_rope_table.py)")
             last.append(len(aid) + cur_len - 1)
             aid += cated
             arow += [b] * cur_len

@@ -172,3 +172,77 @@ def test_gelu_erf_table_and_exact_form(exact_math_lib):
     if _reference_host():
         x = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(BF16)
         assert np.array_equal(F.gelu(x).view(torch.int16).numpy().astype(np.uint16)[ok], tab[ok])
+
+
+# ------------------------------------------------------------------- RoPE cos / sin
+_ROPE_SHIM = r"""
+#define T5G_HD
+#include "exact_math.h"
+extern "C" void rope_eval(const float* ang, long n, const unsigned* exc, int ne, unsigned short* c,
+                          unsigned short* s) {
+    for (long i = 0; i < n; ++i) {
+        const float a = t5g_exact::rope_trig(ang[i], 0, exc, ne), b = t5g_exact::rope_trig(ang[i], 1, exc, ne);
+        unsigned ua, ub;
+        __builtin_memcpy(&ua, &a, 4);
+        __builtin_memcpy(&ub, &b, 4);
+        c[i] = (unsigned short)(ua >> 16);
+        s[i] = (unsigned short)(ub >> 16);
+    }
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def rope_lib(tmp_path_factory):
+    d = tmp_path_factory.mktemp("rope_trig")
+    src = d / "shim.cpp"
+    src.write_text(_ROPE_SHIM)
+    so = d / "shim.so"
+    inc = os.path.join(REPO, "t5gemma-tts_amd", "csrc")
+    r = subprocess.run(["g++", "-O2", "-ffp-contract=off", "-shared", "-fPIC", "-I", inc, str(src), "-o", str(so)],
+                       capture_output=True, text=True)
+    if r.returncode:
+        pytest.skip(f"g++ unavailable: {r.stderr[-300:]}")
+    return C.CDLL(str(so))
+
+
+def _rope_eval(lib, ang, exc):
+    ang = np.ascontiguousarray(ang, np.float32)
+    c = np.zeros(ang.size, np.uint16)
+    s = np.zeros(ang.size, np.uint16)
+    e = np.ascontiguousarray(exc, "<u4") if exc is not None else None
+    lib.rope_eval(ang.ctypes.data_as(C.c_void_p), C.c_long(ang.size),
+                  e.ctypes.data_as(C.c_void_p) if e is not None else None, 0 if e is None else len(e),
+                  c.ctypes.data_as(C.c_void_p), s.ctypes.data_as(C.c_void_p))
+    return c, s
+
+
+def test_rope_trig_matches_reference_host(rope_lib):
+    """RoPE cos / sin of exact_math.h (correctly rounded + data/rope_trig_exc.bin) == the
+    reference host's torch (MKL VML) cos / sin after the bf16 cast, on the angles of the
+    601-code prompt golden, of random position sets of the enumerated family and of every
+    table entry; without the table they differ exactly on the table's angles."""
+    if not _reference_host():
+        pytest.skip("MKL's cos / sin are compared on the reference host only")
+    from t5gemma_tts_amd import _lib
+    exc = _lib.rope_exc_table()
+    assert exc.ndim == 2 and exc.shape[1] == 2 and np.all(np.diff(exc[:, 0].astype(np.int64)) > 0)
+    inv = (1.0 / (10000.0 ** (torch.arange(0, 256, 2, dtype=torch.float) / 256))).numpy()
+    rng = np.random.default_rng(5)
+    pos = [np.array([0.0, 2000.0], np.float32)]
+    for e in [603, 2, 3, 4096] + rng.integers(2, 4097, size=40).tolist():
+        t = torch.arange(e, dtype=torch.float32)
+        pos.append(((t / (e - 1)) * 2000.0).numpy())
+        pos.append(np.minimum(np.arange(e, dtype=np.float64) / float(e - 1) * 2000.0, 2000.0).astype(np.float32))
+    pos = np.unique(np.concatenate(pos))
+    ang = np.unique(np.concatenate([(np.float32(f) * pos).astype(np.float32) for f in inv] +
+                                   [exc[:, 0].copy().view(np.float32)]))
+    c, s = _rope_eval(rope_lib, ang, exc)
+    at = torch.from_numpy(ang)
+    rc = torch.cos(at).to(BF16).view(torch.int16).numpy().astype(np.uint16)
+    rs = torch.sin(at).to(BF16).view(torch.int16).numpy().astype(np.uint16)
+    assert np.array_equal(c, rc), int((c != rc).sum())
+    assert np.array_equal(s, rs), int((s != rs).sum())
+    c0, s0 = _rope_eval(rope_lib, ang, None)
+    differ = set(ang[(c0 != rc) | (s0 != rs)].view(np.uint32).tolist())
+    assert differ <= set(exc[:, 0].tolist()) and len(differ) > 0
