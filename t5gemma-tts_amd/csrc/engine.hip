@@ -424,14 +424,22 @@ static int xlin16_dec_parts(t5g_engine* e, const bf16_t* X16, int M, const bf16_
     return exact_linear(a, epi, st);
 }
 
+// fr (decode only, exact_attention_decode_supported): RoPE fused into the scores launch --
+// Q un-rotated, rotated with the step's table; with kv_new also the new key / value appended
+struct XattnFuse {
+    const float* rope_tab = nullptr;
+    const bf16_t* kv_new = nullptr;
+    int ld_new = 0, k_col0 = 0, v_col0 = 0;
+    int ldq = 0;   // row stride of Q when it is not q_dim (the q | k | v buffer)
+};
 static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const int* q_pos, const int* q_len,
                  const bf16_t* K, const bf16_t* Vc, int cap, const int* kv_len, int causal, int window, bf16_t* O,
-                 bf16_t* O16, hipStream_t st) {
+                 bf16_t* O16, hipStream_t st, const XattnFuse& fr = XattnFuse()) {
     const t5g_config& c = e->c;
     ExactAttnArgs a;
     memset(&a, 0, sizeof(a));
     a.Q = Q;
-    a.ldq = e->q_dim;
+    a.ldq = fr.ldq ? fr.ldq : e->q_dim;
     a.Mq = Mq;
     a.q_row = q_row;
     a.q_pos = q_pos;
@@ -451,11 +459,17 @@ static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const
     a.O = O;
     a.ldo = e->q_dim;
     a.O16 = O16;
+    a.rope_tab = fr.rope_tab;
+    a.kv_new = fr.kv_new;
+    a.ld_new = fr.ld_new;
+    a.k_col0 = fr.k_col0;
+    a.v_col0 = fr.v_col0;
     // decode rows (one query each): the scores + P.V launches of xattn.hip
     if (!q_pos && !q_len) {
         const int rc = exact_attention_decode(a, e->asbuf, e->ambuf, cap, st);
-        if (rc != -3) return rc;   // -3: a head shape the decode kernels are not built for
+        if (rc != -3 || fr.rope_tab) return rc;   // -3: a head shape the decode kernels are not built for
     }
+    if (fr.rope_tab) return -1;
     return exact_attention(a, st);
 }
 
@@ -621,37 +635,59 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         // self attention
         RC(xlin16(e, xn16, M, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
                   e->q_dim, e->kv_dim, e->q_dim, st));
-        RopeArgs r = xrope_args(e, M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
-        r.rope_tab = decode ? e->rope_tab : nullptr;
-        r.X = e->qkv;
-        r.ldx = e->qkv_dim;
-        r.nq = c.n_heads;
-        r.nk = r.nv = c.n_kv_heads;
-        r.rope_q = r.rope_k = 1;
-        r.Qout = q;
-        r.ldq = e->q_dim;
-        r.Kc = e->sk[l];
-        r.Vc = e->sv[l];
-        r.c_hstride = (long)c.max_audio * D;
-        r.c_bstride = r.c_hstride * c.n_kv_heads;
-        RC(rope_store(r, st));
-        RC(xattn(e, q, M, tok_row, tok_t, qlen, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1,
-                 c.dec_sliding[l] ? c.sliding_window : 0, att, att16, st));
+        // decode: RoPE of q and k and the cache append happen inside the scores launch
+        const bool fuse = decode && exact_attention_decode_supported(c.n_heads / c.n_kv_heads, D);
+        if (fuse) {
+            XattnFuse fr;
+            fr.rope_tab = e->rope_tab;
+            fr.kv_new = e->qkv;
+            fr.ld_new = e->qkv_dim;
+            fr.k_col0 = e->q_dim;
+            fr.v_col0 = e->q_dim + e->kv_dim;
+            fr.ldq = e->qkv_dim;
+            RC(xattn(e, e->qkv, M, tok_row, tok_t, qlen, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1,
+                     c.dec_sliding[l] ? c.sliding_window : 0, att, att16, st, fr));
+        } else {
+            RopeArgs r = xrope_args(e, M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
+            r.rope_tab = decode ? e->rope_tab : nullptr;
+            r.X = e->qkv;
+            r.ldx = e->qkv_dim;
+            r.nq = c.n_heads;
+            r.nk = r.nv = c.n_kv_heads;
+            r.rope_q = r.rope_k = 1;
+            r.Qout = q;
+            r.ldq = e->q_dim;
+            r.Kc = e->sk[l];
+            r.Vc = e->sv[l];
+            r.c_hstride = (long)c.max_audio * D;
+            r.c_bstride = r.c_hstride * c.n_kv_heads;
+            RC(rope_store(r, st));
+            RC(xattn(e, q, M, tok_row, tok_t, qlen, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1,
+                     c.dec_sliding[l] ? c.sliding_window : 0, att, att16, st));
+        }
         RC(xlin16(e, att16, M, X.o, d, e->q_dim, nullptr, tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0, st));
         RC(norm(L.norms[1], L.norms[2]));
         // PM cross attention
         RC(xlin16(e, xn16, M, X.cross_q, e->q_dim, d, nullptr, q, e->q_dim, nullptr, EPI_BF16, tok_row, rl, e->q_dim, 0,
                   0, st));
-        r = xrope_args(e, M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
-        r.rope_tab = decode ? e->rope_tab : nullptr;
-        r.X = q;
-        r.ldx = e->q_dim;
-        r.nq = c.n_heads;
-        r.rope_q = 1;
-        r.Qout = q;
-        r.ldq = e->q_dim;
-        RC(rope_store(r, st));
-        RC(xattn(e, q, M, tok_row, tok_t, qlen, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, att16, st));
+        if (fuse) {   // q RoPE inside the scores launch
+            XattnFuse fr;
+            fr.rope_tab = e->rope_tab;
+            RC(xattn(e, q, M, tok_row, tok_t, qlen, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, att16, st,
+                     fr));
+        } else {
+            RopeArgs r = xrope_args(e, M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
+            r.rope_tab = decode ? e->rope_tab : nullptr;
+            r.X = q;
+            r.ldx = e->q_dim;
+            r.nq = c.n_heads;
+            r.rope_q = 1;
+            r.Qout = q;
+            r.ldq = e->q_dim;
+            RC(rope_store(r, st));
+            RC(xattn(e, q, M, tok_row, tok_t, qlen, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, att16,
+                     st));
+        }
         RC(xlin16(e, att16, M, X.cross_o, d, e->q_dim, nullptr, tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0, st));
         RC(norm(L.norms[3], L.norms[4]));
         // GeGLU MLP: act straight into the down projection's operand order

@@ -290,11 +290,18 @@ struct ExactAttnArgs {
     bf16_t* O;
     int ldo;
     bf16_t* O16;              // optional: the output again in the X16 layout (K = ldo)
+    // decode only (exact_attention_decode): RoPE fused into the scores launch
+    const float* rope_tab;    // non-null: Q holds the UN-rotated queries; rotate them with
+                              // rope_tab[row] (bf16 cos | sin, engine rope table)
+    const bf16_t* kv_new;     // non-null: the step's un-rotated key / value rows of row r at
+    int ld_new, k_col0, v_col0;   // kv_new[r * ld_new + k_col0 / v_col0 + head * D]: rotated,
+                                  // appended at slot kv_len[row] - 1 of K / V (written) and used
 };
 int exact_attention(const ExactAttnArgs& a, hipStream_t st);
 // decode (one query per row, at its last key): scores + P.V launches (xattn.hip) on the
 // scratch sbuf [Mq][Hq][cap] / mbuf [Mq][Hkv][ceil(cap / 64)][G]
 int exact_attention_decode(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, hipStream_t st);
+bool exact_attention_decode_supported(int G, int D);   // head shapes the decode launches are built for
 
 // ---- sampler -------------------------------------------------------------------
 struct SamplerRow {           // per-utterance parameters (device)

@@ -33,10 +33,22 @@ __device__ __forceinline__ void xd_range(const ExactAttnArgs& a, int row, int& l
     lo = (a.window > 0 && a.causal && hi >= a.window) ? hi - a.window : 0;
 }
 
-template <int G, int XD_D>
+// RoPE of one rotation pair as rope_store_kernel computes it (attn.hip): the three bf16
+// tensor ops of apply_rotary_pos_emb
+__device__ __forceinline__ void xd_rope(float x1, float x2, float c, float sn, float& o1, float& o2) {
+    o1 = rbf(rbf(x1 * c) + rbf(-x2 * sn));
+    o2 = rbf(rbf(x2 * c) + rbf(x1 * sn));
+}
+
+// FUSE: the queries arrive un-rotated and are rotated while staged (rope_tab), and, with
+// kv_new, the workgroup holding the row's new key (slot kv_len - 1) rotates it, appends it
+// and its value to the cache and uses the rotated key directly (no separate RoPE launch).
+template <int G, int XD_D, bool FUSE>
 __global__ __launch_bounds__(64) void xattn_scores_kernel(ExactAttnArgs a, float* sbuf, float* mbuf, int cap,
                                                           int nsplit) {
+    constexpr int H2 = XD_D / 2;
     __shared__ float qs[G][XD_D];
+    __shared__ uint32_t knew[FUSE ? XD_D / 2 : 1];   // the rotated new key as bf16 pairs
     const int qi = blockIdx.x, kvh = blockIdx.y, ch = blockIdx.z, lane = threadIdx.x;
     const int row = a.q_row ? a.q_row[qi] : qi;
     int lo, hi;
@@ -50,13 +62,48 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(ExactAttnArgs a, float
 #pragma unroll
     for (int j = 0; j < XD_D / 8; ++j) kv[j] = *(const u32x4*)(kr + 8 * j);
     // the G query rows of this kv head (GQA: heads kvh * G + g), broadcast from LDS
-    for (int i = lane; i < G * XD_D / 2; i += 64) {
-        const int g = i / (XD_D / 2), p = i % (XD_D / 2);
-        const uint32_t w = *(const uint32_t*)(a.Q + (long)qi * a.ldq + (kvh * G + g) * XD_D + 2 * p);
-        qs[g][2 * p] = bf_lo(w);
-        qs[g][2 * p + 1] = bf_hi(w);
+    if constexpr (FUSE) {
+        const float* tab = a.rope_tab + (long)row * XD_D;
+        for (int i = lane; i < G * H2; i += 64) {
+            const int g = i / H2, d = i % H2;
+            const bf16_t* qh = a.Q + (long)qi * a.ldq + (kvh * G + g) * XD_D;
+            float o1, o2;
+            xd_rope(bf2f(qh[d]), bf2f(qh[d + H2]), tab[d], tab[H2 + d], o1, o2);
+            qs[g][d] = o1;
+            qs[g][d + H2] = o2;
+        }
+        // the workgroup holding the new key: rotate it (two pairs per lane), append K and V
+        const bool has_new = a.kv_new && hi - 1 >= c0 && hi - 1 < c0 + XD_CH;
+        if (has_new) {
+            const long slot = hi - 1;
+            const bf16_t* kn = a.kv_new + (long)qi * a.ld_new + a.k_col0 + kvh * XD_D;
+            const bf16_t* vn = a.kv_new + (long)qi * a.ld_new + a.v_col0 + kvh * XD_D;
+            bf16_t* kc = (bf16_t*)a.K + row * a.kv_bstride + kvh * a.kv_hstride + slot * XD_D;
+            bf16_t* vc = (bf16_t*)a.V + row * a.kv_bstride + kvh * a.kv_hstride + slot * XD_D;
+            for (int d = lane; d < H2; d += 64) {
+                float o1, o2;
+                xd_rope(bf2f(kn[d]), bf2f(kn[d + H2]), tab[d], tab[H2 + d], o1, o2);
+                kc[d] = f2bf(o1);
+                kc[d + H2] = f2bf(o2);
+                ((bf16_t*)knew)[d] = f2bf(o1);
+                ((bf16_t*)knew)[d + H2] = f2bf(o2);
+            }
+            for (int d = lane; d < XD_D; d += 64) vc[d] = vn[d];
+        }
+        __syncthreads();
+        if (has_new && key == hi - 1) {
+#pragma unroll
+            for (int j = 0; j < XD_D / 8; ++j) kv[j] = *(const u32x4*)&knew[4 * j];
+        }
+    } else {
+        for (int i = lane; i < G * XD_D / 2; i += 64) {
+            const int g = i / (XD_D / 2), p = i % (XD_D / 2);
+            const uint32_t w = *(const uint32_t*)(a.Q + (long)qi * a.ldq + (kvh * G + g) * XD_D + 2 * p);
+            qs[g][2 * p] = bf_lo(w);
+            qs[g][2 * p + 1] = bf_hi(w);
+        }
+        __syncthreads();
     }
-    __syncthreads();
     float sc[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -221,14 +268,20 @@ __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const fl
 template <int G, int D>
 static void launch_xd(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, int nsplit, hipStream_t st) {
     const dim3 gs((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)nsplit), gp((unsigned)a.Mq, (unsigned)a.Hkv, D / XD_DZ);
-    hipLaunchKernelGGL((xattn_scores_kernel<G, D>), gs, dim3(64), 0, st, a, sbuf, mbuf, cap, nsplit);
+    if (a.rope_tab) hipLaunchKernelGGL((xattn_scores_kernel<G, D, true>), gs, dim3(64), 0, st, a, sbuf, mbuf, cap, nsplit);
+    else hipLaunchKernelGGL((xattn_scores_kernel<G, D, false>), gs, dim3(64), 0, st, a, sbuf, mbuf, cap, nsplit);
     hipLaunchKernelGGL((xattn_pv_kernel<G, D>), gp, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
+}
+
+bool exact_attention_decode_supported(int G, int D) {
+    return (G == 2 && (D == 256 || D == 128 || D == 64)) || (G == 1 && (D == 256 || D == 64));
 }
 
 int exact_attention_decode(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, hipStream_t st) {
     if (a.Mq <= 0) return 0;
     if (!a.Q || !a.K || !a.V || !a.kv_len || !a.O || !sbuf || !mbuf || a.Hq % a.Hkv) return -1;
     if (a.q_pos || a.q_len) return -1;   // one query per row, at its last key
+    if (a.kv_new && !a.rope_tab) return -1;
     const int G = a.Hq / a.Hkv;
     const int nsplit = (cap + XD_CH - 1) / XD_CH;
     if ((cap + SDPA_KV_BLOCK - 1) / SDPA_KV_BLOCK > SDPA_MAX_BLOCKS) return -1;
