@@ -358,7 +358,7 @@ def main():
             if B <= 16:   # the step runs the whole post-self-attention block in one launch
                 us_k, kname = us.value, _lib.FUSED_BLOCK_KERNEL
                 alg_bytes = _lib.fused_block_bytes(B, wl_tx, d, f)
-                pmc = os.path.join(REPO, "profiles", "r03_pmc_fused_block.json")
+                pmc = os.path.join(REPO, "profiles", "r04_pmc_fused_block.json")   # this round's kernel
             else:
                 us_k, alg_bytes, kname = us.value, _lib.fused_mlp_bytes(B, d, f), _lib.FUSED_MLP_KERNEL
                 pmc = os.path.join(REPO, "profiles", "r03_pmc_fused_mlp.json")
@@ -374,7 +374,10 @@ def main():
         achieved = alg_bytes / (us_k * 1e-6) / 1e9
         traffic = None
         if os.path.exists(pmc) and B == 8:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_call")
+            pj = json.load(open(pmc))
+            # the PMC pass must be of the kernel this line prices
+            if any(kname.startswith(k) or k.startswith(kname) for k in pj.get("kernels", [])):
+                traffic = pj.get("hbm_bytes_per_call")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(achieved / 8000.0, 4), "traffic": traffic, "kernel": kname,
                 "algorithmic_bytes": int(alg_bytes), "avg_us": round(us_k, 2)}

@@ -260,12 +260,13 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
 }
 
 // ---------------------------------------------------------------------------
-// The engine's own encoder / prefill GEMMs run the register ring (pf_reg defaults to true):
-// in the engine the LDS-staged kernel made the last token tile's sums vary from run to run
-// (tools/diag_det_logits.py); the register ring does not. t5g_gemm's
-// T5G_GEMM_PREFILL still selects the LDS kernel (probes, PMC passes).
+// The engine's encoder / prefill GEMMs run the LDS-staged kernel (gemm_pfl_kernel). Round 3
+// had moved them to the register ring because the last token tile's sums varied from run
+// to run: a wave could reach the ring's barrier with its own ds_reads of the slot still in
+// flight while the DMA refilled it; the barrier now waits for lgkmcnt(0) too (gemm.hip
+// wait_vm_barrier; tests/test_gpu_prefill_lds.py, tools/diag_det_logits.py).
 static int gemm(const bf16_t* X, int ldx, int M, const void* W, int N, int K, int splits, const void* bias,
-                void* Y, int ldy, int epi, hipStream_t st, bool prefill = false, bool pf_reg = true) {
+                void* Y, int ldy, int epi, hipStream_t st, bool prefill = false, bool pf_reg = false) {
     GemmArgs a;
     memset(&a, 0, sizeof(a));
     a.prefill = prefill ? (pf_reg ? 2 : 1) : 0;
