@@ -348,6 +348,7 @@ def main():
         import ctypes as C
         from t5gemma_tts_amd import _lib
         L = _lib.lib()
+        eng.set_exact(False)   # the parity sub-run leaves the exact kernels selected
         d, f = cfg.backbone.hidden_size, cfg.backbone.intermediate_size
         st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         if not args.no_fused:

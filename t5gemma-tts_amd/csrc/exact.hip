@@ -612,12 +612,192 @@ __global__ __launch_bounds__(256) void exact_attn_kernel(ExactAttnArgs a) {
     }
 }
 
+// The same SDPA with one workgroup per (query token, query head) for a compile-time head
+// dim (the engine's prefill / encoder calls): the scores are computed once (not once per
+// output slice), every key's row is requested in one go, and thread d < D owns output
+// dimension d, its chunk sums chained in registers from V values requested 32 keys at a
+// time. Same arithmetic, in the same order, as exact_attn_kernel.
+template <int D>
+__global__ __launch_bounds__(256) void exact_attn_hd_kernel(ExactAttnArgs a) {
+    static_assert(D % 32 == 0 && D <= 256, "head dim");
+    __shared__ float qs_[D];
+    __shared__ float sp[XA_BLOCK + 16];
+    __shared__ float bsum;
+    __shared__ float red[4];
+    const int qi = blockIdx.x, h = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int row = a.q_row ? a.q_row[qi] : qi;
+    const int Tk_all = a.kv_len[row];
+    const int Tq = a.q_len ? a.q_len[row] : 1;
+    const int tq = a.q_pos ? a.q_pos[qi] : Tq - 1;
+    const int abs_t = tq + (Tk_all - Tq);
+    const bool has_mask = a.window > 0 && Tk_all >= a.window;
+    int lo = 0;
+    if (has_mask && Tq == 1 && a.causal) lo = Tk_all - a.window;
+    const int Tk = Tk_all - lo;
+    const bool sdpa_causal = a.causal && !has_mask && Tq > 1;
+    const int qsz = sdpa_qsplit(Tq);
+    const int qb0 = tq - tq % qsz;
+    const int mblk = min(qsz, Tq - qb0);
+    const int nk = sdpa_causal ? min(qb0 + mblk + (Tk_all - Tq), Tk) : Tk;
+    const bool pack = xa_need_pack(Tq, Tk, a.Hq, D, a.threads, sdpa_causal);
+    const bool gemv = mblk == 1 && !pack;
+    const int kvh = h / (a.Hq / a.Hkv);
+    const bf16_t* Kb = a.K + row * a.kv_bstride + kvh * a.kv_hstride + (long)lo * D;
+    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride + (long)lo * D;
+    for (int d = tid; d < D; d += 256) qs_[d] = bf2f(a.Q[(long)qi * a.ldq + h * D + d]);
+    __syncthreads();
+    const int d = min(tid, D - 1);   // this thread's output dimension (threads >= D idle in P.V)
+    float m = -INFINITY, l = 0.f, dst = 0.f;
+    for (int bs = 0; bs < nk; bs += XA_BLOCK) {
+        const int blen = min(XA_BLOCK, Tk - bs);
+        // ---- scores: thread per key, the key's row requested whole before the dot product
+#pragma unroll 1
+        for (int kk = tid; kk < blen; kk += 256) {
+            const int key = bs + kk, kabs = key + lo;
+            bool vis;
+            if (has_mask) {
+                if (Tq == 1 && a.causal) vis = true;
+                else if (a.causal) vis = kabs <= abs_t && kabs > abs_t - a.window;
+                else vis = abs(abs_t - kabs) <= a.window;
+            } else {
+                vis = !sdpa_causal || kabs <= abs_t;
+            }
+            const bf16_t* kr = Kb + (long)(key < nk ? key : 0) * D;
+            // q is read from LDS inside the loop: hoisted out it would take D registers
+            int z = 0;
+            asm volatile("" : "+v"(z));
+            const float* qv = qs_ + z;
+            u32x4 kv[D / 8];
+#pragma unroll
+            for (int j = 0; j < D / 8; ++j) kv[j] = *(const u32x4*)(kr + 8 * j);
+            float s = -INFINITY;
+            if (vis && key < nk) {
+                float tot;
+                if (gemv) {
+                    float acc[16];
+#pragma unroll
+                    for (int l2 = 0; l2 < 16; ++l2) acc[l2] = 0.f;
+#pragma unroll
+                    for (int cb = 0; cb < D / 32; ++cb) {
+#pragma unroll
+                        for (int l2 = 0; l2 < 16; ++l2) {
+                            const uint32_t kw = kv[cb * 4 + (l2 >> 2)][l2 & 3];
+                            acc[l2] = fmaf(qv[cb * 32 + 2 * l2 + 1], bf_hi(kw), acc[l2]);
+                            acc[l2] = fmaf(qv[cb * 32 + 2 * l2], bf_lo(kw), acc[l2]);
+                        }
+                    }
+                    float v8[8], v4[4];
+#pragma unroll
+                    for (int l2 = 0; l2 < 8; ++l2) v8[l2] = __fadd_rn(acc[l2], acc[l2 + 8]);
+#pragma unroll
+                    for (int l2 = 0; l2 < 4; ++l2) v4[l2] = __fadd_rn(v8[2 * l2], v8[2 * l2 + 1]);
+                    tot = __fadd_rn(__fadd_rn(v4[0], v4[1]), __fadd_rn(v4[2], v4[3]));
+                } else {
+                    tot = 0.f;
+#pragma unroll
+                    for (int cb = 0; cb < D / 32; ++cb) {
+                        float e = 0.f, o = 0.f;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const uint32_t kw = kv[cb * 4 + (i >> 2)][i & 3];
+                            e = fmaf(qv[cb * 32 + 2 * i], bf_lo(kw), e);
+                            o = fmaf(qv[cb * 32 + 2 * i + 1], bf_hi(kw), o);
+                        }
+                        tot = __fadd_rn(tot, __fadd_rn(e, o));
+                    }
+                }
+                s = __fmul_rn(tot, a.scale);
+            }
+            sp[kk] = s;
+        }
+        __syncthreads();
+        // ---- running max, exp, lane-ordered block sum (wave 0); p rounded to bf16
+        float lm = -INFINITY;
+        for (int kk = tid; kk < blen; kk += 256) lm = fmaxf(lm, sp[kk]);
+        lm = wave_max(lm);
+        if (lane == 0) red[wave] = lm;
+        __syncthreads();
+        const float mn = fmaxf(m, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+        __syncthreads();
+        for (int kk = tid; kk < blen; kk += 256) sp[kk] = sdpa_p(__fsub_rn(sp[kk], mn), kk, blen);
+        if (tid < 16) sp[blen + tid] = 0.f;
+        __syncthreads();
+        if (wave == 0) {
+            const float ts = sdpa_block_sum_lds<XA_BLOCK>(sp, blen, lane);
+            if (lane == 0) bsum = ts;
+        }
+        __syncthreads();
+        const float et = sdpa_block_rescale(m, mn);
+        l = fmaf(et, l, bsum);
+        for (int kk = tid; kk < blen; kk += 256) sp[kk] = rbf(sp[kk]);
+        __syncthreads();
+        // ---- P.V of dimension d onto the rescaled output, in the GEMM's chunk order
+        const int ch = gemv ? 8 : (pack ? xa_even_div_chunk(blen) : 32);
+        const int nch = (blen + ch - 1) / ch;
+        const bf16_t* vc = Vb + (long)bs * D + d;
+        float acc = bs == 0 ? 0.f : __fmul_rn(dst, et);
+        // gemv: 32 keys' values (4 groups) per round trip; E/O: one chunk's (<= 32) per
+        // round trip -- a packed chunk length (an even divisor of the block) need not divide
+        // 32. Keys past the chunk / block read key 0 and are not used.
+        const int step = gemv ? 32 : ch;
+#pragma unroll 1
+        for (int k0 = 0; k0 < blen; k0 += step) {
+            const int kend = min(k0 + step, blen);
+            float vv[32];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) vv[j] = bf2f(vc[(long)(k0 + j < kend ? k0 + j : 0) * D]);
+            if (gemv) {
+                // groups of 8 keys: pairs, odd key first, a fresh chain each, added in order
+#pragma unroll
+                for (int g8 = 0; g8 < 4; ++g8) {
+                    const int c0 = k0 + 8 * g8;
+                    if (c0 >= blen) break;
+                    const int cn = min(8, blen - c0);
+                    float tmp = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; j += 2) {
+                        if (j < cn) {
+                            if (j + 1 < cn) tmp = fmaf(sp[c0 + j + 1], vv[8 * g8 + j + 1], tmp);
+                            tmp = fmaf(sp[c0 + j], vv[8 * g8 + j], tmp);
+                        }
+                    }
+                    acc = __fadd_rn(acc, tmp);
+                }
+            } else {
+                // the E/O chains of the chunk [k0, kend)
+                const int cn = kend - k0;
+                float e = 0.f, o = 0.f;
+#pragma unroll
+                for (int j = 0; j < 32; j += 2) {
+                    if (j < cn) e = fmaf(sp[k0 + j], vv[j], e);
+                    if (j + 1 < cn) o = fmaf(sp[k0 + j + 1], vv[j + 1], o);
+                }
+                const float cs = __fadd_rn(e, o);
+                acc = (bs == 0 && k0 == 0) ? cs : __fadd_rn(acc, cs);
+            }
+        }
+        dst = acc;
+        m = mn;
+        __syncthreads();
+    }
+    if (tid < D) {
+        const bf16_t o = f2bf(__fmul_rn(dst, __fdiv_rn(1.0f, l)));
+        a.O[(long)qi * a.ldo + h * D + tid] = o;
+        if (a.O16) a.O16[x16_off(qi, h * D + tid, a.ldo / 32)] = o;
+    }
+}
+
 int exact_attention(const ExactAttnArgs& a, hipStream_t st) {
     if (a.Mq <= 0) return 0;
     if (!a.Q || !a.K || !a.V || !a.kv_len || !a.O || a.D > XA_MAXD || a.D % 32 || a.Hq % a.Hkv || a.threads <= 0)
         return -1;
-    hipLaunchKernelGGL(exact_attn_kernel, dim3((unsigned)a.Mq, (unsigned)a.Hq, (unsigned)((a.D + XA_DS - 1) / XA_DS)),
-                       dim3(256), 0, st, a);
+    const dim3 g2((unsigned)a.Mq, (unsigned)a.Hq);
+    if (a.D == 256) hipLaunchKernelGGL(exact_attn_hd_kernel<256>, g2, dim3(256), 0, st, a);
+    else if (a.D == 128) hipLaunchKernelGGL(exact_attn_hd_kernel<128>, g2, dim3(256), 0, st, a);
+    else if (a.D == 64) hipLaunchKernelGGL(exact_attn_hd_kernel<64>, g2, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(exact_attn_kernel, dim3((unsigned)a.Mq, (unsigned)a.Hq, (unsigned)((a.D + XA_DS - 1) / XA_DS)),
+                            dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
