@@ -388,6 +388,10 @@ int t5g_engine_set_noise_mt(t5g_engine* e, const uint32_t* raw_dev, int32_t step
  * final slots). T5G_EUNSUPPORTED where the emulation does not follow std::sort (heapsort
  * fallback, NaN); pure host function. */
 int t5g_sort_emu(int32_t n, int32_t S, int32_t* pos, float* val, int32_t* tag);
+/* The same replay on one GPU wave (the sampler's path for <= 63 survivors), device arrays;
+ * the fail code (0 = reproduced) is written to fail_dev[0]. Tests. */
+int t5g_sort_emu_wave(int32_t n, int32_t S, int32_t* pos_dev, float* val_dev, int32_t* tag_dev,
+                      int32_t* fail_dev, void* stream);
 
 #ifdef __cplusplus
 }

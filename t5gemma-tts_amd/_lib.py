@@ -144,6 +144,7 @@ SIGNATURES = {
     "t5g_mt_exponential": (C.c_int, [_P, _L, _P, _P]),
     "t5g_engine_set_noise_mt": (C.c_int, [_P, _P, _I]),
     "t5g_sort_emu": (C.c_int, [_I, _I, _P, _P, _P]),
+    "t5g_sort_emu_wave": (C.c_int, [_I, _I, _P, _P, _P, _P, _P]),
 }
 
 # parity mode: the reference host's bf16 nn.GELU() (erf) table (tools/cpu_order/make_gelu_table.py)

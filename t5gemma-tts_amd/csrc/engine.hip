@@ -1601,6 +1601,12 @@ extern "C" int t5g_engine_set_rope_exc(t5g_engine* e, const uint32_t* tab, int32
     return T5G_OK;
 }
 
+extern "C" int t5g_sort_emu_wave(int32_t n, int32_t S, int32_t* pos_dev, float* val_dev, int32_t* tag_dev,
+                                 int32_t* fail_dev, void* stream) {
+    RC(sort_emu_wave(n, S, pos_dev, val_dev, tag_dev, fail_dev, (hipStream_t)stream));
+    return T5G_OK;
+}
+
 extern "C" void* t5g_engine_cache_ptr(t5g_engine* e, int32_t layer, int32_t which, int64_t* head_stride,
                                       int64_t* row_stride) {
     if (!e || layer < 0 || layer >= e->c.n_dec_layers || which < 0 || which > 3) return nullptr;

@@ -945,9 +945,27 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
                 stag[r] = tid;
             }
             __syncthreads();
+            // <= 63 survivors: the replay on wave 0 (one survivor per lane, sort_emu.h
+            // se_sort_wave); more: one thread (se_sort). Same steps, same slots.
+            if (nf <= 63) {
+                if (wid == 0) {
+                    SEWave W{V, nf, tid < nf ? spos[tid] : 0x7fffffff, tid < nf ? sval[tid] : -INFINITY,
+                             tid < nf ? stag[tid] : 0, 0};
+                    int* stk = (int*)&wh[2][0];
+                    const int f = se_sort_wave(W, stk, stk + SE_STACK, stk + 2 * SE_STACK);
+                    if (tid < nf) {
+                        spos[tid] = W.pos;
+                        sval[tid] = W.val;
+                        stag[tid] = W.tag;
+                    }
+                    if (tid == 0) sh_int[7] = f;
+                }
+                __syncthreads();
+            }
             if (tid == 0) {
                 SortEmu E{V, nf, spos, sval, stag, 0};
-                if (se_sort(E) || vc == -INFINITY) {
+                const int sfail = nf <= 63 ? sh_int[7] : se_sort(E);
+                if (sfail || vc == -INFINITY) {
                     sh_int[1] = 1 | 4;   // not reproducible here: stall for the host
                 } else {
                     // the cut group [g0, g1) of cv / ci, reordered by final slot
@@ -975,6 +993,26 @@ __global__ __launch_bounds__(FT) void sampler_fast_kernel(SamplerArgs a) {
         finish_row(a, pr, st, b, token, amax, ambiguous, eff_len);
     }
     T5G_TS(6);
+}
+
+// test entry: se_sort_wave on one wave over caller arrays (S <= 63), fail code in out[0]
+__global__ __launch_bounds__(64) void sort_emu_wave_kernel(int n, int S, int* pos, float* val, int* tag, int* out) {
+    __shared__ int stk[3 * SE_STACK];
+    const int l = threadIdx.x;
+    SEWave W{n, S, l < S ? pos[l] : 0x7fffffff, l < S ? val[l] : -INFINITY, l < S ? tag[l] : 0, 0};
+    const int f = se_sort_wave(W, stk, stk + SE_STACK, stk + 2 * SE_STACK);
+    if (l < S) {
+        pos[l] = W.pos;
+        val[l] = W.val;
+        tag[l] = W.tag;
+    }
+    if (l == 0) out[0] = f;
+}
+
+int sort_emu_wave(int n, int S, int* pos, float* val, int* tag, int* out, hipStream_t st) {
+    if (S < 0 || S > 63 || n < 0 || !out || (S > 0 && (!pos || !val || !tag))) return -1;
+    hipLaunchKernelGGL(sort_emu_wave_kernel, dim3(1), dim3(64), 0, st, n, S, pos, val, tag, out);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 size_t sampler_fast_ws_bytes(int B) {

@@ -222,4 +222,179 @@ SE_HD int se_sort(SortEmu& E) {
     return 0;
 }
 
+#if defined(__HIPCC__)
+// ---- the same replay on one wave: survivor i of S <= 63 in lane i, lanes kept sorted by
+// slot (inactive lanes: slot INT_MAX, value -inf), so "index by slot" is the lane index and
+// the rank / membership / lookup queries are ballots. Every function is called by all 64
+// lanes of the wave with uniform arguments; the pending-range stack lives in LDS
+// (st_* [SE_STACK], this wave only). Same steps, same results as se_sort.
+struct SEWave {
+    int n, S;
+    int pos;      // this lane's survivor slot (INT_MAX: none)
+    float val;
+    int tag;
+    int fail;
+};
+
+__device__ __forceinline__ int sew_lane() { return (int)(threadIdx.x & 63); }
+__device__ __forceinline__ int sew_rank_lt(const SEWave& W, int p) { return __popcll(__ballot(W.pos < p)); }
+__device__ __forceinline__ bool sew_any(const SEWave& W, int lo, int hi) { return __ballot(W.pos >= lo && W.pos < hi) != 0ull; }
+__device__ __forceinline__ int sew_rdi(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float sew_rdf(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ float sew_val_at(const SEWave& W, int p) {
+    const unsigned long long m = __ballot(W.pos == p);
+    return m ? sew_rdf(W.val, __ffsll((long long)m) - 1) : -INFINITY;
+}
+// lanes back into slot order (bitonic network over the 64 lanes)
+__device__ __forceinline__ void sew_sort_lanes(SEWave& W) {
+    const int lane = sew_lane();
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int pp = __shfl_xor(W.pos, j, 64);
+            const float pv = __shfl_xor(W.val, j, 64);
+            const int pt = __shfl_xor(W.tag, j, 64);
+            const bool up = (lane & k) == 0, lower = (lane & j) == 0;
+            const bool take = lower == up ? pp < W.pos : pp > W.pos;
+            if (take) { W.pos = pp; W.val = pv; W.tag = pt; }
+        }
+}
+// std::iter_swap of the slots p != q
+__device__ __forceinline__ void sew_swap(SEWave& W, int p, int q) {
+    if (p == q) return;
+    const int lane = sew_lane();
+    const unsigned long long mp = __ballot(W.pos == p), mq = __ballot(W.pos == q);
+    if (mp && mq) {   // both hold survivors: exchange value and tag (slots keep their order)
+        const int lp = __ffsll((long long)mp) - 1, lq = __ffsll((long long)mq) - 1;
+        const float vp = sew_rdf(W.val, lp), vq = sew_rdf(W.val, lq);
+        const int tp = sew_rdi(W.tag, lp), tq = sew_rdi(W.tag, lq);
+        if (lane == lp) { W.val = vq; W.tag = tq; }
+        if (lane == lq) { W.val = vp; W.tag = tp; }
+    } else if (mp || mq) {
+        if (W.pos == p) W.pos = q;
+        else if (W.pos == q) W.pos = p;
+        sew_sort_lanes(W);
+    }
+}
+__device__ __forceinline__ void sew_median_to_first(SEWave& W, int result, int a, int b, int c) {
+    const float va = sew_val_at(W, a), vb = sew_val_at(W, b), vc = sew_val_at(W, c);
+    int m;
+    if (va > vb) {
+        if (vb > vc) m = b;
+        else if (va > vc) m = c;
+        else m = a;
+    } else if (va > vc) m = a;
+    else if (vb > vc) m = c;
+    else m = b;
+    sew_swap(W, result, m);
+}
+__device__ __forceinline__ int sew_partition(SEWave& W, int first, int last, int pivot_pos) {
+    const int lane = sew_lane();
+    const float pv = sew_val_at(W, pivot_pos);
+    if (pv == -INFINITY) {   // se_partition's closed form, every interval / survivor on its own lane
+        const int i0 = sew_rank_lt(W, first), i1 = sew_rank_lt(W, last);
+        const int span = last - 1 - first;
+        const int c = lane - i0;
+        const int prev = __shfl_up(W.pos, 1, 64);
+        const int klo = c == 0 ? 0 : prev - first - c + 1;
+        const int khi = c == i1 - i0 ? span + 1 : W.pos - first - c - 1;
+        const int kneed = span - c <= 0 ? 0 : (span - c + 1) / 2;
+        const int k = klo > kneed ? klo : kneed;
+        const unsigned long long ok = __ballot(lane >= i0 && lane <= i1 && klo <= khi && k <= khi);
+        int K = 0, fK = first;
+        if (ok) {
+            const int cs = __ffsll((long long)ok) - 1;
+            K = sew_rdi(k, cs);
+            fK = first + K + (cs - i0);
+        }
+        int ret = fK;
+        if (K > 0 && ret > last - K) ret = last - K;
+        const int jm = sew_rank_lt(W, last - K);
+        // survivors j in [jm, i1) move to the (last - 1 - pos)-th -inf slot from first:
+        // slot first + k + c, c = #staying survivors t (lanes [i0, jm)) with
+        // pos_t - (t - i0) <= first + k (non-decreasing in t: a binary search)
+        // (every lane runs the search: a shuffle reads only from active lanes)
+        const int d = (lane >= i0 && lane < jm) ? W.pos - (lane - i0) : 0x7fffffff;
+        const bool mover = lane >= jm && lane < i1;
+        const int kj = mover ? last - 1 - W.pos : 0;
+        int lo = i0, hi = jm;
+        for (int it = 0; it < 7; ++it) {
+            const int mid = (lo + hi) >> 1;
+            const int dm = __shfl(d, mid & 63, 64);
+            if (lo < hi) {
+                if (dm <= first + kj) lo = mid + 1;
+                else hi = mid;
+            }
+        }
+        if (mover) W.pos = first + kj + (lo - i0);
+        sew_sort_lanes(W);
+        return ret;
+    }
+    // survivor pivot: the Hoare loop, each step a wave query
+    int f = first, l = last;
+    for (;;) {
+        while (sew_val_at(W, f) > pv) ++f;
+        --l;
+        const unsigned long long m = __ballot(W.pos <= l && W.val >= pv && W.pos != 0x7fffffff);
+        if (!m) { W.fail = 3; return f; }
+        l = sew_rdi(W.pos, 63 - __clzll((long long)m));
+        if (!(f < l)) return f;
+        sew_swap(W, f, l);
+        ++f;
+    }
+}
+
+// se_sort on one wave. Inputs in lanes 0..S-1 sorted by slot; returns the fail code
+// (0: lanes 0..S-1 hold the survivors in final slot order).
+__device__ inline int se_sort_wave(SEWave& W, int* st_first, int* st_last, int* st_depth) {
+    const int lane = sew_lane();
+    W.fail = 0;
+    if (__ballot(lane < W.S && W.val != W.val)) { W.fail = 1; return W.fail; }
+    if (W.n <= 1 || W.S == 0) return 0;
+    int lg = 0;
+    while ((2L << lg) <= W.n) ++lg;
+    int sp = 0;
+    if (lane == 0) { st_first[0] = 0; st_last[0] = W.n; st_depth[0] = 2 * lg; }
+    ++sp;
+    while (sp > 0) {
+        --sp;
+        __builtin_amdgcn_wave_barrier();
+        int first = __builtin_amdgcn_readfirstlane(st_first[sp]);
+        int last = __builtin_amdgcn_readfirstlane(st_last[sp]);
+        int depth = __builtin_amdgcn_readfirstlane(st_depth[sp]);
+        while (last - first > 16 && sew_any(W, first, last)) {
+            if (depth == 0) { W.fail = 4; return W.fail; }
+            --depth;
+            const int mid = first + (last - first) / 2;
+            sew_median_to_first(W, first, first + 1, mid, last - 1);
+            const int cut = sew_partition(W, first + 1, last, first);
+            if (W.fail) return W.fail;
+            if (sew_any(W, cut, last)) {
+                if (sp == SE_STACK) { W.fail = 5; return W.fail; }
+                if (lane == 0) { st_first[sp] = cut; st_last[sp] = last; st_depth[sp] = depth; }
+                __builtin_amdgcn_wave_barrier();
+                ++sp;
+            }
+            last = cut;
+        }
+    }
+    // final insertion sort, survivor by survivor in slot order
+    for (int i = 0; i < W.S; ++i) {
+        const float v = sew_rdf(W.val, i);
+        const int pi = sew_rdi(W.pos, i), t = sew_rdi(W.tag, i);
+        const unsigned long long m = __ballot(lane < i && W.val >= v);
+        const int j = m ? 63 - __clzll((long long)m) : -1;
+        const int np = j >= 0 ? sew_rdi(W.pos, j) + 1 : 0;
+        if (j < 0 && pi >= 16) { W.fail = 6; return W.fail; }
+        if (np == pi) continue;
+        const int up_p = __shfl_up(W.pos, 1, 64), up_t = __shfl_up(W.tag, 1, 64);
+        const float up_v = __shfl_up(W.val, 1, 64);
+        if (lane > j + 1 && lane <= i) { W.pos = up_p + 1; W.val = up_v; W.tag = up_t; }
+        if (lane == j + 1) { W.pos = np; W.val = v; W.tag = t; }
+    }
+    return 0;
+}
+#endif
+
 }  // namespace t5g

@@ -302,6 +302,7 @@ int exact_attention(const ExactAttnArgs& a, hipStream_t st);
 // scratch sbuf [Mq][Hq][cap] / mbuf [Mq][Hkv][ceil(cap / 64)][G]
 int exact_attention_decode(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, hipStream_t st);
 bool exact_attention_decode_supported(int G, int D);   // head shapes the decode launches are built for
+int sort_emu_wave(int n, int S, int* pos, float* val, int* tag, int* out, hipStream_t st);   // sampler.hip test entry
 
 // ---- sampler -------------------------------------------------------------------
 struct SamplerRow {           // per-utterance parameters (device)
