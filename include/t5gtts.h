@@ -359,7 +359,9 @@ int t5g_time_xmm(const void* X16_dev, int32_t M, const void* const* W16_list, in
 /* Single exact-order SDPA call on caller buffers (parity tests): one reference call per row b
  * with q_len[b] queries (q rows packed, q_row / q_pos per query) over kv_len[b] keys of a
  * [B][n_kv_heads][cap][head_dim] cache, torch 2.10 CPU flash-attention numerics incl. its
- * GEMM selection (gemv / unpacked / packed, threads = the reference thread count). */
+ * GEMM selection (gemv / unpacked / packed, threads = the reference thread count).
+ * q_pos = q_len = null: one query per row at its last key, on the decode launches the
+ * engine runs (scores + P.V, csrc/xattn.hip). */
 int t5g_exact_attention(const void* q_dev, int32_t Mq, const int32_t* q_row_dev, const int32_t* q_pos_dev,
                         const int32_t* q_len_dev, const void* k_cache_dev, const void* v_cache_dev, int32_t cap,
                         const int32_t* kv_len_dev, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,

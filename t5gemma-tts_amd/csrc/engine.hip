@@ -1972,6 +1972,18 @@ extern "C" int t5g_exact_attention(const void* q, int32_t Mq, const int32_t* q_r
     a.threads = threads;
     a.O = (bf16_t*)out;
     a.ldo = a.ldq;
+    if (!q_pos && !q_len) {   // one query per row at its last key: the engine's decode launches (xattn.hip)
+        hipStream_t st = (hipStream_t)stream;
+        const int G = n_heads / n_kv_heads, nsplit = (cap + 63) / 64;
+        float *sb = nullptr, *mb = nullptr;
+        HIPCHK(hipMallocAsync((void**)&sb, (size_t)Mq * n_heads * cap * 4, st));
+        HIPCHK(hipMallocAsync((void**)&mb, (size_t)Mq * n_kv_heads * nsplit * G * 4, st));
+        const int rc = exact_attention_decode(a, sb, mb, cap, st);
+        hipFreeAsync(sb, st);
+        hipFreeAsync(mb, st);
+        RC(rc);
+        return T5G_OK;
+    }
     RC(exact_attention(a, (hipStream_t)stream));
     return T5G_OK;
 }

@@ -43,28 +43,34 @@ __device__ __forceinline__ void xd_rope(float x1, float x2, float c, float sn, f
 // FUSE: the queries arrive un-rotated and are rotated while staged (rope_tab), and, with
 // kv_new, the workgroup holding the row's new key (slot kv_len - 1) rotates it, appends it
 // and its value to the cache and uses the rotated key directly (no separate RoPE launch).
+// Four threads per key (t = 4 key + qa): thread qa keeps the gemv's lane accumulators
+// l2 = 4 qa .. 4 qa + 3 (its 16-byte slice of every 32-element chunk of the key's row) and
+// chains them over the chunks; the hadd tree (l2 + l2 ^ 8, adjacent pairs, pairs, last
+// pair) then takes two exchanges inside the quad -- the oneDNN gemv's adds in its order.
 template <int G, int XD_D, bool FUSE>
-__global__ __launch_bounds__(64) void xattn_scores_kernel(ExactAttnArgs a, float* sbuf, float* mbuf, int cap,
-                                                          int nsplit) {
-    constexpr int H2 = XD_D / 2;
+__global__ __launch_bounds__(256) void xattn_scores_kernel(ExactAttnArgs a, float* sbuf, float* mbuf, int cap,
+                                                           int nsplit) {
+    constexpr int H2 = XD_D / 2, NCB = XD_D / 32;
     __shared__ float qs[G][XD_D];
     __shared__ uint32_t knew[FUSE ? XD_D / 2 : 1];   // the rotated new key as bf16 pairs
-    const int qi = blockIdx.x, kvh = blockIdx.y, ch = blockIdx.z, lane = threadIdx.x;
+    __shared__ float wmax[4][G];
+    const int qi = blockIdx.x, kvh = blockIdx.y, ch = blockIdx.z, tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6, kl = tid >> 2, qa = tid & 3;
     const int row = a.q_row ? a.q_row[qi] : qi;
     int lo, hi;
     xd_range(a, row, lo, hi);
     const int c0 = lo + ch * XD_CH;
     if (c0 >= hi) return;
-    const int key = c0 + lane;
+    const int key = c0 + kl;
     const bool valid = key < hi;
-    const bf16_t* kr = a.K + row * a.kv_bstride + kvh * a.kv_hstride + (long)(valid ? key : c0) * XD_D;
-    u32x4 kv[XD_D / 8];
+    const bf16_t* kr = a.K + row * a.kv_bstride + kvh * a.kv_hstride + (long)(valid ? key : c0) * XD_D + 8 * qa;
+    u32x4 kv[NCB];
 #pragma unroll
-    for (int j = 0; j < XD_D / 8; ++j) kv[j] = *(const u32x4*)(kr + 8 * j);
+    for (int cb = 0; cb < NCB; ++cb) kv[cb] = *(const u32x4*)(kr + 32 * cb);
     // the G query rows of this kv head (GQA: heads kvh * G + g), broadcast from LDS
     if constexpr (FUSE) {
         const float* tab = a.rope_tab + (long)row * XD_D;
-        for (int i = lane; i < G * H2; i += 64) {
+        for (int i = tid; i < G * H2; i += 256) {
             const int g = i / H2, d = i % H2;
             const bf16_t* qh = a.Q + (long)qi * a.ldq + (kvh * G + g) * XD_D;
             float o1, o2;
@@ -72,7 +78,7 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(ExactAttnArgs a, float
             qs[g][d] = o1;
             qs[g][d + H2] = o2;
         }
-        // the workgroup holding the new key: rotate it (two pairs per lane), append K and V
+        // the workgroup holding the new key: rotate it, append K and V
         const bool has_new = a.kv_new && hi - 1 >= c0 && hi - 1 < c0 + XD_CH;
         if (has_new) {
             const long slot = hi - 1;
@@ -80,7 +86,7 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(ExactAttnArgs a, float
             const bf16_t* vn = a.kv_new + (long)qi * a.ld_new + a.v_col0 + kvh * XD_D;
             bf16_t* kc = (bf16_t*)a.K + row * a.kv_bstride + kvh * a.kv_hstride + slot * XD_D;
             bf16_t* vc = (bf16_t*)a.V + row * a.kv_bstride + kvh * a.kv_hstride + slot * XD_D;
-            for (int d = lane; d < H2; d += 64) {
+            for (int d = tid; d < H2; d += 256) {
                 float o1, o2;
                 xd_rope(bf2f(kn[d]), bf2f(kn[d + H2]), tab[d], tab[H2 + d], o1, o2);
                 kc[d] = f2bf(o1);
@@ -88,15 +94,15 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(ExactAttnArgs a, float
                 ((bf16_t*)knew)[d] = f2bf(o1);
                 ((bf16_t*)knew)[d + H2] = f2bf(o2);
             }
-            for (int d = lane; d < XD_D; d += 64) vc[d] = vn[d];
+            for (int d = tid; d < XD_D; d += 256) vc[d] = vn[d];
         }
         __syncthreads();
         if (has_new && key == hi - 1) {
 #pragma unroll
-            for (int j = 0; j < XD_D / 8; ++j) kv[j] = *(const u32x4*)&knew[4 * j];
+            for (int cb = 0; cb < NCB; ++cb) kv[cb] = *(const u32x4*)&knew[cb * 16 + 4 * qa];
         }
     } else {
-        for (int i = lane; i < G * XD_D / 2; i += 64) {
+        for (int i = tid; i < G * XD_D / 2; i += 256) {
             const int g = i / (XD_D / 2), p = i % (XD_D / 2);
             const uint32_t w = *(const uint32_t*)(a.Q + (long)qi * a.ldq + (kvh * G + g) * XD_D + 2 * p);
             qs[g][2 * p] = bf_lo(w);
@@ -107,33 +113,38 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(ExactAttnArgs a, float
     float sc[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        float acc[16];
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};   // lane accumulators l2 = 4 qa + i
 #pragma unroll
-        for (int l2 = 0; l2 < 16; ++l2) acc[l2] = 0.f;
+        for (int cb = 0; cb < NCB; ++cb) {
+            const float* qc = &qs[g][cb * 32 + 8 * qa];
 #pragma unroll
-        for (int cb = 0; cb < XD_D / 32; ++cb) {
-            const int c = cb * 32;
-#pragma unroll
-            for (int l2 = 0; l2 < 16; ++l2) {
-                const uint32_t kw = kv[cb * 4 + (l2 >> 2)][l2 & 3];
-                acc[l2] = fmaf(qs[g][c + 2 * l2 + 1], bf_hi(kw), acc[l2]);
-                acc[l2] = fmaf(qs[g][c + 2 * l2], bf_lo(kw), acc[l2]);
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t kw = kv[cb][i];
+                acc[i] = fmaf(qc[2 * i + 1], bf_hi(kw), acc[i]);
+                acc[i] = fmaf(qc[2 * i], bf_lo(kw), acc[i]);
             }
         }
-        float v8[8], v4[4];
+        // v8[l2] = acc[l2] + acc[l2 + 8] (partner quad lane qa ^ 2), on lanes qa = 0, 1
+        float v8[4];
 #pragma unroll
-        for (int l2 = 0; l2 < 8; ++l2) v8[l2] = __fadd_rn(acc[l2], acc[l2 + 8]);
-#pragma unroll
-        for (int l2 = 0; l2 < 4; ++l2) v4[l2] = __fadd_rn(v8[2 * l2], v8[2 * l2 + 1]);
-        sc[g] = __fmul_rn(__fadd_rn(__fadd_rn(v4[0], v4[1]), __fadd_rn(v4[2], v4[3])), a.scale);
+        for (int i = 0; i < 4; ++i) v8[i] = __fadd_rn(acc[i], xlane<2>(acc[i]));
+        // v4: lane 0 holds v8[0..3] -> v4[0], v4[1]; lane 1 holds v8[4..7] -> v4[2], v4[3]
+        const float va = __fadd_rn(__fadd_rn(v8[0], v8[1]), __fadd_rn(v8[2], v8[3]));
+        // (v4[0] + v4[1]) + (v4[2] + v4[3]) on lane qa = 0
+        sc[g] = __fmul_rn(__fadd_rn(va, xlane<1>(va)), a.scale);
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        const float s = valid ? sc[g] : -INFINITY;
-        if (valid) sbuf[((long)qi * a.Hq + kvh * G + g) * cap + (key - lo)] = s;
+        const bool own = valid && qa == 0;
+        const float s = own ? sc[g] : -INFINITY;
+        if (own) sbuf[((long)qi * a.Hq + kvh * G + g) * cap + (key - lo)] = s;
         const float mx = wave_max(s);
-        if (lane == 0) mbuf[(((long)qi * a.Hkv + kvh) * nsplit + ch) * G + g] = mx;
+        if (lane == 0) wmax[wave][g] = mx;
     }
+    __syncthreads();
+    if (tid < G)
+        mbuf[(((long)qi * a.Hkv + kvh) * nsplit + ch) * G + tid] =
+            fmaxf(fmaxf(wmax[0][tid], wmax[1][tid]), fmaxf(wmax[2][tid], wmax[3][tid]));
 }
 
 template <int G, int XD_D>
@@ -268,8 +279,8 @@ __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const fl
 template <int G, int D>
 static void launch_xd(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, int nsplit, hipStream_t st) {
     const dim3 gs((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)nsplit), gp((unsigned)a.Mq, (unsigned)a.Hkv, D / XD_DZ);
-    if (a.rope_tab) hipLaunchKernelGGL((xattn_scores_kernel<G, D, true>), gs, dim3(64), 0, st, a, sbuf, mbuf, cap, nsplit);
-    else hipLaunchKernelGGL((xattn_scores_kernel<G, D, false>), gs, dim3(64), 0, st, a, sbuf, mbuf, cap, nsplit);
+    if (a.rope_tab) hipLaunchKernelGGL((xattn_scores_kernel<G, D, true>), gs, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
+    else hipLaunchKernelGGL((xattn_scores_kernel<G, D, false>), gs, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
     hipLaunchKernelGGL((xattn_pv_kernel<G, D>), gp, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
 }
 

@@ -137,6 +137,42 @@ def test_xmm_decode_parts_bitwise(M, N, K, kb):
 
 
 # ------------------------------------------------------------------------- SDPA
+@pytest.mark.parametrize("Tk,window,G", [(1, 0, 2), (60, 0, 2), (64, 0, 2), (65, 0, 2), (152, 0, 2), (513, 0, 2),
+                                         (903, 0, 2), (40, 8, 2), (600, 0, 1), (200, 0, 1)])
+def test_decode_attention_launches_bitwise_vs_cpu_order(Tk, window, G):
+    """The engine's decode attention launches (csrc/xattn.hip: the scores launch, four threads
+    per key keeping the gemv's lane accumulators, and the P.V launch) == oracle.cpu_order.sdpa
+    for one query per row at its last key: 3 rows of different lengths, 4 kv heads."""
+    _need_gpu()
+    from oracle import cpu_order
+    from t5gemma_tts_amd import _lib
+    L = _lib.lib()
+    Hkv, D = 4, 256
+    Hq = Hkv * G
+    lens = [Tk, max(1, Tk - 7), max(1, Tk // 2)]
+    B, cap = len(lens), max(Tk, 64)
+    g = torch.Generator().manual_seed(Tk * 31 + window + G)
+    q = torch.randn(B, Hq, D, generator=g).to(BF16)
+    kc = torch.randn(B, Hkv, cap, D, generator=g).to(BF16)
+    vc = torch.randn(B, Hkv, cap, D, generator=g).to(BF16)
+    i32 = dict(dtype=torch.int32, device="cuda")
+    kv_len = torch.tensor(lens, **i32)
+    o = torch.zeros(B, Hq * D, dtype=BF16, device="cuda")
+    qd, kd, vd = q.reshape(B, Hq * D).cuda(), kc.cuda(), vc.cuda()   # held: the call reads them
+    rc = L.t5g_exact_attention(C.c_void_p(qd.data_ptr()), B, None, None, None, C.c_void_p(kd.data_ptr()),
+                               C.c_void_p(vd.data_ptr()), cap, C.c_void_p(kv_len.data_ptr()), Hq, Hkv, D, 1,
+                               window, 1.0 / 16, 8, C.c_void_p(o.data_ptr()), _st())
+    assert rc == 0
+    torch.cuda.synchronize()
+    got = o.cpu().view(B, Hq, D)
+    for b, n in enumerate(lens):
+        lo = n - window if (window and n >= window) else 0
+        kk = kc[b, :, lo:n].repeat_interleave(G, 0)
+        vv = vc[b, :, lo:n].repeat_interleave(G, 0)
+        ref = cpu_order.sdpa(q[b][:, None], kk, vv, 1.0 / 16, is_causal=True, Hq=Hq)[:, 0]
+        assert torch.equal(got[b].view(torch.int16), ref.view(torch.int16)), (b, n)
+
+
 @pytest.mark.parametrize("Tq,Tk,causal,window", [
     (1, 1, 1, 0), (1, 60, 0, 0), (1, 152, 1, 0), (1, 903, 1, 0), (1, 600, 1, 0),   # decode (gemv)
     (60, 60, 0, 0), (33, 33, 0, 0), (152, 152, 1, 0), (152, 60, 0, 0), (200, 200, 1, 0),   # prefill / encoder
