@@ -329,7 +329,7 @@ int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void* stream, f
  * exact-erf form, equal except on 24 inputs in [-5.4, -3.1]); threads: the reference
  * host's torch thread count (8, the only measured K-split table; others -> EUNSUPPORTED).
  * enable = 0 returns to the fast kernels. Per-utterance token counts (text, prompt + 1)
- * must not exceed 1024 in parity mode (the measured table, csrc/ref_ksplit.h). Synchronous. */
+ * must not exceed 5001 in parity mode (the measured table, csrc/ref_ksplit.h). Synchronous. */
 int t5g_engine_set_exact(t5g_engine* e, int32_t enable, const uint16_t* gelu_lut, int32_t threads);
 /* Single exact-order Linear on caller buffers (parity tests): Y = X . W^T on a packed W in
  * the reference's order (32-element E/O chunk chains, chunk sums folded; K split into

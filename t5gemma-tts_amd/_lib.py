@@ -153,7 +153,7 @@ GELU_ERF_TABLE = os.path.join(_PKG, "data", "gelu_erf_bf16.bin")
 # value after the bf16 cast (tools/cpu_order/make_rope_table.py); covers every position
 # of an utterance whose estimated total length is <= ROPE_EXC_MAX_LEN
 ROPE_EXC_TABLE = os.path.join(_PKG, "data", "rope_trig_exc.bin")
-ROPE_EXC_MAX_LEN = 4096
+ROPE_EXC_MAX_LEN = 8192
 
 
 def rope_exc_table():
@@ -179,7 +179,7 @@ def gelu_erf_table():
 # the K-split table of the reference host's F.linear was measured for this many threads
 # and per-utterance token counts up to EXACT_MAX_TOKENS (csrc/ref_ksplit.h)
 EXACT_THREADS = 8
-EXACT_MAX_TOKENS = 1024
+EXACT_MAX_TOKENS = 5001
 
 _lib = None
 

@@ -271,7 +271,7 @@ __host__ __device__ inline long x16_off(long m, int k, int KB) {
 }
 // torch CPU SDPA kv blocks (common.h sdpa_*): keys per block, blocks per row (kv_cap <= 4096)
 constexpr int SDPA_KV_BLOCK = 512;
-constexpr int SDPA_MAX_BLOCKS = 8;
+constexpr int SDPA_MAX_BLOCKS = 16;   // 8 192 keys
 
 struct ExactAttnArgs {
     const bf16_t* Q;          // [Mq][ldq] RoPE'd queries

@@ -355,6 +355,12 @@ def gen_config_goldens(RT, which):
         x, y, _ = make_batch(cfg, 1, seed=20251226, T_x=16, T_p=0)[0]
         gen_cases_golden(RT, "golden_c1", [_row_case(x, y, 150, 4200, top_k=1, top_p=1.0, temperature=1.0)],
                          {"extra_cutoff": 5.0})
+    if "longprompt2k" in which:   # a 2 001-token prefill: the K-split table past M = 1 024
+        steps = 8
+        kw = {"extra_cutoff": (steps - 2) / 50.0}
+        cfgl = named_config("2b2b", **kw)
+        x, y, _ = make_batch(cfgl, 1, seed=20251227, T_x=60, T_p=2000)[0]
+        gen_cases_golden(RT, "golden_longprompt2k", [_row_case(x, y, len(y) + 1, 4400)], kw)
     if "longprompt" in which:
         steps = 16
         kw = {"extra_cutoff": (steps - 2) / 50.0}
@@ -421,7 +427,7 @@ if __name__ == "__main__":
         gen_full_golden(RT)
     if "long" in todo:
         gen_long_golden(RT)
-    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt")]
+    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt", "longprompt2k")]
     if cfg_todo:
         gen_config_goldens(RT, cfg_todo)
     if "mid" in todo:

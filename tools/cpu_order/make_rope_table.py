@@ -26,7 +26,7 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 OUT = os.path.join(REPO, "t5gemma-tts_amd", "data", "rope_trig_exc.bin")
-E_MAX = 4096
+E_MAX = 8192
 SCALE = 2000.0
 
 
