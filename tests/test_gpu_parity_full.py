@@ -241,7 +241,7 @@ def test_c3_batch8_exact_vs_reference():
 # (tests/golden/make_golden.py gen_config_goldens), each alone and inside a batch of the
 # workload's own size (the other rows: bench.make_batch rows of the same shape)
 CONFIG_GOLDENS = [("golden_c2", 1, 0), ("golden_c1", 1, 0), ("golden_c4", 8, 3), ("golden_c2", 32, 17),
-                  ("golden_longprompt", 1, 0), ("golden_longprompt", 4, 2)]
+                  ("golden_longprompt", 1, 0), ("golden_longprompt", 4, 2), ("golden_longprompt2k", 1, 0)]
 
 
 @pytest.mark.timeout(900)
@@ -279,7 +279,8 @@ def test_config_golden_exact(name, batch, slot):
             seeds.append(5000 + b)
     p = SamplingParams(top_k=c["top_k"], top_p=c["top_p"], min_p=c["min_p"], temperature=c["temperature"],
                        stop_repetition=c["stop_repetition"])
-    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=batch, max_text=64, max_audio=1024,
+    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=batch, max_text=64,
+                           max_audio=max(1024, len(c["y"]) + len(c["gen"]) + 16),
                            max_gen=max(760, len(c["gen"]) + 8))
     out = eng.generate(utts, p, seeds=seeds, parity=True, record_logits=True)
     n = len(c["gen"])
