@@ -182,6 +182,8 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="C5: generate + XCodec2 decode in the timed region")
     ap.add_argument("--no-fused", action="store_true",
                     help="decode MLP half as three launches instead of the persistent fused launch (A/B)")
+    ap.add_argument("--no-attn-flash", action="store_true",
+                    help="fast path: decode self attention as the two-launch aten-order form (A/B)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo (CPU collectives; lets N ranks share one GPU "
                          "to rehearse the sharded path)")
@@ -232,6 +234,8 @@ def main():
                            max_audio=wl_tp + 1 + n_tok_row + 8, max_gen=n_tok_row + 4)
     if args.no_fused:
         eng.set_fused(False)
+    if args.no_attn_flash:
+        eng.set_attn_flash(False)
     codec = None
     if args.e2e:
         from t5gemma_tts_amd.codec import XCodec2Decoder, codec_44k, synthetic_codec_weights

@@ -290,6 +290,19 @@ typedef struct {
 int64_t t5g_attention_decode_work_bytes(int32_t B, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
                                         int32_t cap);
 int t5g_attention_decode(const t5g_attn_decode_args* args, void* stream);
+/* The fast path's form of the same attention (the engine's default decode self attention
+ * in fast mode, t5g_engine_set_attn_flash): rows of > 64 keys finish in ONE launch -- each
+ * 64-key chunk's workgroup computes an online-softmax partial (chunk max, sum of exp,
+ * unnormalised bf16(p).V), the last to arrive for a (row, kv head) combines them. Not
+ * aten's 512-key block order (fast-mode numerics); rows of <= 64 keys as
+ * t5g_attention_decode. `work` as t5g_attention_decode_work_bytes(); its last
+ * B * n_kv_heads words are arrival tickets that must be zero before the first call (each
+ * call leaves them zero). */
+int t5g_attention_decode_flash(const t5g_attn_decode_args* args, void* stream);
+/* Decode self attention in fast mode: 1 (default) the one-launch flash form above, 0 the
+ * two-launch aten-order form (scores, then P.V / combine). Reference: [tf]
+ * T5GemmaSelfAttention :264-304; no reference-side equivalent switch. */
+int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable);
 
 /* Sampler launch shape: 0 (default) the 16-slice multi-block kernel, falling back per row to
  * the single-block kernel when a row's top-k / survivor set exceeds it; 1 the single-block

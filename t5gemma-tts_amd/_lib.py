@@ -128,6 +128,8 @@ SIGNATURES = {
     "t5g_time_gemv": (C.c_int, [C.POINTER(GemvArgs), C.POINTER(_P), _I, _I, _P, C.POINTER(_F)]),
     "t5g_attention_decode_work_bytes": (_L, [_I, _I, _I, _I, _I]),
     "t5g_attention_decode": (C.c_int, [C.POINTER(AttnDecodeArgs), _P]),
+    "t5g_attention_decode_flash": (C.c_int, [C.POINTER(AttnDecodeArgs), _P]),
+    "t5g_engine_set_attn_flash": (C.c_int, [_P, _I]),
     "t5g_engine_set_exact": (C.c_int, [_P, _I, _P, _I]),
     "t5g_engine_set_sampler_path": (C.c_int, [_P, _I]),
     "t5g_engine_set_fused": (C.c_int, [_P, _I]),

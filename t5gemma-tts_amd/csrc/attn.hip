@@ -18,6 +18,8 @@
 
 namespace t5g {
 
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
 T5G_TS_UNIT(attn)
 
 // ---------------------------------------------------------------------------
@@ -300,7 +302,154 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 constexpr int QSMAX = 4;   // q / appended-k/v projection slabs read by the decode kernel
 constexpr int DCH = 64;    // keys per decode chunk
 
-template <int D, int G, bool VFIRST>
+// Flash-form tail of a chunk workgroup (see attn_decode_kernel): sm holds the chunk's
+// scaled scores, vr its V rows (appended value included). Partials go out as sc1
+// (write-through) buffer stores; every storing wave drains; one lane takes the (row, kv
+// head)'s ticket; the workgroup whose add returns nch - 1 reads them back with sc1 loads
+// (the sampler's / fused block's hand-off form, CDNA guide G16 row 1) and resets the ticket.
+template <int D, int G>
+__device__ __forceinline__ void attn_flash_finish(const AttnArgs& a, float (&sm)[G][DCH], const u32x4 (&vr)[DCH / (4 * (64 / (D / 8)))],
+                                                  int qi, int kvh, int sp, int nch, int n, int wave, int lane, int kg,
+                                                  int dl) {
+    constexpr int LPK = D / 8;
+    constexpr int KPW = 64 / LPK;
+    constexpr int KPB = KPW * 4;
+    constexpr int NIT = DCH / KPB;
+    constexpr int FB = 16;  // chunk partials per combine batch (one batch up to 1 024 keys)
+    __shared__ f32x4 ored[4][G][LPK][2];
+    __shared__ float cstat[G][2];
+    __shared__ float wts[G][64];
+    __shared__ float lsum[G];
+    __shared__ int last;
+    const int tid = (int)threadIdx.x;
+    const long rec = ((long)qi * a.Hkv + kvh) * a.nsplit;   // chunk records of this (row, kv head)
+    if (wave < G) {
+        const int g = wave;
+        const float s = lane < n ? sm[g][lane] : -INFINITY;
+        const float mx = wave_max(s);
+        const float p = lane < n ? __expf(s - mx) : 0.f;
+        sm[g][lane] = rbf(p);
+        const float l = xsum<64>(p);
+        if (lane == 0) {
+            cstat[g][0] = mx;
+            cstat[g][1] = l;
+        }
+    }
+    __syncthreads();
+    float o[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        const int jl = i * KPB + wave * KPW + kg;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float p = sm[g][jl];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                o[g][2 * jj] += p * bf_lo(vr[i][jj]);
+                o[g][2 * jj + 1] += p * bf_hi(vr[i][jj]);
+            }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+            for (int off = LPK; off < 64; off <<= 1) o[g][jj] += __shfl_xor(o[g][jj], off, 64);
+    if (kg == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            ored[wave][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
+            ored[wave][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
+        }
+    }
+    __syncthreads();
+    const long nrec = (long)a.Mq * a.Hkv * a.nsplit;
+    const __amdgpu_buffer_rsrc_t prs = frag_rsrc(a.fpart, (uint32_t)(nrec * G * D * 4));
+    const __amdgpu_buffer_rsrc_t srs = frag_rsrc(a.fstat, (uint32_t)(nrec * G * 2 * 4));
+    for (int idx = tid; idx < G * LPK; idx += 256) {
+        const int g = idx / LPK, d8 = idx % LPK;
+        const f32x4 lo4 = ored[0][g][d8][0] + ored[1][g][d8][0] + ored[2][g][d8][0] + ored[3][g][d8][0];
+        const f32x4 hi4 = ored[0][g][d8][1] + ored[1][g][d8][1] + ored[2][g][d8][1] + ored[3][g][d8][1];
+        const int off = (int)((((rec + sp) * G + g) * D + 8 * d8) * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo4), prs, off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi4), prs, off + 16, 0, 16);
+    }
+    if (tid < G) {
+        const u32x2_t st = {__float_as_uint(cstat[tid][0]), __float_as_uint(cstat[tid][1])};
+        __builtin_amdgcn_raw_buffer_store_b64(st, srs, (int)((((rec + sp) * G + tid) * 2) * 4), 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    T5G_TS(3);
+    if (tid == 0)
+        last = __hip_atomic_fetch_add(a.fticket + (long)qi * a.Hkv + kvh, 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nch - 1);
+    __syncthreads();
+    T5G_TS(4);
+    if (!last) return;
+    // ---- the combine (last chunk to arrive). Waves 0..G-1: the chunk weights
+    // exp(m_c - M) and the sum; waves G..: the output octets, their first batch of
+    // partials requested before the weights are known.
+    if (tid == 0) __hip_atomic_store(a.fticket + (long)qi * a.Hkv + kvh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    constexpr int NOUT = G * D / 4;                   // f32x4 outputs
+    static_assert(NOUT <= 256 - 64 * G, "flash combine geometry");
+    const int ot = tid - 64 * G;                       // output thread index
+    const bool outer = ot >= 0 && ot < NOUT;
+    const int og = outer ? ot / (D / 4) : 0, o4 = outer ? ot % (D / 4) : 0;
+    auto pload = [&](f32x4 (&pv)[FB], int c0) {
+#pragma unroll
+        for (int k = 0; k < FB; ++k) {
+            int off = (c0 + k < nch && outer) ? (int)((((rec + c0 + k) * G + og) * D + 4 * o4) * 4) : (int)0x7ffffff0;
+            asm volatile("" : "+v"(off));
+            pv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, off, 0, 16));
+        }
+    };
+    f32x4 pv[FB];
+    pload(pv, 0);
+    if (wave < G) {
+        const int g = wave;
+        float m = -INFINITY, l = 0.f;
+        if (lane < nch) {
+            const u32x2_t st = __builtin_amdgcn_raw_buffer_load_b64(srs, (int)((((rec + lane) * G + g) * 2) * 4), 0, 16);
+            m = __uint_as_float(st[0]);
+            l = __uint_as_float(st[1]);
+        }
+        const float M = wave_max(m);
+        const float w = lane < nch ? __expf(m - M) : 0.f;
+        const float L = xsum<64>(w * l);
+        wts[g][lane] = w;
+        if (lane == 0) lsum[g] = L;
+    }
+    __syncthreads();
+    T5G_TS(6);
+    if (!outer) return;
+    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < nch; c0 += FB) {
+        if (c0 > 0) pload(pv, c0);
+#pragma unroll
+        for (int k = 0; k < FB; ++k) {
+            const float w = c0 + k < nch ? wts[og][c0 + k] : 0.f;
+            acc += w * pv[k];
+        }
+    }
+    const float inv = 1.0f / lsum[og];
+    const u32x2_t ow = {pack2(acc[0] * inv, acc[1] * inv), pack2(acc[2] * inv, acc[3] * inv)};
+    *(u32x2_t*)(a.O + (long)qi * a.ldo + (kvh * G + og) * D + 4 * o4) = ow;
+    T5G_TS_BY(5, 64 * G);
+}
+
+//  * FLASH (fast path, a.flash): rows of > 64 keys finish in the same launch -- each
+//    chunk's workgroup requests its V with K, computes its online-softmax partial (chunk
+//    max m_c, l_c = sum exp(s - m_c), unnormalised bf16(p).V) and hands it off through
+//    write-through stores + an arrival ticket; the last chunk of the (row, kv head) to
+//    arrive combines: O = sum_c exp(m_c - M) o_c / sum_c exp(m_c - M) l_c (M = max m_c).
+//    Not aten's 512-key block order: fast mode only (parity mode runs xattn.hip).
+template <int D, int G, bool VFIRST, bool FLASH = false>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     constexpr int LPK = D / 8;
     constexpr int KPW = 64 / LPK;
@@ -391,6 +540,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     // cross attention) requests it with K; otherwise it is requested after the scores, so
     // NIT V registers are not held through the K stream: <= 128 VGPRs, four workgroups per
     // CU, 1 024 chunk workgroups in one round (32 rows x 4 kv heads x 8 chunks)
+    // (all K requests ahead of all V requests measured the same: the data phase is the
+    // memory system's loaded latency for every chunk's requests at once, not the order)
     u32x4 kr[NIT], vr[NIT];
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
@@ -399,7 +550,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
         if constexpr (VFIRST)
             vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  vrs, single ? off : (int)0x7ffffff0, 0, 0));
+                                                  vrs, (single || FLASH) ? off : (int)0x7ffffff0, 0, 0));
     }
     float q[G][8];
     if (a.Qpart) {
@@ -504,6 +655,12 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
     }
     __syncthreads();
     T5G_TS(2);
+    if constexpr (FLASH) {
+        if (!single) {
+            attn_flash_finish<D, G>(a, sm, vr, qi, kvh, sp, (span + DCH - 1) / DCH, n, wave, lane, kg, dl);
+            return;
+        }
+    }
     if (!single) {
         // publish the chunk's scores and maxima (read by the next two launches)
         if (wave < G) {
@@ -929,6 +1086,10 @@ static int launch_decode(const AttnArgs& a_in, hipStream_t st) {
         }
     }
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)a.nsplit);
+    if (a.flash && a.nsplit > 1) {
+        hipLaunchKernelGGL((attn_decode_kernel<D, G, true, true>), grid, dim3(256), 0, st, a);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
     if (a.nsplit == 1) hipLaunchKernelGGL((attn_decode_kernel<D, G, true>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_decode_kernel<D, G, false>), grid, dim3(256), 0, st, a);
     if (a.nsplit > 1) {
@@ -949,6 +1110,9 @@ int attention_decode(const AttnArgs& a, hipStream_t st) {
     if (a.eager || a.kv_cap <= 0 || a.kv_cap > SDPA_KV_BLOCK * SDPA_MAX_BLOCKS) return -1;
     if (a.nsplit != (a.kv_cap + DCH - 1) / DCH) return -1;   // 64-key chunks from the row start
     if (a.nsplit > 1 && (!a.sbuf || !a.mbuf || a.nsplit > 64)) return -1;
+    if (a.flash && a.nsplit > 1 && (!a.fpart || !a.fstat || !a.fticket || a.G * a.D / 4 > 256 - 64 * a.G ||
+                                    (long)a.Mq * a.Hkv * a.nsplit * a.G * a.D * 4 > 0x7fff0000L))
+        return -1;
     if (a.append && (!a.Qpart || !a.rope_tab || (a.G + 2) * a.D / 4 > 256)) return -1;
     if (a.Qpart && (a.q_nsplit < 1 || a.q_nsplit > QSMAX)) return -1;
     if (a.D == 256 && a.G == 2) return launch_decode<256, 2>(a, st);

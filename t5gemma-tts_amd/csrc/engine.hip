@@ -85,6 +85,12 @@ struct t5g_engine {
     static constexpr int s_qkv = 2, s_o = 4, s_down = 8;
     float* asbuf = nullptr;   // decode attention scores of rows > 64 keys [B][Hq][max(max_audio, max_text)]
     float* ambuf = nullptr;   // decode attention chunk maxima [B][Hkv][nsplit][G]
+    // flash-form decode attention (fast path, t5g_engine_set_attn_flash): chunk partials,
+    // chunk (max, sum), one arrival ticket per (row, kv head) -- zeroed here, left zero
+    bool attn_flash = true;
+    float* afpart = nullptr;    // [B][Hkv][nsplit][G][D]
+    float* afstat = nullptr;    // [B][Hkv][nsplit][G][2]
+    unsigned* aftick = nullptr; // [B][Hkv]
     int B = 0;            // rows of the current call
     int text_max = 0;     // longest text of the current call (host hint; 0: max_text)
     const bf16_t* noise = nullptr;
@@ -207,6 +213,9 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     const int cap_max = c.max_audio > c.max_text ? c.max_audio : c.max_text;
     rc |= alloc(e, &e->asbuf, (int64_t)B * c.n_heads * cap_max);
     rc |= alloc(e, &e->ambuf, (int64_t)B * Hkv * nsplit_max * G);
+    rc |= alloc(e, &e->afpart, (int64_t)B * Hkv * nsplit_max * G * D);
+    rc |= alloc(e, &e->afstat, (int64_t)B * Hkv * nsplit_max * G * 2);
+    rc |= alloc(e, &e->aftick, (int64_t)B * Hkv);
     const int64_t enc_cache = (int64_t)B * Hkv * c.max_text * D;
     rc |= alloc(e, &e->enc_k, enc_cache);
     rc |= alloc(e, &e->enc_v, enc_cache);
@@ -952,6 +961,10 @@ static int decode_attention(t5g_engine* e, int M, const bf16_t* K, const bf16_t*
     a.append = append ? 1 : 0;
     a.k_col0 = e->q_dim - q_col0;
     a.v_col0 = e->q_dim + e->kv_dim - q_col0;
+    a.flash = e->attn_flash ? 1 : 0;
+    a.fpart = e->afpart;
+    a.fstat = e->afstat;
+    a.fticket = e->aftick;
     return attention_decode(a, st);
 }
 
@@ -1491,6 +1504,15 @@ extern "C" int t5g_engine_poison_handoff(t5g_engine* e, uint32_t code) {
     return T5G_OK;
 }
 
+extern "C" int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable) {
+    if (!e) return T5G_EINVAL;
+    if (e->attn_flash != (enable != 0)) {
+        e->attn_flash = enable != 0;
+        drop_graphs(e);   // captured launches follow the flag
+    }
+    return T5G_OK;
+}
+
 extern "C" int t5g_engine_set_text_max(t5g_engine* e, int32_t n) {
     if (!e || n < 0 || n > e->c.max_text) return T5G_EINVAL;
     const int before = e->text_max > 0 ? e->text_max : e->c.max_text;
@@ -1718,20 +1740,37 @@ extern "C" int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void
 }
 
 // work = scores | chunk maxima (fp32)
-static void attn_work_layout(int B, int Hq, int Hkv, int cap, int64_t* sc, int64_t* mx) {
-    const int64_t nsplit = (cap + 63) / 64;
-    *sc = (int64_t)B * Hq * cap;
-    *mx = (int64_t)B * Hkv * nsplit * (Hq / Hkv);
+// work of t5g_attention_decode(_flash), in 4-byte words: scores | chunk maxima | flash
+// partials | flash chunk stats | flash tickets (last, so one zeroing covers them)
+struct AttnWork {
+    int64_t sc, mx, fp, fs, tk;
+};
+static AttnWork attn_work_layout(int B, int Hq, int Hkv, int D, int cap) {
+    const int64_t nsplit = (cap + 63) / 64, G = Hq / Hkv;
+    AttnWork w;
+    w.sc = (int64_t)B * Hq * cap;
+    w.mx = (int64_t)B * Hkv * nsplit * G;
+    w.fp = (int64_t)B * Hkv * nsplit * G * D;
+    w.fs = (int64_t)B * Hkv * nsplit * G * 2;
+    w.tk = (int64_t)B * Hkv;
+    return w;
 }
 
 extern "C" int64_t t5g_attention_decode_work_bytes(int32_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t cap) {
     if (B <= 0 || Hkv <= 0 || Hq % Hkv || D <= 0 || cap <= 0) return -1;
-    int64_t s, m;
-    attn_work_layout(B, Hq, Hkv, cap, &s, &m);
-    return (s + m) * 4;
+    const AttnWork w = attn_work_layout(B, Hq, Hkv, D, cap);
+    return (w.sc + w.mx + w.fp + w.fs + w.tk) * 4;
 }
 
+static int attention_decode_abi(const t5g_attn_decode_args* g, bool flash, void* stream);
 extern "C" int t5g_attention_decode(const t5g_attn_decode_args* g, void* stream) {
+    return attention_decode_abi(g, false, stream);
+}
+extern "C" int t5g_attention_decode_flash(const t5g_attn_decode_args* g, void* stream) {
+    return attention_decode_abi(g, true, stream);
+}
+
+static int attention_decode_abi(const t5g_attn_decode_args* g, bool flash, void* stream) {
     if (!g || !g->q || !g->k_cache || !g->v_cache || !g->kv_len || !g->out || !g->work) return T5G_EINVAL;
     if (g->B <= 0 || g->n_kv_heads <= 0 || g->n_heads % g->n_kv_heads || g->cap <= 0 || g->cap > 4096)
         return T5G_EINVAL;
@@ -1756,10 +1795,13 @@ extern "C" int t5g_attention_decode(const t5g_attn_decode_args* g, void* stream)
     a.chunk = 64;
     a.nsplit = (g->cap + 63) / 64;
     a.kv_cap = g->cap;
-    int64_t ns, nm;
-    attn_work_layout(g->B, g->n_heads, g->n_kv_heads, g->cap, &ns, &nm);
+    const AttnWork w = attn_work_layout(g->B, g->n_heads, g->n_kv_heads, g->head_dim, g->cap);
     a.sbuf = (float*)g->work;
-    a.mbuf = a.sbuf + ns;
+    a.mbuf = a.sbuf + w.sc;
+    a.flash = flash ? 1 : 0;
+    a.fpart = a.mbuf + w.mx;
+    a.fstat = a.fpart + w.fp;
+    a.fticket = (unsigned*)(a.fstat + w.fs);
     RC(attention_decode(a, (hipStream_t)stream));
     return T5G_OK;
 }

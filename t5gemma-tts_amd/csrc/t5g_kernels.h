@@ -207,6 +207,13 @@ struct AttnArgs {
     int append, k_col0, v_col0;
     int dbg_seq;             // diagnostic timeline slot (T5G_DBG_TS builds only)
     int head_split;          // set by the decode launcher: q heads run one per workgroup
+    // flash form (fast path): rows of > 64 keys in ONE launch -- each 64-key chunk's
+    // workgroup writes its online-softmax partial (max, sum, unnormalised P.V), the last to
+    // arrive for a (row, kv head) combines them. Tickets start (and are left) at zero.
+    int flash;
+    float* fpart;            // [Mq][Hkv][nsplit][G][D]
+    float* fstat;            // [Mq][Hkv][nsplit][G][2] (chunk max, chunk sum)
+    unsigned* fticket;       // [Mq][Hkv]
 };
 int attention(const AttnArgs& a, hipStream_t st);
 // decode-shaped (64-key chunks over blockIdx.z + one P.V / combine launch, sdpa numerics)

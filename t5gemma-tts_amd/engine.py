@@ -220,6 +220,12 @@ class T5GemmaTTSEngine:
         (csrc/fused.hip)."""
         _lib.check(self.L.t5g_engine_set_fused(self.h, 1 if enable else 0), "set_fused")
 
+    def set_attn_flash(self, enable: bool) -> None:
+        """Fast-path decode self attention as one split-key launch with an online-softmax
+        combine (default) or as the two-launch aten-order form (scores, then P.V / combine);
+        parity mode is unaffected (csrc/attn.hip)."""
+        _lib.check(self.L.t5g_engine_set_attn_flash(self.h, 1 if enable else 0), "set_attn_flash")
+
     def close(self):
         if getattr(self, "h", None):
             self.L.t5g_engine_destroy(self.h)

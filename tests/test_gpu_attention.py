@@ -43,7 +43,7 @@ def _exact(q, K, V, lens, scale):
     return out
 
 
-def _run(L, B, lens, Hq=8, Hkv=4, D=256, causal=1, seed=0):
+def _run(L, B, lens, Hq=8, Hkv=4, D=256, causal=1, seed=0, flash=False):
     from t5gemma_tts_amd import _lib
     lib = _lib.lib()
     g = torch.Generator().manual_seed(seed)
@@ -57,14 +57,18 @@ def _run(L, B, lens, Hq=8, Hkv=4, D=256, causal=1, seed=0):
     out = torch.zeros(B, Hq * D, dtype=BF16, device=dev)
     nb = lib.t5g_attention_decode_work_bytes(B, Hq, Hkv, D, cap)
     assert nb > 0
-    work = torch.empty(nb // 4, dtype=torch.float32, device=dev)
+    work = torch.zeros(nb // 4, dtype=torch.float32, device=dev)   # flash: tickets start at zero
     a = _lib.AttnDecodeArgs(B=B, n_heads=Hq, n_kv_heads=Hkv, head_dim=D, q=qd.data_ptr(), k_cache=Kd.data_ptr(),
                             v_cache=Vd.data_ptr(), cap=cap, kv_len=lens_d.data_ptr(), causal=causal, window=0,
                             scale=D ** -0.5, out=out.data_ptr(), work=work.data_ptr())
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    _lib.check(lib.t5g_attention_decode(C.byref(a), st), "attention_decode")
+    fn = lib.t5g_attention_decode_flash if flash else lib.t5g_attention_decode
+    _lib.check(fn(C.byref(a), st), "attention_decode")
     torch.cuda.synchronize()
     got = out.cpu().view(B, Hq, D).double()
+    if flash:   # the tickets are left at zero for the next call
+        nt = B * Hkv
+        assert int(work[-nt:].view(torch.int32).abs().sum().item()) == 0
     return got, q, K, V
 
 
@@ -117,3 +121,29 @@ def test_cross_attention_decode_tx60():
     same = (got == ref).float().mean().item()
     print(f"cross T_x=60: bit-equal to CPU SDPA {same:.5f}")
     assert same >= 0.998, same
+
+
+@pytest.mark.parametrize("L,B", [(65, 8), (152, 8), (527, 8), (903, 8), (2100, 8), (527, 32)])
+def test_self_attention_decode_flash(L, B):
+    """The fast path's one-launch form (t5g_attention_decode_flash: per-chunk online-softmax
+    partials, combined by the last chunk to arrive) against exact fp64 attention over the
+    same bf16 inputs. Rows of <= 64 keys take the aten-order kernel (bit-equal to CPU SDPA).
+    Tolerance: 2^-7 relative to max |exact| per output (fast-mode numerics: bf16 p, fp32
+    sums in a different order, bf16 output), and a mean error no larger than 1.5x that of
+    the aten-order form on the same inputs."""
+    _need_gpu()
+    lens = [max(1, L - (L // B) * i) for i in range(B)]
+    lens[1] = 1
+    lens[2] = min(L, 64)
+    got, q, K, V = _run(L, B, lens, seed=L + B, flash=True)
+    base, _, _, _ = _run(L, B, lens, seed=L + B, flash=False)
+    exact = _exact(q, K, V, lens, 256 ** -0.5)
+    err = (got - exact).abs()
+    err_base = (base - exact).abs()
+    print(f"flash L<={L} B={B}: max |err| {err.max().item():.3g} (aten-order {err_base.max().item():.3g}), "
+          f"mean {err.mean().item():.3g} ({err_base.mean().item():.3g})")
+    assert err.max().item() <= 2.0 ** -7 * max(1.0, exact.abs().max().item())
+    assert err.mean().item() <= 1.5 * err_base.mean().item() + 1e-6
+    # rows of <= 64 keys: the same kernel path as the aten-order form, bit-equal
+    small = [b for b in range(B) if lens[b] <= 64]
+    assert torch.equal(got[small], base[small])
