@@ -441,6 +441,7 @@ struct XattnFuse {
     const bf16_t* kv_new = nullptr;
     int ld_new = 0, k_col0 = 0, v_col0 = 0;
     int ldq = 0;   // row stride of Q when it is not q_dim (the q | k | v buffer)
+    int span_max = 0;   // host bound on every row's keys (0: cap)
 };
 static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const int* q_pos, const int* q_len,
                  const bf16_t* K, const bf16_t* Vc, int cap, const int* kv_len, int causal, int window, bf16_t* O,
@@ -474,6 +475,7 @@ static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const
     a.ld_new = fr.ld_new;
     a.k_col0 = fr.k_col0;
     a.v_col0 = fr.v_col0;
+    a.span_max = fr.span_max;
     // decode rows (one query each): the scores + P.V launches of xattn.hip
     if (!q_pos && !q_len) {
         const int rc = exact_attention_decode(a, e->asbuf, e->ambuf, cap, st);
@@ -683,6 +685,7 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         if (fuse) {   // q RoPE inside the scores launch
             XattnFuse fr;
             fr.rope_tab = e->rope_tab;
+            fr.span_max = e->text_max;   // the call's longest text (host hint): <= 64 keys -> one launch
             RC(xattn(e, q, M, tok_row, tok_t, qlen, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, att16, st,
                      fr));
         } else {

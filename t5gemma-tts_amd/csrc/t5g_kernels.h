@@ -303,6 +303,8 @@ struct ExactAttnArgs {
     const bf16_t* kv_new;     // non-null: the step's un-rotated key / value rows of row r at
     int ld_new, k_col0, v_col0;   // kv_new[r * ld_new + k_col0 / v_col0 + head * D]: rotated,
                                   // appended at slot kv_len[row] - 1 of K / V (written) and used
+    int span_max;             // decode: no row attends to more keys (0: cap); <= 64 without
+                              // kv_new runs the one-launch form (xattn_single_kernel)
 };
 int exact_attention(const ExactAttnArgs& a, hipStream_t st);
 // decode (one query per row, at its last key): scores + P.V launches (xattn.hip) on the

@@ -274,11 +274,158 @@ __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const fl
     }
 }
 
+// Rows of one 64-key chunk (cap <= 64: the PM cross attention over the text keys) in ONE
+// launch: workgroup (row, kv head, 32-dimension slice) recomputes the row's <= 64 scores
+// itself -- the scores kernel's code, four threads per key; the slices of a row share an
+// XCD (blockIdx.x = row fastest), so the K rows come from its L2 -- then runs the P.V
+// kernel's one-block path on them from LDS. The same operations in the same order as the
+// two launches (the chunk max is the block's running max; a 64-entry block-sum buffer adds
+// the same terms as the 512-entry one, the rest being +0), so the output is bit-identical.
+template <int G, int XD_D, bool FUSE>
+__global__ __launch_bounds__(256) void xattn_single_kernel(ExactAttnArgs a) {
+    constexpr int NCB = XD_D / 32, H2 = XD_D / 2;
+    constexpr int DP = XD_DZ / 2;                // dimension pairs per workgroup (16)
+    constexpr int NG8 = XD_CH / 8;               // 8-key groups of the chunk
+    __shared__ float qs[G][XD_D];
+    __shared__ float wmax[4][G];
+    __shared__ float ss[G][XD_CH];
+    __shared__ float pex[G][XD_CH + 16];
+    __shared__ float pbf[G][XD_CH];
+    __shared__ float tmp[NG8][G][XD_DZ];
+    __shared__ float l_s[G];
+    const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6, kl = tid >> 2, qa = tid & 3;
+    const int row = a.q_row ? a.q_row[qi] : qi;
+    int lo, hi;
+    xd_range(a, row, lo, hi);
+    const int span = hi - lo;
+    if (span <= 0) return;
+    const int key = lo + kl;
+    const bool valid = key < hi;
+    const bf16_t* kr = a.K + row * a.kv_bstride + kvh * a.kv_hstride + (long)(valid ? key : lo) * XD_D + 8 * qa;
+    u32x4 kv[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) kv[cb] = *(const u32x4*)(kr + 32 * cb);
+    // the V words of this lane's 8-key group (lanes of groups past the chunk: none)
+    const int dp = tid % DP, gl = tid / DP;
+    const bool vlane = gl < NG8;
+    const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride + (long)lo * XD_D + z * XD_DZ;
+    uint32_t vw[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        vw[j] = *(const uint32_t*)(Vb + (long)min(vlane ? gl * 8 + j : 0, span - 1) * XD_D + 2 * dp);
+    if constexpr (FUSE) {
+        const float* tab = a.rope_tab + (long)row * XD_D;
+        for (int i = tid; i < G * H2; i += 256) {
+            const int g = i / H2, d = i % H2;
+            const bf16_t* qh = a.Q + (long)qi * a.ldq + (kvh * G + g) * XD_D;
+            float o1, o2;
+            xd_rope(bf2f(qh[d]), bf2f(qh[d + H2]), tab[d], tab[H2 + d], o1, o2);
+            qs[g][d] = o1;
+            qs[g][d + H2] = o2;
+        }
+    } else {
+        for (int i = tid; i < G * XD_D / 2; i += 256) {
+            const int g = i / (XD_D / 2), p = i % (XD_D / 2);
+            const uint32_t w = *(const uint32_t*)(a.Q + (long)qi * a.ldq + (kvh * G + g) * XD_D + 2 * p);
+            qs[g][2 * p] = bf_lo(w);
+            qs[g][2 * p + 1] = bf_hi(w);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+            const float* qc = &qs[g][cb * 32 + 8 * qa];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t kw = kv[cb][i];
+                acc[i] = fmaf(qc[2 * i + 1], bf_hi(kw), acc[i]);
+                acc[i] = fmaf(qc[2 * i], bf_lo(kw), acc[i]);
+            }
+        }
+        float v8[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v8[i] = __fadd_rn(acc[i], xlane<2>(acc[i]));
+        const float va = __fadd_rn(__fadd_rn(v8[0], v8[1]), __fadd_rn(v8[2], v8[3]));
+        const float sc = __fmul_rn(__fadd_rn(va, xlane<1>(va)), a.scale);
+        const bool own = valid && qa == 0;
+        const float sv = own ? sc : -INFINITY;
+        if (own) ss[g][kl] = sv;
+        const float mx = wave_max(sv);
+        if (lane == 0) wmax[wave][g] = mx;
+    }
+    __syncthreads();
+    // exact p of the block (= the chunk) against its max
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const float mb = fmaxf(fmaxf(wmax[0][g], wmax[1][g]), fmaxf(wmax[2][g], wmax[3][g]));
+        if (tid < XD_CH) {
+            const float p = tid < span ? sdpa_p(__fsub_rn(ss[g][tid], mb), tid, span) : 0.f;
+            pex[g][tid] = p;
+            pbf[g][tid] = rbf(p);
+        } else if (tid < XD_CH + 16) {
+            pex[g][tid] = 0.f;
+        }
+    }
+    __syncthreads();
+    if (wave < G) {
+        const int g = wave;
+        const float mb = fmaxf(fmaxf(wmax[0][g], wmax[1][g]), fmaxf(wmax[2][g], wmax[3][g]));
+        const float ts = sdpa_block_sum_lds<XD_CH>(pex[g], span, lane);
+        const float l = fmaf(sdpa_block_rescale(-INFINITY, mb), 0.f, ts);
+        if (lane == 0) l_s[g] = l;
+    }
+    const int ngrp = (span + 7) / 8;
+    if (vlane && gl < ngrp) {
+        const int k0 = gl * 8, cn = min(8, span - k0);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+                if (j < cn) {
+                    if (j + 1 < cn) {
+                        const float p1 = pbf[g][k0 + j + 1];
+                        t0 = fmaf(p1, bf_lo(vw[j + 1]), t0);
+                        t1 = fmaf(p1, bf_hi(vw[j + 1]), t1);
+                    }
+                    const float p0 = pbf[g][k0 + j];
+                    t0 = fmaf(p0, bf_lo(vw[j]), t0);
+                    t1 = fmaf(p0, bf_hi(vw[j]), t1);
+                }
+            }
+            tmp[gl][g][2 * dp] = t0;
+            tmp[gl][g][2 * dp + 1] = t1;
+        }
+    }
+    __syncthreads();
+    if (tid < G * XD_DZ) {
+        const int fg = tid / XD_DZ, fd = tid % XD_DZ;
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < NG8; ++u)
+            if (u < ngrp) acc = __fadd_rn(acc, tmp[u][fg][fd]);
+        const int col = (kvh * G + fg) * XD_D + z * XD_DZ + fd;
+        const bf16_t o = f2bf(__fmul_rn(acc, __fdiv_rn(1.0f, l_s[fg])));
+        a.O[(long)qi * a.ldo + col] = o;
+        if (a.O16) a.O16[x16_off(qi, col, a.ldo / 32)] = o;
+    }
+}
+
 // decode attention (one query per row, gemv numerics) on the scores scratch sbuf
 // [Mq][Hq][cap] and chunk maxima mbuf [Mq][Hkv][nsplit][G]
 template <int G, int D>
 static void launch_xd(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, int nsplit, hipStream_t st) {
     const dim3 gs((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)nsplit), gp((unsigned)a.Mq, (unsigned)a.Hkv, D / XD_DZ);
+    const int span_max = a.span_max > 0 ? min(a.span_max, cap) : cap;
+    if (span_max <= XD_CH && !a.kv_new) {   // one chunk per row, nothing appended: one launch
+        if (a.rope_tab) hipLaunchKernelGGL((xattn_single_kernel<G, D, true>), gp, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((xattn_single_kernel<G, D, false>), gp, dim3(256), 0, st, a);
+        return;
+    }
     if (a.rope_tab) hipLaunchKernelGGL((xattn_scores_kernel<G, D, true>), gs, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
     else hipLaunchKernelGGL((xattn_scores_kernel<G, D, false>), gs, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
     hipLaunchKernelGGL((xattn_pv_kernel<G, D>), gp, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
