@@ -421,6 +421,10 @@ if __name__ == "__main__":
     if "tiny_eager" in todo:
         gen_model_golden(RT, "tiny", {"attn_implementation": "eager"}, seed=8, n_cases=4,
                          out="golden_tiny_eager")
+    if "tiny_s8_sdpa" in todo:
+        # golden_tiny_eager's weights (seed 8) under sdpa attention: the export-loading test's
+        # token-exact target (parity mode covers the sdpa path; eager runs the fast kernels)
+        gen_model_golden(RT, "tiny", {}, seed=8, n_cases=4, out="golden_tiny_s8_sdpa")
     if "tiny_window" in todo:
         gen_model_golden(RT, "tiny", {"sliding_window": 8}, seed=9, n_cases=4, out="golden_tiny_window")
     if "full" in todo:
