@@ -22,6 +22,15 @@ restates them; products of two bf16 values are exact in fp32.
   the head dim; P.V over 32-key chunks + tail, or, when aten packs, chunks of the largest
   even divisor <= 32 of the even-padded block length); later kv blocks accumulate onto the
   rescaled output. Softmax pieces from ``oracle.sdpa_emu``.
+* eager attention pieces (the reference default attn_implementation, [tf]
+  modeling_t5gemma.py:199-230; the full restatement is not done yet):
+  ``softmax_lastdim`` = nn.functional.softmax(x_bf16, -1, dtype=float32) on this host
+  (aten's AVX-512 float path: Sleef expf_u10 on every element, reduce_all with one 16-lane
+  accumulator and a zero-filled partial tail, halves tree, x * (1 / sum)); ``matmul_m1_pv``
+  = torch.matmul of one bf16 probability row with a bf16 V, per its three measured regimes
+  (K <= 16: 4 interleaved accumulators, remainder into the first, folded in order;
+  17 <= K < 64: one VDPBF16PS pair chain, odd product first; K >= 64: the E/O 32-element
+  chunks with no K split).
 """
 from __future__ import annotations
 
@@ -292,3 +301,88 @@ def uninstall(oracle_module) -> None:
     if saved is not None:
         O.T5GemmaTTSOracle._lin, O.rms_norm, O.attention = saved
         O._cpu_order_saved = None
+
+
+# ------------------------------------------------------------------------- eager pieces
+_R_LN2 = f32(1.442695040888963407359924681001892137426645954152985934135449406931)
+_L2U, _L2L = f32(0.693145751953125), f32(1.428606765330187045e-06)
+_EXPC = [f32(x) for x in (0.000198527617612853646278381, 0.00139304355252534151077271, 0.00833336077630519866943359,
+                          0.0416664853692054748535156, 0.166666671633720397949219, 0.5)]
+
+
+def _fma32(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """fp32 fused multiply-add: the double product of two fp32 values is exact."""
+    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(f32)
+
+
+def sleef_expf(d: np.ndarray) -> np.ndarray:
+    """Sleef_expf16_u10 (sleefsimdsp.c xexpf; aten Vectorized<float>::exp,
+    ATen/cpu/vec/vec512/vec512_float.h:307) for arguments <= 0 (softmax's x - max)."""
+    d = np.asarray(d, f32)
+    q = np.rint((d * _R_LN2).astype(f32)).astype(np.int32)
+    qf = q.astype(f32)
+    s = _fma32(qf, np.full_like(d, -_L2U), d)
+    s = _fma32(qf, np.full_like(d, -_L2L), s)
+    u = np.full_like(d, _EXPC[0])
+    for c in _EXPC[1:]:
+        u = _fma32(u, s, np.full_like(d, c))
+    u = (f32(1.0) + _fma32((s * s).astype(f32), u, s)).astype(f32)
+    e1 = q >> 1
+    u = (u * np.exp2(e1).astype(f32)).astype(f32)
+    u = (u * np.exp2(q - e1).astype(f32)).astype(f32)
+    return np.where(d < -104, f32(0), u).astype(f32)
+
+
+def _reduce_all16(x: np.ndarray) -> np.ndarray:
+    """aten vec::reduce_all<float>(+) over the last dim of x [R, n], 16-lane vectors."""
+    R, n = x.shape
+    if n < 16:
+        acc = x[:, 0].copy()
+        for i in range(1, n):
+            acc = (acc + x[:, i]).astype(f32)
+        return acc
+    acc = x[:, :16].copy()
+    d = 16
+    while d < n - (n % 16):
+        acc = (acc + x[:, d:d + 16]).astype(f32)
+        d += 16
+    if n - d > 0:
+        acc[:, :n - d] = (acc[:, :n - d] + x[:, d:]).astype(f32)
+    w = 16
+    while w > 1:
+        w //= 2
+        acc = (acc[:, :w] + acc[:, w:2 * w]).astype(f32)
+    return acc[:, 0]
+
+
+def softmax_lastdim(x: torch.Tensor) -> torch.Tensor:
+    """nn.functional.softmax(x, dim=-1, dtype=torch.float32) for a bf16 x, as the reference
+    host computes it (tests/test_cpu_order_cpu.py pins it bitwise)."""
+    sh = x.shape
+    xf = x.float().reshape(-1, sh[-1]).numpy()
+    e = sleef_expf((xf - xf.max(-1, keepdims=True)).astype(f32))
+    inv = (f32(1.0) / _reduce_all16(e)).astype(f32)
+    return torch.from_numpy((e * inv[:, None]).astype(f32)).reshape(sh)
+
+
+def matmul_m1_pv(p: np.ndarray, v: np.ndarray) -> np.ndarray:
+    """torch.matmul of one bf16 row p [K] with a bf16 v [K, N] (fp32 values) -> unrounded
+    fp32 [N], in the reference host's order for that K (three measured regimes)."""
+    K, N = v.shape
+    P = (p[:, None] * v).astype(f32)
+    if K >= 64:
+        return eo_chunk_matmul(p[None, :].astype(f32), v.astype(f32))[0]
+    if K >= 17:
+        acc = np.zeros(N, f32)
+        for k in range(0, K, 2):
+            if k + 1 < K:
+                acc = (acc + P[k + 1]).astype(f32)
+            acc = (acc + P[k]).astype(f32)
+        return acc
+    a = np.zeros((4, N), f32)
+    main = K - K % 4
+    for k in range(main):
+        a[k % 4] = (a[k % 4] + P[k]).astype(f32)
+    for k in range(main, K):
+        a[0] = (a[0] + P[k]).astype(f32)
+    return (((a[0] + a[1]).astype(f32) + a[2]).astype(f32) + a[3]).astype(f32)

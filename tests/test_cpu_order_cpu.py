@@ -246,3 +246,38 @@ def test_rope_trig_matches_reference_host(rope_lib):
     c0, s0 = _rope_eval(rope_lib, ang, None)
     differ = set(ang[(c0 != rc) | (s0 != rs)].view(np.uint32).tolist())
     assert differ <= set(exc[:, 0].tolist()) and len(differ) > 0
+
+
+def test_eager_softmax_restatement_bitwise():
+    """oracle.cpu_order.softmax_lastdim == nn.functional.softmax(bf16, -1, dtype=float32) on
+    this host, bit for bit, at lengths 1 ... 903 (the eager attention's softmax, [tf]
+    modeling_t5gemma.py:226)."""
+    import torch
+    from oracle import cpu_order
+    g = torch.Generator().manual_seed(3)
+    for L in (1, 5, 16, 17, 60, 64, 152, 527, 903):
+        x = (torch.randn(32, L, generator=g) * 3).to(torch.bfloat16)
+        ref = torch.softmax(x, dim=-1, dtype=torch.float32)
+        got = cpu_order.softmax_lastdim(x)
+        assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), L
+
+
+def test_eager_pv_one_row_regimes_bitwise():
+    """oracle.cpu_order.matmul_m1_pv == torch.matmul(p [1,1,1,K], v [1,1,K,256]) in bf16 on
+    this host for K in each measured regime, on absorption inputs (+-2^24 pairs whose
+    survivors reveal the summation order)."""
+    import numpy as np
+    import torch
+    from oracle import cpu_order
+    rng = np.random.default_rng(5)
+    for K in (4, 7, 13, 16, 17, 33, 60, 63, 64, 100):
+        p = rng.integers(1, 4, size=K).astype(np.float32)
+        v = rng.integers(0, 4, size=(K, 256)).astype(np.float32)
+        for n in range(256):
+            i, j = rng.choice(K, 2, replace=False)
+            v[i, n], v[j, n] = 2.0 ** 24, -2.0 ** 24
+            p[i] = p[j] = 1.0
+        pt, vt = torch.from_numpy(p).to(torch.bfloat16), torch.from_numpy(v).to(torch.bfloat16)
+        ref = torch.matmul(pt.view(1, 1, 1, K), vt.view(1, 1, K, 256)).view(256)
+        got = torch.from_numpy(cpu_order.matmul_m1_pv(pt.float().numpy(), vt.float().numpy())).to(torch.bfloat16)
+        assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), K
