@@ -318,7 +318,8 @@ def _fma32(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
 def sleef_expf(d: np.ndarray) -> np.ndarray:
     """Sleef_expf16_u10 (sleefsimdsp.c xexpf; aten Vectorized<float>::exp,
     ATen/cpu/vec/vec512/vec512_float.h:307) for arguments <= 0 (softmax's x - max)."""
-    d = np.asarray(d, f32)
+    d0 = np.asarray(d, f32)
+    d = np.maximum(d0, f32(-110.0))   # below -104 the result is 0 (selected at the end)
     q = np.rint((d * _R_LN2).astype(f32)).astype(np.int32)
     qf = q.astype(f32)
     s = _fma32(qf, np.full_like(d, -_L2U), d)
@@ -330,7 +331,7 @@ def sleef_expf(d: np.ndarray) -> np.ndarray:
     e1 = q >> 1
     u = (u * np.exp2(e1).astype(f32)).astype(f32)
     u = (u * np.exp2(q - e1).astype(f32)).astype(f32)
-    return np.where(d < -104, f32(0), u).astype(f32)
+    return np.where(d0 < -104, f32(0), u).astype(f32)
 
 
 def _reduce_all16(x: np.ndarray) -> np.ndarray:
@@ -386,3 +387,113 @@ def matmul_m1_pv(p: np.ndarray, v: np.ndarray) -> np.ndarray:
     for k in range(main, K):
         a[0] = (a[0] + P[k]).astype(f32)
     return (((a[0] + a[1]).astype(f32) + a[2]).astype(f32) + a[3]).astype(f32)
+
+
+def _eo32_b(A: np.ndarray, B: np.ndarray) -> np.ndarray:
+    """eo_chunk_matmul batched over heads: A [H, M, K], B [H, K, N] -> [H, M, N]."""
+    H, M, K = A.shape
+    N = B.shape[2]
+    tot = None
+    for c in range(0, K, 32):
+        n = min(32, K - c)
+        e = (A[:, :, c, None] * B[:, None, c, :]).astype(f32)
+        o = (A[:, :, c + 1, None] * B[:, None, c + 1, :]).astype(f32) if n > 1 else np.zeros((H, M, N), f32)
+        for t in range(2, n):
+            pr = (A[:, :, c + t, None] * B[:, None, c + t, :]).astype(f32)
+            if t % 2 == 0:
+                e = (e + pr).astype(f32)
+            else:
+                o = (o + pr).astype(f32)
+        sm = (e + o).astype(f32)
+        tot = sm if tot is None else (tot + sm).astype(f32)
+    return tot
+
+
+def _pair_b(A: np.ndarray, B: np.ndarray) -> np.ndarray:
+    """one VDPBF16PS pair chain per output (odd product first), batched: [H,M,K] x [H,K,N]."""
+    H, M, K = A.shape
+    acc = np.zeros((H, M, B.shape[2]), f32)
+    for k in range(0, K, 2):
+        if k + 1 < K:
+            acc = (acc + (A[:, :, k + 1, None] * B[:, None, k + 1, :]).astype(f32)).astype(f32)
+        acc = (acc + (A[:, :, k, None] * B[:, None, k, :]).astype(f32)).astype(f32)
+    return acc
+
+
+def _u4_b(A: np.ndarray, B: np.ndarray) -> np.ndarray:
+    """4 interleaved accumulators (remainder into the first), folded in order; batched."""
+    H, M, K = A.shape
+    a = np.zeros((4, H, M, B.shape[2]), f32)
+    main = K - K % 4
+    for k in range(K):
+        u = k % 4 if k < main else 0
+        a[u] = (a[u] + (A[:, :, k, None] * B[:, None, k, :]).astype(f32)).astype(f32)
+    return (((a[0] + a[1]).astype(f32) + a[2]).astype(f32) + a[3]).astype(f32)
+
+
+def eager_matmul(A: np.ndarray, B: np.ndarray, op: str) -> np.ndarray:
+    """torch.matmul of the eager attention's bf16 [1, 8, M, K] x [1, 8, K, N] on the reference
+    host (the 2b-2b call: batch 1, 8 query heads, head_dim 256), with the accumulation model
+    oneDNN selects for that shape (tools/cpu_order/probe_eager_table.py ->
+    eager_table_2b2b.jsonl): q.k^T ('qk') 4 accumulators when M * N == 2 else the E/O
+    32-element chunks; P.V ('pv') the pair chain when M * K < 64 and (M == 1 or K even), else
+    the E/O chunks. No K split at any probed size."""
+    H, M, K = A.shape
+    N = B.shape[2]
+    if op == "qk":
+        return _u4_b(A, B) if M * N == 2 else _eo32_b(A, B)
+    if M * K < 64 and (M == 1 or K % 2 == 0):
+        return _pair_b(A, B)
+    return _eo32_b(A, B)
+
+
+def _bf(x: np.ndarray) -> np.ndarray:
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=f32)).to(BF16).float().numpy()
+
+
+def eager_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, softcap: float,
+                    mask: Optional[torch.Tensor]) -> torch.Tensor:
+    """[tf] eager_attention_forward (:199-230) for one call of the reference (q [H, Tq, D],
+    k / v [H, Tk, D] bf16 with the GQA heads already repeated; mask bool [Tq, Tk], True =
+    attend, or None): q.k^T, x scale, / softcap -> tanh -> x softcap, + finfo.min where
+    masked, fp32 softmax -> bf16, P.V -- every bf16 tensor op an fp32 operation rounded
+    once (checked over all bf16 inputs for / 50, x 50 and tanh), the matmuls and the softmax
+    in the orders above. Returns [H, Tq, D] bf16."""
+    qf, kf, vf = q.float().numpy(), k.float().numpy(), v.float().numpy()
+    w = _bf(eager_matmul(qf, np.ascontiguousarray(kf.transpose(0, 2, 1)), "qk"))
+    w = _bf(w * f32(scale))
+    if softcap:
+        w = _bf(w / f32(softcap))
+        w = torch.tanh(torch.from_numpy(w).to(torch.float64)).to(BF16).float().numpy()
+        w = _bf(w * f32(softcap))
+    if mask is not None:
+        add = np.where(mask.numpy(), f32(0), f32(torch.finfo(BF16).min)).astype(f32)
+        w = _bf(w + add[None])
+    p = softmax_lastdim(torch.from_numpy(w).to(BF16)).to(BF16).float().numpy()
+    o = eager_matmul(p, vf, "pv")
+    return torch.from_numpy(o).to(BF16)
+
+
+def install_eager_attention(oracle_module) -> None:
+    """Route only the oracle's eager attention through ``eager_attention`` (its Linears and
+    norms stay torch's -- the reference's own ops on this host); ``uninstall`` undoes it."""
+    O = oracle_module
+    if getattr(O, "_cpu_order_saved", None) is None:
+        O._cpu_order_saved = (O.T5GemmaTTSOracle._lin, O.rms_norm, O.attention)
+    base = O._cpu_order_saved[2]
+
+    def _attention(q, k, v, *, scale, softcap, n_rep, mask, is_causal, impl):
+        if impl != "eager":
+            return base(q, k, v, scale=scale, softcap=softcap, n_rep=n_rep, mask=mask, is_causal=is_causal, impl=impl)
+        B, H, Tq, D = q.shape
+        Tk = k.shape[2]
+        k = k.repeat_interleave(n_rep, 1) if n_rep > 1 else k
+        v = v.repeat_interleave(n_rep, 1) if n_rep > 1 else v
+        if mask is None and is_causal and Tq > 1:
+            mask = (torch.arange(Tq)[:, None] + (Tk - Tq) >= torch.arange(Tk)[None, :])
+        mk = None if mask is None else mask.reshape(mask.shape[-2], mask.shape[-1])
+        outs = [eager_attention(q[b], k[b], v[b], scale, softcap, mk) for b in range(B)]
+        o = torch.stack(outs)
+        return o.transpose(1, 2).reshape(B, Tq, H * D)
+
+    O.attention = _attention

@@ -355,6 +355,22 @@ def gen_config_goldens(RT, which):
         x, y, _ = make_batch(cfg, 1, seed=20251226, T_x=16, T_p=0)[0]
         gen_cases_golden(RT, "golden_c1", [_row_case(x, y, 150, 4200, top_k=1, top_p=1.0, temperature=1.0)],
                          {"extra_cutoff": 5.0})
+    if "eager2b" in which:
+        # the reference default attn_implementation "eager" (softcap 50) on the 2b-2b model:
+        # a C3 voice-clone row, a prompt-less short text (decode from 1 key: the one-row
+        # matmul regimes) and a 7-token text with a 5-frame prompt (a 6-query prefill whose
+        # P.V takes the pair chain; odd-K cross attention)
+        kw = {"attn_implementation": "eager", "extra_cutoff": 0.5}
+        cfge = named_config("2b2b", **kw)
+        x1, y1, _ = make_batch(cfge, 1, seed=20251228, T_x=60, T_p=151)[0]
+        x2, y2, _ = make_batch(cfge, 1, seed=20251229, T_x=12, T_p=0)[0]
+        r3 = np.random.default_rng(20251230)   # 3 transcript ids, x_sep, 3 target ids; 4 codes + y_sep
+        x3 = r3.integers(3, cfge.backbone.text_vocab_size - 1, size=7).tolist()
+        x3[3] = cfge.x_sep_token
+        y3 = r3.integers(0, cfge.audio_vocab_size, size=4).tolist() + [cfge.y_sep_token]
+        gen_cases_golden(RT, "golden_2b2b_eager", [_row_case(x1, y1, len(y1) + 1, 4500),
+                                                   _row_case(x2, y2, len(y2) + 16, 4501),
+                                                   _row_case(x3, y3, len(y3) + 1, 4502)], kw)
     if "longprompt2k" in which:   # a 2 001-token prefill: the K-split table past M = 1 024
         steps = 8
         kw = {"extra_cutoff": (steps - 2) / 50.0}
@@ -431,7 +447,7 @@ if __name__ == "__main__":
         gen_full_golden(RT)
     if "long" in todo:
         gen_long_golden(RT)
-    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt", "longprompt2k")]
+    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt", "longprompt2k", "eager2b")]
     if cfg_todo:
         gen_config_goldens(RT, cfg_todo)
     if "mid" in todo:

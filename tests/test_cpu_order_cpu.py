@@ -281,3 +281,34 @@ def test_eager_pv_one_row_regimes_bitwise():
         ref = torch.matmul(pt.view(1, 1, 1, K), vt.view(1, 1, K, 256)).view(256)
         got = torch.from_numpy(cpu_order.matmul_m1_pv(pt.float().numpy(), vt.float().numpy())).to(torch.bfloat16)
         assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), K
+
+
+def test_eager_attention_restatement_reproduces_reference_full_depth():
+    """The reference default attn_implementation 'eager' (softcap 50) on the full 2b-2b model:
+    with only the attention restated (oracle.cpu_order.eager_attention: the measured oneDNN
+    matmul selection, the Sleef-exp softmax; Linears / norms stay torch's, the reference's
+    own ops on this host), the oracle reproduces golden_2b2b_eager -- a C3 voice-clone row,
+    a prompt-less short text and a 6-query prefill -- tokens and every logit row (sha)."""
+    import hashlib
+    import oracle.t5g_oracle as O
+    from oracle import cpu_order
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.weights import state_dict_digest, synthetic_weights
+    meta = json.load(open(os.path.join(GOLDEN, "golden_2b2b_eager.json")))
+    torch.set_num_threads(meta["threads"])
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    assert state_dict_digest(sd) == meta["weight_sha256"]
+    cpu_order.install_eager_attention(O)
+    try:
+        orc = O.T5GemmaTTSOracle(cfg, sd)
+        for ci, c in enumerate(meta["cases"]):
+            p = O.SamplerParams(top_k=c["top_k"], top_p=c["top_p"], min_p=c["min_p"], temperature=c["temperature"],
+                                stop_repetition=c["stop_repetition"], silence_tokens=tuple(c["silence_tokens"]))
+            out = orc.generate(c["x"], c["y"], c["tgt"], p, seed=c["seed"], record_logits=True)
+            assert out["gen"].view(-1).tolist() == c["gen"], ci
+            bits = out["logits"].contiguous().view(torch.int16).numpy()
+            shas = [hashlib.sha256(r.astype(np.int16).tobytes()).hexdigest()[:16] for r in bits]
+            assert shas == c["logit_sha"], ci
+    finally:
+        cpu_order.uninstall(O)
