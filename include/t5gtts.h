@@ -379,6 +379,20 @@ int t5g_exact_attention(const void* q_dev, int32_t Mq, const int32_t* q_row_dev,
                         const int32_t* q_len_dev, const void* k_cache_dev, const void* v_cache_dev, int32_t cap,
                         const int32_t* kv_len_dev, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
                         int32_t causal, int32_t window, float scale, int32_t threads, void* out_dev, void* stream);
+/* The same call for eager attention (attn_implementation="eager", the reference default;
+ * [tf] eager_attention_forward modeling_t5gemma.py:199-230): bf16 q.k^T, x scale, tanh
+ * softcap (tanh from tanh_lut_dev: the reference host's bf16 tanh, 65 536 entries),
+ * masked fp32 softmax, bf16 P.V, in the reference host's orders (csrc/eager.hip; restated
+ * for n_heads = 8, head_dim = 256 -- the reference model's call shape -- else
+ * T5G_EUNSUPPORTED). Replaces the eager branch of the reference's attention interface. */
+int t5g_eager_attention(const void* q_dev, int32_t Mq, const int32_t* q_row_dev, const int32_t* q_pos_dev,
+                        const int32_t* q_len_dev, const void* k_cache_dev, const void* v_cache_dev, int32_t cap,
+                        const int32_t* kv_len_dev, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
+                        int32_t causal, int32_t window, float scale, float softcap, const uint16_t* tanh_lut_dev,
+                        void* out_dev, void* stream);
+/* Parity mode for an eager-attention checkpoint: the reference host's bf16 tanh table
+ * (data/tanh_bf16.bin), required before t5g_engine_set_exact on such a config. */
+int t5g_engine_set_tanh_lut(t5g_engine* e, const uint16_t* lut_host);
 
 /* --- parity-mode noise on the device (csrc/noise.hip) --------------------------------
  * The reference's torch.multinomial draws V exponential variates per step from torch's CPU

@@ -147,6 +147,8 @@ SIGNATURES = {
     "t5g_engine_set_noise_mt": (C.c_int, [_P, _P, _I]),
     "t5g_sort_emu": (C.c_int, [_I, _I, _P, _P, _P]),
     "t5g_sort_emu_wave": (C.c_int, [_I, _I, _P, _P, _P, _P, _P]),
+    "t5g_engine_set_tanh_lut": (C.c_int, [_P, _P]),
+    "t5g_eager_attention": (C.c_int, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _F, _F, _P, _P, _P]),
 }
 
 # parity mode: the reference host's bf16 nn.GELU() (erf) table (tools/cpu_order/make_gelu_table.py)
@@ -162,7 +164,31 @@ def rope_exc_table():
     """The exception table as a uint32 numpy array [n, 2] (angle bits, cos | sin << 16)."""
     import numpy as np
     return np.fromfile(ROPE_EXC_TABLE, dtype="<u4").reshape(-1, 2)
+# parity mode, eager attention: the reference host's bf16 torch.tanh table
+# (tools/cpu_order/make_tanh_table.py) and the call shape the eager restatement was
+# measured for (oracle/cpu_order.py eager_matmul: 8 query heads of 256, batch 1)
+TANH_TABLE = os.path.join(_PKG, "data", "tanh_bf16.bin")
+EAGER_SHAPE = dict(n_heads=8, head_dim=256)
 _gelu_tab = None
+_tanh_tab = None
+
+
+def tanh_table():
+    """(ctypes uint16 array of 65 536 entries) the reference host's tanh on every bf16 input."""
+    global _tanh_tab
+    if _tanh_tab is None:
+        raw = open(TANH_TABLE, "rb").read()
+        if len(raw) != 65536 * 2:
+            raise RuntimeError(f"{TANH_TABLE}: {len(raw)} bytes, expected 131072")
+        _tanh_tab = (C.c_uint16 * 65536).from_buffer_copy(raw)
+    return _tanh_tab
+
+
+def eager_restated(bb) -> bool:
+    """Whether parity mode reproduces this backbone's eager (softcap) attention: the
+    measured call shape only (the reference's oneDNN picks its matmul kernels by shape)."""
+    return bb.softcap == 0.0 or (bb.num_attention_heads == EAGER_SHAPE["n_heads"]
+                                 and bb.head_dim == EAGER_SHAPE["head_dim"])
 
 
 def gelu_erf_table():

@@ -1,0 +1,284 @@
+// Eager attention in the reference host's CPU order (parity mode for checkpoints with
+// attn_implementation="eager", the reference default: hf_export/configuration_t5gemma_voice.py:59,
+// config.py:87). [tf] eager_attention_forward (modeling_t5gemma.py:199-230):
+//   w = bf16(q.k^T) ; w = bf16(w * scale) ; w = bf16(tanh(bf16(w / softcap)) * softcap) ;
+//   w += finfo.min where masked ; p = bf16(softmax_fp32(w)) ; o = bf16(p.V)
+// as oracle.cpu_order.eager_attention restates it (pinned bitwise on the reference's own
+// 26+26-layer eager run, tests/test_cpu_order_cpu.py):
+//   * the matmuls in the accumulation model oneDNN selects for the reference's call shape
+//     (batch 1, 8 query heads, head_dim 256; tools/cpu_order/eager_table_2b2b.jsonl):
+//     q.k^T 4 interleaved accumulators when Tq * Tk == 2, else per 32-element chunk an
+//     even and an odd fmaf chain, chunk = E + O, chunks folded in order; P.V one pair chain
+//     (odd product first) when Tq * Tk < 64 and (Tq == 1 or Tk even), else the E/O chunks
+//     over the keys -- no K split;
+//   * the softmax of aten's AVX-512 float path: Sleef expf_u10 of every (w - max), one
+//     16-lane accumulator (lane j % 16, a zero-filled partial tail) reduced by the halves
+//     tree, x * (1 / sum);
+//   * tanh from the reference host's bf16 table (data/tanh_bf16.bin).
+// Two launches: eager_scores_kernel (workgroup per (query, kv head, 64 keys): four threads
+// per key, each two 32-element chunk sums, one thread folds the eight in order) writes the
+// post-softcap scores; eager_pv_kernel (workgroup per (query, kv head, 32 output dims))
+// recomputes the row's softmax from them and runs P.V for its slice.
+#include "common.h"
+#include "t5g_kernels.h"
+
+namespace t5g {
+
+constexpr int EA_D = 256;      // head_dim of the measured call shape
+constexpr int EA_CH = 64;      // keys per scores workgroup
+constexpr int EA_DZ = 32;      // output dims per P.V workgroup
+constexpr int EA_MAXK = 6144;  // keys per call (parity mode: <= 5 001 tokens)
+
+struct EaRow {
+    int row, Tq, Tk, lo, abs_t;
+    bool has_mask, causal_mask;
+};
+
+// the call's keys and mask, exact.hip's conventions (DynamicSlidingWindowLayer trims a
+// long-enough sliding cache to its last `window` keys at decode; prefill builds the mask)
+__device__ __forceinline__ EaRow ea_row(const ExactAttnArgs& a, int qi) {
+    EaRow r;
+    r.row = a.q_row ? a.q_row[qi] : qi;
+    const int Tk_all = a.kv_len[r.row];
+    r.Tq = a.q_len ? a.q_len[r.row] : 1;
+    const int tq = a.q_pos ? a.q_pos[qi] : r.Tq - 1;
+    r.abs_t = tq + (Tk_all - r.Tq);
+    r.has_mask = a.window > 0 && Tk_all >= a.window;
+    r.lo = (r.has_mask && r.Tq == 1 && a.causal) ? Tk_all - a.window : 0;
+    r.Tk = Tk_all - r.lo;
+    r.causal_mask = a.causal && !r.has_mask && r.Tq > 1;
+    return r;
+}
+
+__device__ __forceinline__ bool ea_visible(const ExactAttnArgs& a, const EaRow& r, int key) {
+    const int kabs = key + r.lo;
+    if (r.has_mask) {
+        if (r.Tq == 1 && a.causal) return true;
+        if (a.causal) return kabs <= r.abs_t && kabs > r.abs_t - a.window;
+        return abs(r.abs_t - kabs) <= a.window;
+    }
+    return !r.causal_mask || kabs <= r.abs_t;
+}
+
+// Sleef_expf16_u10 (sleefsimdsp.c xexpf; aten Vectorized<float>::exp) for d <= 0
+__device__ __forceinline__ float ea_sleef_expf(float d) {
+    if (d < -104.f) return 0.f;
+    const float q = rintf(__fmul_rn(d, 1.442695040888963407359924681001892137426645954152985934135449406931f));
+    float s = fmaf(q, -0.693145751953125f, d);
+    s = fmaf(q, -1.428606765330187045e-06f, s);
+    float u = 0.000198527617612853646278381f;
+    u = fmaf(u, s, 0.00139304355252534151077271f);
+    u = fmaf(u, s, 0.00833336077630519866943359f);
+    u = fmaf(u, s, 0.0416664853692054748535156f);
+    u = fmaf(u, s, 0.166666671633720397949219f);
+    u = fmaf(u, s, 0.5f);
+    u = __fadd_rn(1.0f, fmaf(__fmul_rn(s, s), u, s));
+    const int qi = (int)q, e1 = qi >> 1;
+    u = __fmul_rn(u, __int_as_float((e1 + 127) << 23));
+    return __fmul_rn(u, __int_as_float((qi - e1 + 127) << 23));
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void eager_scores_kernel(ExactAttnArgs a, float* sbuf, int cap) {
+    __shared__ float qs[G][EA_D];
+    __shared__ float cs[G][EA_CH][9];   // chunk sums [head][key][chunk] (padded)
+    const int qi = blockIdx.x, kvh = blockIdx.y, ch = blockIdx.z, tid = threadIdx.x;
+    const int kl = tid >> 2, qa = tid & 3;
+    const EaRow r = ea_row(a, qi);
+    const int c0 = ch * EA_CH;
+    if (c0 >= r.Tk) return;
+    const int key = c0 + kl;
+    const bool valid = key < r.Tk;
+    const bf16_t* kb = a.K + r.row * a.kv_bstride + kvh * a.kv_hstride + (long)r.lo * EA_D;
+    // this thread's 64 dims of its key (chunks 2 qa, 2 qa + 1)
+    u32x4 kv[8];
+    const bf16_t* kr = kb + (long)(valid ? key : c0) * EA_D + 64 * qa;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kv[i] = *(const u32x4*)(kr + 8 * i);
+    for (int i = tid; i < G * EA_D; i += 256) {
+        const int g = i / EA_D, d = i % EA_D;
+        qs[g][d] = bf2f(a.Q[(long)qi * a.ldq + (kvh * G + g) * EA_D + d]);
+    }
+    __syncthreads();
+    const bool u4 = r.Tq * r.Tk == 2;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            const int c = 2 * qa + cc;
+            // chunk c = dims 32 c .. 32 c + 31 = kv[4 cc .. 4 cc + 3]; pair i of word w holds
+            // dims 32 c + 8 w' + 2 i (lo) and + 1 (hi), w' = w - 4 cc
+            float e = 0.f, o = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t kw = kv[4 * cc + w][i];
+                    const int dd = 32 * c + 8 * w + 2 * i;
+                    if (w == 0 && i == 0) {
+                        e = __fmul_rn(qs[g][dd], bf_lo(kw));
+                        o = __fmul_rn(qs[g][dd + 1], bf_hi(kw));
+                    } else {
+                        e = fmaf(qs[g][dd], bf_lo(kw), e);
+                        o = fmaf(qs[g][dd + 1], bf_hi(kw), o);
+                    }
+                }
+            cs[g][kl][c] = __fadd_rn(e, o);
+        }
+    }
+    __syncthreads();
+    if (qa != 0 || !valid) return;
+    const bool vis = ea_visible(a, r, key);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        float s;
+        if (u4) {   // 4 interleaved accumulators over the 256 dims (no remainder), in order
+            const bf16_t* kk = kb + (long)key * EA_D;
+            float ac[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int d = 0; d < EA_D; ++d) ac[d & 3] = fmaf(qs[g][d], bf2f(kk[d]), ac[d & 3]);
+            s = __fadd_rn(__fadd_rn(__fadd_rn(ac[0], ac[1]), ac[2]), ac[3]);
+        } else {
+            s = cs[g][kl][0];
+#pragma unroll
+            for (int c = 1; c < 8; ++c) s = __fadd_rn(s, cs[g][kl][c]);
+        }
+        float w = rbf(s);
+        w = rbf(__fmul_rn(w, a.scale));
+        if (a.softcap > 0.f) {
+            w = rbf(__fdiv_rn(w, a.softcap));
+            w = bf2f(a.tanh_lut[__float_as_uint(w) >> 16]);
+            w = rbf(__fmul_rn(w, a.softcap));
+        }
+        sbuf[((long)qi * a.Hq + kvh * G + g) * cap + key] = vis ? w : -INFINITY;
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void eager_pv_kernel(ExactAttnArgs a, const float* sbuf, int cap) {
+    extern __shared__ __attribute__((aligned(16))) float ea_smem[];
+    float* pb = ea_smem;                       // [G][Tk]: e, then bf16-rounded p
+    __shared__ float cs[256 / (G * EA_DZ)][G * EA_DZ];   // chunk sums of one round [chunk lane][output]
+    const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const EaRow r = ea_row(a, qi);
+    const int Tk = r.Tk;
+    if (Tk <= 0) return;
+    // ---- softmax of each head's row (wave g): max, Sleef exp, 16-lane sum, x (1 / sum)
+    if (wave < G) {
+        const int g = wave;
+        const float* sr = sbuf + ((long)qi * a.Hq + kvh * G + g) * cap;
+        float* p = pb + g * Tk;
+        float m = -INFINITY;
+        for (int j = lane; j < Tk; j += 64) m = fmaxf(m, sr[j]);
+        m = wave_max(m);
+        for (int j = lane; j < Tk; j += 64) {
+            const float w = sr[j];
+            p[j] = w == -INFINITY ? 0.f : ea_sleef_expf(__fsub_rn(w, m));
+        }
+        __builtin_amdgcn_wave_barrier();
+        float sum;
+        if (Tk < 16) {
+            sum = p[0];
+            for (int j = 1; j < Tk; ++j) sum = __fadd_rn(sum, p[j]);
+        } else {
+            const int n16 = Tk - Tk % 16;
+            float acc = 0.f;
+            if (lane < 16) {
+                acc = p[lane];
+                for (int j = 16 + lane; j < n16; j += 16) acc = __fadd_rn(acc, p[j]);
+                if (lane < Tk - n16) acc = __fadd_rn(acc, p[n16 + lane]);
+            }
+            acc = __fadd_rn(acc, xlane<8>(acc));
+            acc = __fadd_rn(acc, xlane<4>(acc));
+            acc = __fadd_rn(acc, xlane<2>(acc));
+            acc = __fadd_rn(acc, xlane<1>(acc));
+            sum = __shfl(acc, 0, 64);
+        }
+        const float inv = __fdiv_rn(1.0f, sum);
+        __builtin_amdgcn_wave_barrier();
+        for (int j = lane; j < Tk; j += 64) p[j] = rbf(__fmul_rn(p[j], inv));
+    }
+    __syncthreads();
+    // ---- P.V of this workgroup's 32 dims for the G heads
+    const int o = tid % (G * EA_DZ), cl = tid / (G * EA_DZ);   // output, chunk lane
+    constexpr int NCL = 256 / (G * EA_DZ);
+    const int g = o / EA_DZ, d = z * EA_DZ + o % EA_DZ;
+    const bf16_t* vb = a.V + r.row * a.kv_bstride + kvh * a.kv_hstride + (long)r.lo * EA_D + d;
+    const float* p = pb + g * Tk;
+    float tot = 0.f;
+    const bool pair = r.Tq * Tk < 64 && (r.Tq == 1 || Tk % 2 == 0);
+    if (pair) {
+        if (cl == 0) {
+            float acc = 0.f;
+            for (int k = 0; k < Tk; k += 2) {
+                if (k + 1 < Tk) acc = fmaf(p[k + 1], bf2f(vb[(long)(k + 1) * EA_D]), acc);
+                acc = fmaf(p[k], bf2f(vb[(long)k * EA_D]), acc);
+            }
+            tot = acc;
+        }
+    } else {
+        const int nch = (Tk + 31) / 32;
+        for (int r0 = 0; r0 < nch; r0 += NCL) {
+            const int c = r0 + cl;
+            if (c < nch) {
+                const int k0 = 32 * c, n = min(32, Tk - k0);
+                float vv[32];
+#pragma unroll
+                for (int t = 0; t < 32; ++t) vv[t] = bf2f(vb[(long)(k0 + min(t, n - 1)) * EA_D]);
+                float e = __fmul_rn(p[k0], vv[0]);
+                float od = n > 1 ? __fmul_rn(p[k0 + 1], vv[1]) : 0.f;
+#pragma unroll
+                for (int t = 2; t < 32; ++t) {
+                    if (t < n) {
+                        if (t & 1) od = fmaf(p[k0 + t], vv[t], od);
+                        else e = fmaf(p[k0 + t], vv[t], e);
+                    }
+                }
+                cs[cl][o] = __fadd_rn(e, od);
+            }
+            __syncthreads();
+            if (cl == 0) {
+                for (int u = 0; u < NCL && r0 + u < nch; ++u)
+                    tot = (r0 + u == 0) ? cs[u][o] : __fadd_rn(tot, cs[u][o]);
+            }
+            __syncthreads();
+        }
+    }
+    if (cl == 0) {
+        const int col = (kvh * G + g) * EA_D + d;
+        const bf16_t ob = f2bf(tot);
+        a.O[(long)qi * a.ldo + col] = ob;
+        if (a.O16) a.O16[x16_off(qi, col, a.ldo / 32)] = ob;
+    }
+}
+
+int eager_attention(const ExactAttnArgs& a, float* sbuf, int cap, hipStream_t st) {
+    if (a.Mq <= 0) return 0;
+    if (!a.Q || !a.K || !a.V || !a.kv_len || !a.O || !sbuf || !a.tanh_lut) return -1;
+    // the measured call shape (tools/cpu_order/eager_table_2b2b.jsonl): 8 query heads of 256
+    if (a.D != EA_D || a.Hq != 8 || a.Hq % a.Hkv || cap <= 0 || cap > EA_MAXK) return -3;
+    const int G = a.Hq / a.Hkv;
+    const dim3 gs((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)((cap + EA_CH - 1) / EA_CH));
+    const dim3 gp((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(EA_D / EA_DZ));
+    const size_t shm = (size_t)G * cap * sizeof(float);
+    if (G == 2) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
+        static bool attr[64] = {};   // function attributes are per device
+        if (!attr[dev]) {
+            (void)hipFuncSetAttribute((const void*)eager_pv_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)(2 * EA_MAXK * sizeof(float)));
+            attr[dev] = true;
+        }
+        hipLaunchKernelGGL(eager_scores_kernel<2>, gs, dim3(256), 0, st, a, sbuf, cap);
+        hipLaunchKernelGGL(eager_pv_kernel<2>, gp, dim3(256), shm, st, a, sbuf, cap);
+    } else if (G == 1) {
+        hipLaunchKernelGGL(eager_scores_kernel<1>, gs, dim3(256), 0, st, a, sbuf, cap);
+        hipLaunchKernelGGL(eager_pv_kernel<1>, gp, dim3(256), shm, st, a, sbuf, cap);
+    } else {
+        return -3;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace t5g

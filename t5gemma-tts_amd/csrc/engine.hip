@@ -113,6 +113,7 @@ struct t5g_engine {
     int exact_threads = REF_KSPLIT_THREADS;
     uint16_t* ksplit_dev = nullptr;     // ref_ksplit.h tables [REF_KSPLIT_NSHAPES][REF_KSPLIT_MAX_M]
     uint16_t* gelu_lut_dev = nullptr;   // [65536] bf16 -> bf16 nn.GELU() of the reference host
+    uint16_t* tanh_lut_dev = nullptr;   // [65536] bf16 -> bf16 torch.tanh of the reference host (eager)
     // parity mode's Linears on the f32 MFMA (xmm.hip): E16 copies of the packed weights
     // (made once, at the first t5g_engine_set_exact) and X16 activation buffers
     struct XLayer {
@@ -476,6 +477,19 @@ static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const
     a.k_col0 = fr.k_col0;
     a.v_col0 = fr.v_col0;
     a.span_max = fr.span_max;
+    if (c.softcap > 0.f) {
+        // eager attention (eager.hip): decode rows on the engine's scores scratch, packed
+        // (prefill / encoder) calls on a stream-ordered one (not inside a captured graph)
+        if (fr.rope_tab || fr.kv_new) return -1;
+        a.softcap = c.softcap;
+        a.tanh_lut = e->tanh_lut_dev;
+        if (!q_pos && !q_len) return eager_attention(a, e->asbuf, cap, st);
+        float* sb = nullptr;
+        if (hipMallocAsync((void**)&sb, (size_t)Mq * c.n_heads * cap * sizeof(float), st) != hipSuccess) return -2;
+        const int rc = eager_attention(a, sb, cap, st);
+        hipFreeAsync(sb, st);
+        return rc;
+    }
     // decode rows (one query each): the scores + P.V launches of xattn.hip
     if (!q_pos && !q_len) {
         const int rc = exact_attention_decode(a, e->asbuf, e->ambuf, cap, st);
@@ -648,7 +662,7 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         RC(xlin16(e, xn16, M, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
                   e->q_dim, e->kv_dim, e->q_dim, st));
         // decode: RoPE of q and k and the cache append happen inside the scores launch
-        const bool fuse = decode && exact_attention_decode_supported(c.n_heads / c.n_kv_heads, D);
+        const bool fuse = decode && c.softcap <= 0.f && exact_attention_decode_supported(c.n_heads / c.n_kv_heads, D);
         if (fuse) {
             XattnFuse fr;
             fr.rope_tab = e->rope_tab;
@@ -803,7 +817,10 @@ extern "C" int t5g_engine_set_exact(t5g_engine* e, int32_t enable, const uint16_
         return T5G_OK;
     }
     if (threads != REF_KSPLIT_THREADS) return T5G_EUNSUPPORTED;   // the only measured K-split table
-    if (e->c.softcap > 0.f) return T5G_EUNSUPPORTED;   // eager attention (softcap): not restated
+    // eager attention (softcap): restated for the measured call shape (8 query heads of 256,
+    // eager.hip) once the reference host's tanh table is set (t5g_engine_set_tanh_lut)
+    if (e->c.softcap > 0.f && (!e->tanh_lut_dev || e->c.head_dim != 256 || e->c.n_heads != 8))
+        return T5G_EUNSUPPORTED;
     RC(xmm_prepare(e));
     if (!e->ksplit_dev) {
         RC(alloc(e, &e->ksplit_dev, (int64_t)REF_KSPLIT_NSHAPES * REF_KSPLIT_MAX_M));
@@ -816,6 +833,13 @@ extern "C" int t5g_engine_set_exact(t5g_engine* e, int32_t enable, const uint16_
     e->exact_threads = threads;
     if (!e->exact) drop_graphs(e);
     e->exact = true;
+    return T5G_OK;
+}
+
+extern "C" int t5g_engine_set_tanh_lut(t5g_engine* e, const uint16_t* lut) {
+    if (!e || !lut) return T5G_EINVAL;
+    if (!e->tanh_lut_dev) RC(alloc(e, &e->tanh_lut_dev, 65536));
+    HIPCHK(hipMemcpy(e->tanh_lut_dev, lut, 65536 * sizeof(uint16_t), hipMemcpyHostToDevice));
     return T5G_OK;
 }
 
@@ -1983,6 +2007,47 @@ extern "C" int t5g_xmm_linear(const void* X, int32_t ldx, int32_t M, const void*
     }
     hipFreeAsync(w16, st);
     hipFreeAsync(x16, st);
+    RC(rc);
+    return T5G_OK;
+}
+
+extern "C" int t5g_eager_attention(const void* q, int32_t Mq, const int32_t* q_row, const int32_t* q_pos,
+                                   const int32_t* q_len, const void* k_cache, const void* v_cache, int32_t cap,
+                                   const int32_t* kv_len, int32_t n_heads, int32_t n_kv_heads, int32_t head_dim,
+                                   int32_t causal, int32_t window, float scale, float softcap,
+                                   const uint16_t* tanh_lut, void* out, void* stream) {
+    if (!q || !k_cache || !v_cache || !kv_len || !out || !tanh_lut || Mq <= 0 || cap <= 0 || n_kv_heads <= 0 ||
+        n_heads % n_kv_heads || head_dim <= 0)
+        return T5G_EINVAL;
+    ExactAttnArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Q = (const bf16_t*)q;
+    a.ldq = n_heads * head_dim;
+    a.Mq = Mq;
+    a.q_row = q_row;
+    a.q_pos = q_pos;
+    a.q_len = q_len;
+    a.K = (const bf16_t*)k_cache;
+    a.V = (const bf16_t*)v_cache;
+    a.kv_hstride = (long)cap * head_dim;
+    a.kv_bstride = a.kv_hstride * n_kv_heads;
+    a.kv_len = kv_len;
+    a.Hq = n_heads;
+    a.Hkv = n_kv_heads;
+    a.D = head_dim;
+    a.causal = causal;
+    a.window = window;
+    a.scale = scale;
+    a.softcap = softcap;
+    a.tanh_lut = tanh_lut;
+    a.O = (bf16_t*)out;
+    a.ldo = a.ldq;
+    hipStream_t st = (hipStream_t)stream;
+    float* sb = nullptr;
+    HIPCHK(hipMallocAsync((void**)&sb, (size_t)Mq * n_heads * cap * 4, st));
+    const int rc = eager_attention(a, sb, cap, st);
+    hipFreeAsync(sb, st);
+    if (rc == -3) return T5G_EUNSUPPORTED;
     RC(rc);
     return T5G_OK;
 }

@@ -305,12 +305,17 @@ struct ExactAttnArgs {
                                   // appended at slot kv_len[row] - 1 of K / V (written) and used
     int span_max;             // decode: no row attends to more keys (0: cap); <= 64 without
                               // kv_new runs the one-launch form (xattn_single_kernel)
+    float softcap;            // eager attention (eager.hip): > 0 the tanh logit softcap
+    const uint16_t* tanh_lut; // eager: the reference host's bf16 tanh [65536]
 };
 int exact_attention(const ExactAttnArgs& a, hipStream_t st);
 // decode (one query per row, at its last key): scores + P.V launches (xattn.hip) on the
 // scratch sbuf [Mq][Hq][cap] / mbuf [Mq][Hkv][ceil(cap / 64)][G]
 int exact_attention_decode(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, hipStream_t st);
 bool exact_attention_decode_supported(int G, int D);   // head shapes the decode launches are built for
+// eager attention (attn_implementation="eager") in the reference host's order, eager.hip:
+// scores + softmax/P.V launches on the scratch sbuf [Mq][Hq][cap]; -3: not the measured shape
+int eager_attention(const ExactAttnArgs& a, float* sbuf, int cap, hipStream_t st);
 int sort_emu_wave(int n, int S, int* pos, float* val, int* tag, int* out, hipStream_t st);   // sampler.hip test entry
 
 // ---- sampler -------------------------------------------------------------------

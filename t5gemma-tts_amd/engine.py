@@ -267,6 +267,10 @@ class T5GemmaTTSEngine:
         if bool(enable) == getattr(self, "_exact", False):
             return
         tab = _lib.gelu_erf_table() if enable else None
+        if enable and self.cfg.backbone.softcap != 0.0 and not getattr(self, "_tanh_set", False):
+            # eager attention: the reference host's bf16 tanh (csrc/eager.hip)
+            _lib.check(self.L.t5g_engine_set_tanh_lut(self.h, _lib.tanh_table()), "set_tanh_lut")
+            self._tanh_set = True
         _lib.check(self.L.t5g_engine_set_exact(self.h, 1 if enable else 0, tab, _lib.EXACT_THREADS), "set_exact")
         if enable and getattr(self, "_rope_exc", None) is None:
             self._rope_exc = np.ascontiguousarray(_lib.rope_exc_table())
@@ -291,12 +295,13 @@ class T5GemmaTTSEngine:
             raise ValueError("generators= drives the reference RNG stream: parity=True only")
         if exact is None:
             exact = parity
-        if exact and self.cfg.backbone.softcap != 0.0:
-            # the exact-order kernels restate the sdpa attention path only; an eager (softcap)
-            # checkpoint would not be reproduced bit for bit -- refuse instead of degrading
-            raise ValueError("parity mode restates the reference's sdpa attention path; this configuration uses "
-                             "eager attention with a logit softcap (attn_implementation='eager'), which is not "
-                             "restated bit for bit: run with parity=False (fast kernels, tolerance parity)")
+        if exact and not _lib.eager_restated(self.cfg.backbone):
+            # eager (softcap) attention is restated for the reference model's call shape (8
+            # query heads of 256, csrc/eager.hip); another shape would not be reproduced bit
+            # for bit -- refuse instead of degrading
+            raise ValueError("parity mode restates eager attention (attn_implementation='eager', logit softcap) "
+                             "for 8 query heads of head_dim 256 only (the reference's oneDNN picks its matmul "
+                             "kernels by shape): run with parity=False (fast kernels, tolerance parity)")
         if exact:
             for u in utts:
                 n_y = len(u.y) + 1
@@ -603,12 +608,13 @@ class T5GemmaVoiceForConditionalGeneration:
         if parity is None:
             # the drop-in default: token-exact parity where it is restated (sdpa attention);
             # an eager / softcap checkpoint runs the fast kernels, and says so once
-            parity = cfg.backbone.softcap == 0.0
+            parity = _lib.eager_restated(cfg.backbone)
             if not parity and not getattr(self, "_warned_eager", False):
                 import warnings
-                warnings.warn("eager (softcap) attention checkpoint: inference_tts runs the fast kernels "
-                              "(logits within tolerance of the reference, tokens may differ); the bit-exact "
-                              "parity mode covers the sdpa attention path")
+                warnings.warn("eager (softcap) attention checkpoint of an unmeasured shape: inference_tts runs the "
+                              "fast kernels (logits within tolerance of the reference, tokens may differ); the "
+                              "bit-exact parity mode covers sdpa attention and eager attention with 8 query heads "
+                              "of 256")
                 self._warned_eager = True
         if multi_trial:
             import warnings
