@@ -184,6 +184,9 @@ def main():
                     help="decode MLP half as three launches instead of the persistent fused launch (A/B)")
     ap.add_argument("--no-attn-flash", action="store_true",
                     help="fast path: decode self attention as the two-launch aten-order form (A/B)")
+    ap.add_argument("--attn", choices=("sdpa", "eager"), default="sdpa",
+                    help="the checkpoint's attn_implementation: eager (the reference default, tanh softcap 50) "
+                         "runs parity mode's eager.hip restatement")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo (CPU collectives; lets N ranks share one GPU "
                          "to rehearse the sharded path)")
@@ -225,7 +228,7 @@ def main():
     from t5gemma_tts_amd.engine import SamplingParams, T5GemmaTTSEngine, Utterance
     from t5gemma_tts_amd.weights import synthetic_weights
 
-    cfg = config_2b2b()
+    cfg = config_2b2b(attn_implementation=args.attn)
     B = args.batch or wl_b
     torch.manual_seed(1234)
     sd = synthetic_weights(cfg, seed=1234, device=str(dev))
@@ -431,7 +434,8 @@ def main():
                 "vs_baseline": None, "dtype": "bf16",
                 "data": "synthetic (seeded random 2b-2b weights, random text/prompt codes)",
                 "config": {"workload": f"{desc}: 2b-2b bf16, {B} utterances/GPU, T_x {wl_tx}, {prompt}, "
-                                       f"10 s target (751 tokens/utterance), {mode}",
+                                       f"10 s target (751 tokens/utterance), {mode}"
+                                       + (", eager attention (softcap 50)" if args.attn == "eager" else ""),
                            "global_batch": B * world, "seq_len": wl_tp + 1 + n_tok_row,
                            "parallelism": f"dp{world} (utterance shards)"},
                 "rtf_audio_s_per_wall_s": round(value / 50.0, 3),
