@@ -650,7 +650,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnArgs a) {
         const int jl = i * KPB + wave * KPW + kg;
         if (dl == 0) {
 #pragma unroll
-            for (int g = 0; g < G; ++g) sm[g][jl] = __fmul_rn(s[g], a.scale);
+            for (int g = 0; g < G; ++g) sm[g][jl] = fast_score(s[g], a.scale, a.softcap);
         }
     }
     __syncthreads();

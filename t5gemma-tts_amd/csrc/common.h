@@ -245,6 +245,16 @@ __device__ __forceinline__ float sdpa_block_sum_lds(const float* pl, int blen, i
     }
     return s;
 }
+// fast-path attention score from the fp32 dot product: x scale, or for an eager
+// checkpoint (softcap > 0) the reference's bf16 rounding points of eager_attention_forward
+// ([tf] modeling_t5gemma.py:216-221: bf16 q.k, x scale, / softcap, tanh, x softcap)
+__device__ __forceinline__ float fast_score(float s, float scale, float softcap) {
+    if (softcap > 0.f) {
+        const float v = rbf(rbf(s) * scale);
+        return rbf(rbf(tanhf(rbf(v / softcap))) * softcap);
+    }
+    return __fmul_rn(s, scale);
+}
 // rescale of the previous blocks' sums when the running max grows (std::expf in aten)
 __device__ __forceinline__ float sdpa_block_rescale(float m_old, float m_new) {
     return m_old == -INFINITY ? 0.f : (float)exp((double)__fsub_rn(m_old, m_new));

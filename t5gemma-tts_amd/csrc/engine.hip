@@ -972,6 +972,7 @@ static int decode_attention(t5g_engine* e, int M, const bf16_t* K, const bf16_t*
     a.causal = causal;
     a.window = window;
     a.scale = c.attn_scale;
+    a.softcap = c.softcap;   // eager checkpoints: the fast kernels apply the tanh softcap
     a.O = e->datt;
     a.ldo = e->q_dim;
     a.chunk = 64;
@@ -1048,6 +1049,7 @@ static FusedMlpArgs fused_block_args(t5g_engine* e, int M, int l) {
     fa.Hkv = c.n_kv_heads;
     fa.D = c.head_dim;
     fa.scale = c.attn_scale;
+    fa.softcap = c.softcap;
     fa.att = e->datt2;
     fa.Wo = (const bf16_t*)L.cross_o;
     fa.NGo = ng_pad(c.hidden);
@@ -1076,7 +1078,8 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
     bf16_t* att = decode ? e->datt : e->att;
     bf16_t* act = decode ? e->dact : e->act;
     bf16_t* tmp = e->tmp;
-    const bool eager = c.softcap > 0.f;
+    // eager checkpoints (softcap > 0) take the same decode launches: the attention kernels
+    // apply the tanh softcap in the score (common.h fast_score)
     // split-K factors (decode: spread the weight streams over >= 512 blocks)
     const int s_qkv = decode ? e->s_qkv : 1, s_o = decode ? e->s_o : 1, s_down = decode ? e->s_down : 1;
     // one cos/sin table per step: every layer's q/k rotation uses the same positions
@@ -1155,7 +1158,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         }
         // --- self attention
         const int win = c.dec_sliding[l] ? c.sliding_window : 0;
-        if (decode && !eager) {
+        if (decode) {
             // q|k|v as fp32 split-K slabs; q rotated, k rotated + appended inside attention.
             // At the 2b-2b width: the 12-wave register-X GEMV over 2 k-slices (the fused
             // block's QKV stage, which produced them already when qkv_done)
@@ -1194,7 +1197,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         // the rest of the layer (o-projection, cross attention, MLP half, the last norm and
         // the next layer's q|k|v) as one persistent launch (fused.hip fused_block_kernel;
         // bitwise equal to the launches below)
-        if (decode && e->fused_mlp && !eager && M <= 16 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 &&
+        if (decode && e->fused_mlp && M <= 16 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 &&
             e->q_dim == 2048 && c.n_dec_layers >= 2) {
             const FusedMlpArgs fa = fused_block_args(e, M, l);
             if (fused_mlp_check(fa) == 0) {
@@ -1206,7 +1209,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         RC(out_proj(att, L.o));
         RC(resid(s_o, L.norms[1], L.norms[2]));
         // --- PM cross attention (q rotated by the decoder progress, :149-165)
-        if (decode && !eager) {
+        if (decode) {
             // cross-q: at the 2b-2b width the register-X GEMV over 2 k-slices of 36 k-steps,
             // 12 waves (the fused block's Q stage), so a row's sums never depend on the batch
             int s_q = s_o, rcq = -1;
@@ -1236,7 +1239,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         RC(out_proj(att, L.cross_o));
         // --- norm + GeGLU MLP: at the 2b-2b width, decode rows <= 32, one persistent launch
         // (fused.hip; bitwise equal to the three launches below)
-        if (decode && e->fused_mlp && !eager && M <= 32 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 &&
+        if (decode && e->fused_mlp && M <= 32 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 &&
             c.n_dec_layers >= 2) {
             const int rc = fused_mlp(fused_args(e, M, l), st);
             if (rc == 0) {

@@ -765,7 +765,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
                 }
                 sc = xsum<LPK>(sc);
                 const int jl = i * KPB + wave * KPW + kg;
-                if (dl == 0) al.sm[jl] = __fmul_rn(sc, a.scale);
+                if (dl == 0) al.sm[jl] = fast_score(sc, a.scale, a.softcap);
             }
         }
         __syncthreads();

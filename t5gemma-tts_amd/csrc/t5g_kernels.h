@@ -89,6 +89,7 @@ struct FusedMlpArgs {
     const float* rope_tab;    // [B][D] this step's PM-RoPE cos | sin
     int q_dim, Hq, Hkv, D;
     float scale;
+    float softcap;            // eager checkpoints: the tanh logit softcap (0: none)
     bf16_t* att;              // [M][q_dim] handed off in-launch
     const bf16_t* Wo;         // packed cross o_proj, NGo row groups, K = q_dim
     int NGo;
