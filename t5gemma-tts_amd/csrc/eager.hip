@@ -156,23 +156,30 @@ __global__ __launch_bounds__(256) void eager_scores_kernel(ExactAttnArgs a, floa
 template <int G>
 __global__ __launch_bounds__(256) void eager_pv_kernel(ExactAttnArgs a, const float* sbuf, int cap) {
     extern __shared__ __attribute__((aligned(16))) float ea_smem[];
-    float* pb = ea_smem;                       // [G][Tk]: e, then bf16-rounded p
-    __shared__ float cs[256 / (G * EA_DZ)][G * EA_DZ];   // chunk sums of one round [chunk lane][output]
+    float* pb = ea_smem;                      // [G][Tk]: scores, then e, then bf16-rounded p
+    constexpr int NDP = EA_DZ / 2;            // dimension pairs of the slice (16)
+    constexpr int NCL = 256 / NDP;            // chunk lanes (16)
+    __shared__ float cs[NCL][G][EA_DZ + 1];   // chunk sums of one round [chunk lane][head][dim]
+    __shared__ uint32_t vs[64][NDP];          // pair chain (< 64 keys): the slice's V rows
     const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const EaRow r = ea_row(a, qi);
     const int Tk = r.Tk;
     if (Tk <= 0) return;
+    // ---- the G score rows into LDS in one coalesced pass
+    for (int i = tid; i < G * Tk; i += 256) {
+        const int g = i / Tk, j = i - g * Tk;
+        pb[i] = sbuf[((long)qi * a.Hq + kvh * G + g) * cap + j];
+    }
+    __syncthreads();
     // ---- softmax of each head's row (wave g): max, Sleef exp, 16-lane sum, x (1 / sum)
     if (wave < G) {
-        const int g = wave;
-        const float* sr = sbuf + ((long)qi * a.Hq + kvh * G + g) * cap;
-        float* p = pb + g * Tk;
+        float* p = pb + wave * Tk;
         float m = -INFINITY;
-        for (int j = lane; j < Tk; j += 64) m = fmaxf(m, sr[j]);
+        for (int j = lane; j < Tk; j += 64) m = fmaxf(m, p[j]);
         m = wave_max(m);
         for (int j = lane; j < Tk; j += 64) {
-            const float w = sr[j];
+            const float w = p[j];
             p[j] = w == -INFINITY ? 0.f : ea_sleef_expf(__fsub_rn(w, m));
         }
         __builtin_amdgcn_wave_barrier();
@@ -185,7 +192,16 @@ __global__ __launch_bounds__(256) void eager_pv_kernel(ExactAttnArgs a, const fl
             float acc = 0.f;
             if (lane < 16) {
                 acc = p[lane];
-                for (int j = 16 + lane; j < n16; j += 16) acc = __fadd_rn(acc, p[j]);
+                int j = 16 + lane;
+                // 8 values per LDS round trip, added in order
+                for (; j + 7 * 16 < n16; j += 8 * 16) {
+                    float t[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) t[u] = p[j + 16 * u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, t[u]);
+                }
+                for (; j < n16; j += 16) acc = __fadd_rn(acc, p[j]);
                 if (lane < Tk - n16) acc = __fadd_rn(acc, p[n16 + lane]);
             }
             acc = __fadd_rn(acc, xlane<8>(acc));
@@ -199,22 +215,46 @@ __global__ __launch_bounds__(256) void eager_pv_kernel(ExactAttnArgs a, const fl
         for (int j = lane; j < Tk; j += 64) p[j] = rbf(__fmul_rn(p[j], inv));
     }
     __syncthreads();
-    // ---- P.V of this workgroup's 32 dims for the G heads
-    const int o = tid % (G * EA_DZ), cl = tid / (G * EA_DZ);   // output, chunk lane
-    constexpr int NCL = 256 / (G * EA_DZ);
-    const int g = o / EA_DZ, d = z * EA_DZ + o % EA_DZ;
-    const bf16_t* vb = a.V + r.row * a.kv_bstride + kvh * a.kv_hstride + (long)r.lo * EA_D + d;
-    const float* p = pb + g * Tk;
-    float tot = 0.f;
+    // ---- P.V: thread (dimension pair dp, chunk lane cl) for both heads (they share V)
+    const int dp = tid % NDP, cl = tid / NDP;
+    const int d0 = z * EA_DZ + 2 * dp;
+    const bf16_t* vb = a.V + r.row * a.kv_bstride + kvh * a.kv_hstride + (long)r.lo * EA_D + d0;
     const bool pair = r.Tq * Tk < 64 && (r.Tq == 1 || Tk % 2 == 0);
+    float tot[G][2];
     if (pair) {
-        if (cl == 0) {
-            float acc = 0.f;
-            for (int k = 0; k < Tk; k += 2) {
-                if (k + 1 < Tk) acc = fmaf(p[k + 1], bf2f(vb[(long)(k + 1) * EA_D]), acc);
-                acc = fmaf(p[k], bf2f(vb[(long)k * EA_D]), acc);
+        // the slice's V rows (< 64 keys x 16 bf16 pairs) into LDS in one pass, then one
+        // chain per dimension pair reads them
+        {
+            const bf16_t* vs0 = a.V + r.row * a.kv_bstride + kvh * a.kv_hstride + (long)r.lo * EA_D + z * EA_DZ;
+            for (int i = tid; i < Tk * NDP; i += 256) {
+                const int k = i / NDP, q2 = i % NDP;
+                vs[k][q2] = *(const uint32_t*)(vs0 + (long)k * EA_D + 2 * q2);
             }
-            tot = acc;
+        }
+        __syncthreads();
+        if (cl == 0) {
+            float acc[G][2] = {};
+            for (int k = 0; k < Tk; k += 2) {
+                if (k + 1 < Tk) {
+                    const uint32_t w = vs[k + 1][dp];
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        acc[g][0] = fmaf(pb[g * Tk + k + 1], bf_lo(w), acc[g][0]);
+                        acc[g][1] = fmaf(pb[g * Tk + k + 1], bf_hi(w), acc[g][1]);
+                    }
+                }
+                const uint32_t w = vs[k][dp];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    acc[g][0] = fmaf(pb[g * Tk + k], bf_lo(w), acc[g][0]);
+                    acc[g][1] = fmaf(pb[g * Tk + k], bf_hi(w), acc[g][1]);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                tot[g][0] = acc[g][0];
+                tot[g][1] = acc[g][1];
+            }
         }
     } else {
         const int nch = (Tk + 31) / 32;
@@ -222,33 +262,57 @@ __global__ __launch_bounds__(256) void eager_pv_kernel(ExactAttnArgs a, const fl
             const int c = r0 + cl;
             if (c < nch) {
                 const int k0 = 32 * c, n = min(32, Tk - k0);
-                float vv[32];
+                uint32_t vw[32];
 #pragma unroll
-                for (int t = 0; t < 32; ++t) vv[t] = bf2f(vb[(long)(k0 + min(t, n - 1)) * EA_D]);
-                float e = __fmul_rn(p[k0], vv[0]);
-                float od = n > 1 ? __fmul_rn(p[k0 + 1], vv[1]) : 0.f;
+                for (int t = 0; t < 32; ++t) vw[t] = *(const uint32_t*)(vb + (long)(k0 + min(t, n - 1)) * EA_D);
 #pragma unroll
-                for (int t = 2; t < 32; ++t) {
-                    if (t < n) {
-                        if (t & 1) od = fmaf(p[k0 + t], vv[t], od);
-                        else e = fmaf(p[k0 + t], vv[t], e);
+                for (int g = 0; g < G; ++g) {
+                    const float* pg = pb + g * Tk + k0;
+                    float e0 = __fmul_rn(pg[0], bf_lo(vw[0])), e1 = __fmul_rn(pg[0], bf_hi(vw[0]));
+                    float o0 = 0.f, o1 = 0.f;
+                    if (n > 1) {
+                        o0 = __fmul_rn(pg[1], bf_lo(vw[1]));
+                        o1 = __fmul_rn(pg[1], bf_hi(vw[1]));
                     }
+#pragma unroll
+                    for (int t = 2; t < 32; ++t) {
+                        if (t < n) {
+                            const float pt = pg[t];
+                            if (t & 1) {
+                                o0 = fmaf(pt, bf_lo(vw[t]), o0);
+                                o1 = fmaf(pt, bf_hi(vw[t]), o1);
+                            } else {
+                                e0 = fmaf(pt, bf_lo(vw[t]), e0);
+                                e1 = fmaf(pt, bf_hi(vw[t]), e1);
+                            }
+                        }
+                    }
+                    cs[cl][g][2 * dp] = __fadd_rn(e0, o0);
+                    cs[cl][g][2 * dp + 1] = __fadd_rn(e1, o1);
                 }
-                cs[cl][o] = __fadd_rn(e, od);
             }
             __syncthreads();
             if (cl == 0) {
                 for (int u = 0; u < NCL && r0 + u < nch; ++u)
-                    tot = (r0 + u == 0) ? cs[u][o] : __fadd_rn(tot, cs[u][o]);
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+#pragma unroll
+                        for (int h = 0; h < 2; ++h)
+                            tot[g][h] = (r0 + u == 0) ? cs[u][g][2 * dp + h] : __fadd_rn(tot[g][h], cs[u][g][2 * dp + h]);
             }
             __syncthreads();
         }
     }
     if (cl == 0) {
-        const int col = (kvh * G + g) * EA_D + d;
-        const bf16_t ob = f2bf(tot);
-        a.O[(long)qi * a.ldo + col] = ob;
-        if (a.O16) a.O16[x16_off(qi, col, a.ldo / 32)] = ob;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int col = (kvh * G + g) * EA_D + d0 + h;
+                const bf16_t ob = f2bf(tot[g][h]);
+                a.O[(long)qi * a.ldo + col] = ob;
+                if (a.O16) a.O16[x16_off(qi, col, a.ldo / 32)] = ob;
+            }
     }
 }
 
