@@ -78,6 +78,63 @@ __device__ __forceinline__ float ea_sleef_expf(float d) {
     return __fmul_rn(u, __int_as_float((qi - e1 + 127) << 23));
 }
 
+// the two 32-element chunk sums (E + O chains over dims) of thread qa's quarter of key kl's
+// row, for the G heads, into cs[g][kl][2 qa], [2 qa + 1]
+template <int G>
+__device__ __forceinline__ void ea_chunk_sums(const float (&qs)[G][EA_D], const u32x4 (&kv)[8],
+                                              float (&cs)[G][EA_CH][9], int kl, int qa) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            const int c = 2 * qa + cc;
+            // chunk c = dims 32 c .. 32 c + 31 = kv[4 cc .. 4 cc + 3]; pair i of word w holds
+            // dims 32 c + 8 w + 2 i (lo) and + 1 (hi)
+            float e = 0.f, o = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t kw = kv[4 * cc + w][i];
+                    const int dd = 32 * c + 8 * w + 2 * i;
+                    if (w == 0 && i == 0) {
+                        e = __fmul_rn(qs[g][dd], bf_lo(kw));
+                        o = __fmul_rn(qs[g][dd + 1], bf_hi(kw));
+                    } else {
+                        e = fmaf(qs[g][dd], bf_lo(kw), e);
+                        o = fmaf(qs[g][dd + 1], bf_hi(kw), o);
+                    }
+                }
+            cs[g][kl][c] = __fadd_rn(e, o);
+        }
+    }
+}
+
+// key `key`'s post-softcap score for one head from its 8 chunk sums (or, when the call is
+// Tq * Tk == 2, the 4-accumulator order over the 256 dims)
+__device__ __forceinline__ float ea_score(const ExactAttnArgs& a, const EaRow& r, const float* q, const bf16_t* kb,
+                                          int key, const float* csk) {
+    float s;
+    if (r.Tq * r.Tk == 2) {
+        const bf16_t* kk = kb + (long)key * EA_D;
+        float ac[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int d = 0; d < EA_D; ++d) ac[d & 3] = fmaf(q[d], bf2f(kk[d]), ac[d & 3]);
+        s = __fadd_rn(__fadd_rn(__fadd_rn(ac[0], ac[1]), ac[2]), ac[3]);
+    } else {
+        s = csk[0];
+#pragma unroll
+        for (int c = 1; c < 8; ++c) s = __fadd_rn(s, csk[c]);
+    }
+    float w = rbf(s);
+    w = rbf(__fmul_rn(w, a.scale));
+    if (a.softcap > 0.f) {
+        w = rbf(__fdiv_rn(w, a.softcap));
+        w = bf2f(a.tanh_lut[__float_as_uint(w) >> 16]);
+        w = rbf(__fmul_rn(w, a.softcap));
+    }
+    return w;
+}
+
 template <int G>
 __global__ __launch_bounds__(256) void eager_scores_kernel(ExactAttnArgs a, float* sbuf, int cap) {
     __shared__ float qs[G][EA_D];
@@ -100,78 +157,26 @@ __global__ __launch_bounds__(256) void eager_scores_kernel(ExactAttnArgs a, floa
         qs[g][d] = bf2f(a.Q[(long)qi * a.ldq + (kvh * G + g) * EA_D + d]);
     }
     __syncthreads();
-    const bool u4 = r.Tq * r.Tk == 2;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-            const int c = 2 * qa + cc;
-            // chunk c = dims 32 c .. 32 c + 31 = kv[4 cc .. 4 cc + 3]; pair i of word w holds
-            // dims 32 c + 8 w' + 2 i (lo) and + 1 (hi), w' = w - 4 cc
-            float e = 0.f, o = 0.f;
-#pragma unroll
-            for (int w = 0; w < 4; ++w)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t kw = kv[4 * cc + w][i];
-                    const int dd = 32 * c + 8 * w + 2 * i;
-                    if (w == 0 && i == 0) {
-                        e = __fmul_rn(qs[g][dd], bf_lo(kw));
-                        o = __fmul_rn(qs[g][dd + 1], bf_hi(kw));
-                    } else {
-                        e = fmaf(qs[g][dd], bf_lo(kw), e);
-                        o = fmaf(qs[g][dd + 1], bf_hi(kw), o);
-                    }
-                }
-            cs[g][kl][c] = __fadd_rn(e, o);
-        }
-    }
+    ea_chunk_sums<G>(qs, kv, cs, kl, qa);
     __syncthreads();
     if (qa != 0 || !valid) return;
     const bool vis = ea_visible(a, r, key);
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        float s;
-        if (u4) {   // 4 interleaved accumulators over the 256 dims (no remainder), in order
-            const bf16_t* kk = kb + (long)key * EA_D;
-            float ac[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int d = 0; d < EA_D; ++d) ac[d & 3] = fmaf(qs[g][d], bf2f(kk[d]), ac[d & 3]);
-            s = __fadd_rn(__fadd_rn(__fadd_rn(ac[0], ac[1]), ac[2]), ac[3]);
-        } else {
-            s = cs[g][kl][0];
-#pragma unroll
-            for (int c = 1; c < 8; ++c) s = __fadd_rn(s, cs[g][kl][c]);
-        }
-        float w = rbf(s);
-        w = rbf(__fmul_rn(w, a.scale));
-        if (a.softcap > 0.f) {
-            w = rbf(__fdiv_rn(w, a.softcap));
-            w = bf2f(a.tanh_lut[__float_as_uint(w) >> 16]);
-            w = rbf(__fmul_rn(w, a.softcap));
-        }
-        sbuf[((long)qi * a.Hq + kvh * G + g) * cap + key] = vis ? w : -INFINITY;
-    }
+    for (int g = 0; g < G; ++g)
+        sbuf[((long)qi * a.Hq + kvh * G + g) * cap + key] = vis ? ea_score(a, r, qs[g], kb, key, cs[g][kl]) : -INFINITY;
 }
 
+// softmax + P.V of one (query, kv head, 32-dim slice) from the G post-softcap score rows
+// in LDS pb [G][Tk] (-inf: masked); writes the slice of the G heads' outputs
 template <int G>
-__global__ __launch_bounds__(256) void eager_pv_kernel(ExactAttnArgs a, const float* sbuf, int cap) {
-    extern __shared__ __attribute__((aligned(16))) float ea_smem[];
-    float* pb = ea_smem;                      // [G][Tk]: scores, then e, then bf16-rounded p
+__device__ __forceinline__ void ea_softmax_pv(const ExactAttnArgs& a, const EaRow& r, float* pb, int qi, int kvh,
+                                              int z) {
     constexpr int NDP = EA_DZ / 2;            // dimension pairs of the slice (16)
     constexpr int NCL = 256 / NDP;            // chunk lanes (16)
     __shared__ float cs[NCL][G][EA_DZ + 1];   // chunk sums of one round [chunk lane][head][dim]
     __shared__ uint32_t vs[64][NDP];          // pair chain (< 64 keys): the slice's V rows
-    const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
-    const EaRow r = ea_row(a, qi);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int Tk = r.Tk;
-    if (Tk <= 0) return;
-    // ---- the G score rows into LDS in one coalesced pass
-    for (int i = tid; i < G * Tk; i += 256) {
-        const int g = i / Tk, j = i - g * Tk;
-        pb[i] = sbuf[((long)qi * a.Hq + kvh * G + g) * cap + j];
-    }
-    __syncthreads();
     // ---- softmax of each head's row (wave g): max, Sleef exp, 16-lane sum, x (1 / sum)
     if (wave < G) {
         float* p = pb + wave * Tk;
@@ -316,6 +321,57 @@ __global__ __launch_bounds__(256) void eager_pv_kernel(ExactAttnArgs a, const fl
     }
 }
 
+template <int G>
+__global__ __launch_bounds__(256) void eager_pv_kernel(ExactAttnArgs a, const float* sbuf, int cap) {
+    extern __shared__ __attribute__((aligned(16))) float ea_smem[];
+    float* pb = ea_smem;                      // [G][Tk]: scores, then e, then bf16-rounded p
+    const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
+    const EaRow r = ea_row(a, qi);
+    const int Tk = r.Tk;
+    if (Tk <= 0) return;
+    // the G score rows into LDS in one coalesced pass
+    for (int i = tid; i < G * Tk; i += 256) {
+        const int g = i / Tk, j = i - g * Tk;
+        pb[i] = sbuf[((long)qi * a.Hq + kvh * G + g) * cap + j];
+    }
+    __syncthreads();
+    ea_softmax_pv<G>(a, r, pb, qi, kvh, z);
+}
+
+// Decode rows of <= 64 keys (the cross attention over the text): scores, softmax and P.V in
+// ONE launch -- workgroup (row, kv head, 32-dim slice) computes the row's scores itself (the
+// scores kernel's code; the slices of a row share an XCD, so K comes from its L2) into LDS.
+template <int G>
+__global__ __launch_bounds__(256) void eager_single_kernel(ExactAttnArgs a) {
+    __shared__ float qs[G][EA_D];
+    __shared__ float cs[G][EA_CH][9];
+    __shared__ float pb[G * EA_CH];
+    const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
+    const int kl = tid >> 2, qa = tid & 3;
+    const EaRow r = ea_row(a, qi);
+    if (r.Tk <= 0) return;
+    const bool valid = kl < r.Tk;
+    const bf16_t* kb = a.K + r.row * a.kv_bstride + kvh * a.kv_hstride + (long)r.lo * EA_D;
+    u32x4 kv[8];
+    const bf16_t* kr = kb + (long)(valid ? kl : 0) * EA_D + 64 * qa;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kv[i] = *(const u32x4*)(kr + 8 * i);
+    for (int i = tid; i < G * EA_D; i += 256) {
+        const int g = i / EA_D, d = i % EA_D;
+        qs[g][d] = bf2f(a.Q[(long)qi * a.ldq + (kvh * G + g) * EA_D + d]);
+    }
+    __syncthreads();
+    ea_chunk_sums<G>(qs, kv, cs, kl, qa);
+    __syncthreads();
+    if (qa == 0 && valid) {
+        const bool vis = ea_visible(a, r, kl);
+#pragma unroll
+        for (int g = 0; g < G; ++g) pb[g * r.Tk + kl] = vis ? ea_score(a, r, qs[g], kb, kl, cs[g][kl]) : -INFINITY;
+    }
+    __syncthreads();
+    ea_softmax_pv<G>(a, r, pb, qi, kvh, z);
+}
+
 int eager_attention(const ExactAttnArgs& a, float* sbuf, int cap, hipStream_t st) {
     if (a.Mq <= 0) return 0;
     if (!a.Q || !a.K || !a.V || !a.kv_len || !a.O || !sbuf || !a.tanh_lut) return -1;
@@ -325,6 +381,13 @@ int eager_attention(const ExactAttnArgs& a, float* sbuf, int cap, hipStream_t st
     const dim3 gs((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)((cap + EA_CH - 1) / EA_CH));
     const dim3 gp((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(EA_D / EA_DZ));
     const size_t shm = (size_t)G * cap * sizeof(float);
+    const int span_max = a.span_max > 0 ? min(a.span_max, cap) : cap;
+    if (!a.q_pos && !a.q_len && span_max <= EA_CH) {   // decode rows of <= 64 keys: one launch
+        if (G == 2) hipLaunchKernelGGL(eager_single_kernel<2>, gp, dim3(256), 0, st, a);
+        else if (G == 1) hipLaunchKernelGGL(eager_single_kernel<1>, gp, dim3(256), 0, st, a);
+        else return -3;
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
     if (G == 2) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;

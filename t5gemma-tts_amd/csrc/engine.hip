@@ -712,8 +712,10 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
             r.Qout = q;
             r.ldq = e->q_dim;
             RC(rope_store(r, st));
+            XattnFuse fr;
+            fr.span_max = e->text_max;   // decode rows: the call's longest text (<= 64 keys -> one launch)
             RC(xattn(e, q, M, tok_row, tok_t, qlen, e->ck[l], e->cv[l], c.max_text, e->enc_len, 0, 0, att, att16,
-                     st));
+                     st, fr));
         }
         RC(xlin16(e, att16, M, X.cross_o, d, e->q_dim, nullptr, tmp, d, nullptr, EPI_BF16, tok_row, rl, d, 0, 0, st));
         RC(norm(L.norms[3], L.norms[4]));
