@@ -219,7 +219,13 @@ def _oparams(c):
 # free-running token-exact cases each golden set must keep (measured on MI355X, see
 # profiles/r02_parity_rates.json); every other case must diverge only at an explained
 # sampling-boundary flip (see _explain_divergence)
-MIN_EXACT = {"golden_tiny": 12, "golden_tiny_eager": 4, "golden_tiny_window": 4}
+# golden_tiny_eager runs the FAST kernels (parity mode restates eager attention for the
+# reference model's call shape only, 8 query heads of 256 -- tests/test_gpu_eager.py): since
+# round 4 their decode attention applies the softcap inside the aten-order / flash softmax
+# (common.h fast_score) instead of the separate eager-rounding launch, so 2 of the 4 cases
+# now flip at a sampling boundary -- each flip explained and asserted below (sampler on the
+# GPU's logits picks the GPU's token, on the reference's the reference's, logits within 2 %)
+MIN_EXACT = {"golden_tiny": 12, "golden_tiny_eager": 2, "golden_tiny_window": 4}
 
 
 def _topk_agree(g, r, k, tol):
@@ -282,8 +288,8 @@ def test_tiny_engine_vs_reference_golden(name):
     divergences = []
     for ci, c in enumerate(meta["cases"]):
         u = Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"])
-        # eager (softcap) configurations: the reference RNG and sampler with the fast kernels
-        # (parity mode's exact-order kernels restate the sdpa path and refuse eager)
+        # the tiny eager (softcap) configuration: the reference RNG and sampler with the fast
+        # kernels (parity mode restates eager attention for the 2b-2b call shape only)
         out = eng.generate([u], _params(c), seeds=[c["seed"]], parity=True, record_logits=True,
                            exact=False if name == "golden_tiny_eager" else None)
         w, ex = teacher_forced_check(cfg, sd, u, _oparams(c), c["seed"], out, rtol=0.02)
