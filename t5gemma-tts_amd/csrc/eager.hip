@@ -60,6 +60,37 @@ __device__ __forceinline__ bool ea_visible(const ExactAttnArgs& a, const EaRow& 
     return !r.causal_mask || kabs <= r.abs_t;
 }
 
+// RoPE of one rotation pair as rope_store_kernel computes it (the three bf16 tensor ops of
+// apply_rotary_pos_emb; xattn.hip xd_rope)
+__device__ __forceinline__ void ea_rope(float x1, float x2, float c, float sn, float& o1, float& o2) {
+    o1 = rbf(rbf(x1 * c) + rbf(-x2 * sn));
+    o2 = rbf(rbf(x2 * c) + rbf(x1 * sn));
+}
+
+// stage the G query rows of kv head kvh into qs; with a.rope_tab they arrive un-rotated and
+// are rotated here (decode: the step's per-row cos / sin table)
+template <int G>
+__device__ __forceinline__ void ea_stage_q(const ExactAttnArgs& a, const EaRow& r, int qi, int kvh, float (&qs)[G][256]) {
+    constexpr int H2 = 128;
+    const int tid = threadIdx.x;
+    if (a.rope_tab) {
+        const float* tab = a.rope_tab + (long)r.row * 256;
+        for (int i = tid; i < G * H2; i += 256) {
+            const int g = i / H2, d = i % H2;
+            const bf16_t* qh = a.Q + (long)qi * a.ldq + (kvh * G + g) * 256;
+            float o1, o2;
+            ea_rope(bf2f(qh[d]), bf2f(qh[d + H2]), tab[d], tab[H2 + d], o1, o2);
+            qs[g][d] = o1;
+            qs[g][d + H2] = o2;
+        }
+    } else {
+        for (int i = tid; i < G * 256; i += 256) {
+            const int g = i / 256, d = i % 256;
+            qs[g][d] = bf2f(a.Q[(long)qi * a.ldq + (kvh * G + g) * 256 + d]);
+        }
+    }
+}
+
 // Sleef_expf16_u10 (sleefsimdsp.c xexpf; aten Vectorized<float>::exp) for d <= 0
 __device__ __forceinline__ float ea_sleef_expf(float d) {
     if (d < -104.f) return 0.f;
@@ -152,11 +183,35 @@ __global__ __launch_bounds__(256) void eager_scores_kernel(ExactAttnArgs a, floa
     const bf16_t* kr = kb + (long)(valid ? key : c0) * EA_D + 64 * qa;
 #pragma unroll
     for (int i = 0; i < 8; ++i) kv[i] = *(const u32x4*)(kr + 8 * i);
-    for (int i = tid; i < G * EA_D; i += 256) {
-        const int g = i / EA_D, d = i % EA_D;
-        qs[g][d] = bf2f(a.Q[(long)qi * a.ldq + (kvh * G + g) * EA_D + d]);
+    ea_stage_q<G>(a, r, qi, kvh, qs);
+    // decode self attention (kv_new, with rope_tab): the workgroup holding the row's new key
+    // (the call's last key) rotates it, appends K and V to the cache and uses the rotated key
+    // directly -- xattn.hip's fused form, so no separate RoPE launch
+    __shared__ uint32_t knew[EA_D / 2];
+    const bool has_new = a.kv_new && a.rope_tab && r.Tk - 1 >= c0 && r.Tk - 1 < c0 + EA_CH;
+    if (has_new) {
+        constexpr int H2 = EA_D / 2;
+        const float* tab = a.rope_tab + (long)r.row * EA_D;
+        const long slot = r.lo + r.Tk - 1;
+        const bf16_t* kn = a.kv_new + (long)qi * a.ld_new + a.k_col0 + kvh * EA_D;
+        const bf16_t* vn = a.kv_new + (long)qi * a.ld_new + a.v_col0 + kvh * EA_D;
+        bf16_t* kc = (bf16_t*)a.K + r.row * a.kv_bstride + kvh * a.kv_hstride + slot * EA_D;
+        bf16_t* vc = (bf16_t*)a.V + r.row * a.kv_bstride + kvh * a.kv_hstride + slot * EA_D;
+        for (int d = tid; d < H2; d += 256) {
+            float o1, o2;
+            ea_rope(bf2f(kn[d]), bf2f(kn[d + H2]), tab[d], tab[H2 + d], o1, o2);
+            kc[d] = f2bf(o1);
+            kc[d + H2] = f2bf(o2);
+            ((bf16_t*)knew)[d] = f2bf(o1);
+            ((bf16_t*)knew)[d + H2] = f2bf(o2);
+        }
+        for (int d = tid; d < EA_D; d += 256) vc[d] = vn[d];
     }
     __syncthreads();
+    if (has_new && key == r.Tk - 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kv[i] = *(const u32x4*)&knew[32 * qa + 4 * i];
+    }
     ea_chunk_sums<G>(qs, kv, cs, kl, qa);
     __syncthreads();
     if (qa != 0 || !valid) return;
@@ -356,10 +411,7 @@ __global__ __launch_bounds__(256) void eager_single_kernel(ExactAttnArgs a) {
     const bf16_t* kr = kb + (long)(valid ? kl : 0) * EA_D + 64 * qa;
 #pragma unroll
     for (int i = 0; i < 8; ++i) kv[i] = *(const u32x4*)(kr + 8 * i);
-    for (int i = tid; i < G * EA_D; i += 256) {
-        const int g = i / EA_D, d = i % EA_D;
-        qs[g][d] = bf2f(a.Q[(long)qi * a.ldq + (kvh * G + g) * EA_D + d]);
-    }
+    ea_stage_q<G>(a, r, qi, kvh, qs);
     __syncthreads();
     ea_chunk_sums<G>(qs, kv, cs, kl, qa);
     __syncthreads();
@@ -382,7 +434,9 @@ int eager_attention(const ExactAttnArgs& a, float* sbuf, int cap, hipStream_t st
     const dim3 gp((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(EA_D / EA_DZ));
     const size_t shm = (size_t)G * cap * sizeof(float);
     const int span_max = a.span_max > 0 ? min(a.span_max, cap) : cap;
-    if (!a.q_pos && !a.q_len && span_max <= EA_CH) {   // decode rows of <= 64 keys: one launch
+    if ((a.rope_tab || a.kv_new) && (a.q_pos || a.q_len)) return -1;   // the fused RoPE / append: decode only
+    if (a.kv_new && !a.rope_tab) return -1;
+    if (!a.q_pos && !a.q_len && span_max <= EA_CH && !a.kv_new) {   // decode rows of <= 64 keys: one launch
         if (G == 2) hipLaunchKernelGGL(eager_single_kernel<2>, gp, dim3(256), 0, st, a);
         else if (G == 1) hipLaunchKernelGGL(eager_single_kernel<1>, gp, dim3(256), 0, st, a);
         else return -3;

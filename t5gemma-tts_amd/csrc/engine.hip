@@ -480,7 +480,6 @@ static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const
     if (c.softcap > 0.f) {
         // eager attention (eager.hip): decode rows on the engine's scores scratch, packed
         // (prefill / encoder) calls on a stream-ordered one (not inside a captured graph)
-        if (fr.rope_tab || fr.kv_new) return -1;
         a.softcap = c.softcap;
         a.tanh_lut = e->tanh_lut_dev;
         if (!q_pos && !q_len) return eager_attention(a, e->asbuf, cap, st);
@@ -662,7 +661,7 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         RC(xlin16(e, xn16, M, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
                   e->q_dim, e->kv_dim, e->q_dim, st));
         // decode: RoPE of q and k and the cache append happen inside the scores launch
-        const bool fuse = decode && c.softcap <= 0.f && exact_attention_decode_supported(c.n_heads / c.n_kv_heads, D);
+        const bool fuse = decode && exact_attention_decode_supported(c.n_heads / c.n_kv_heads, D);
         if (fuse) {
             XattnFuse fr;
             fr.rope_tab = e->rope_tab;

@@ -371,6 +371,12 @@ def gen_config_goldens(RT, which):
         gen_cases_golden(RT, "golden_2b2b_eager", [_row_case(x1, y1, len(y1) + 1, 4500),
                                                    _row_case(x2, y2, len(y2) + 16, 4501),
                                                    _row_case(x3, y3, len(y3) + 1, 4502)], kw)
+    if "eager2b_long" in which:   # eager attention after a 602-token prefill
+        steps = 16
+        kw = {"attn_implementation": "eager", "extra_cutoff": (steps - 2) / 50.0}
+        cfgl = named_config("2b2b", **kw)
+        x, y, _ = make_batch(cfgl, 1, seed=20251231, T_x=60, T_p=601)[0]
+        gen_cases_golden(RT, "golden_2b2b_eager_long", [_row_case(x, y, len(y) + 1, 4600)], kw)
     if "longprompt2k" in which:   # a 2 001-token prefill: the K-split table past M = 1 024
         steps = 8
         kw = {"extra_cutoff": (steps - 2) / 50.0}
@@ -447,7 +453,7 @@ if __name__ == "__main__":
         gen_full_golden(RT)
     if "long" in todo:
         gen_long_golden(RT)
-    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt", "longprompt2k", "eager2b")]
+    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt", "longprompt2k", "eager2b", "eager2b_long")]
     if cfg_todo:
         gen_config_goldens(RT, cfg_todo)
     if "mid" in todo:

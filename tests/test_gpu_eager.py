@@ -146,3 +146,30 @@ def test_eager_fast_path(eager_engine):
         assert (fa - xa).abs().max().item() <= 0.03 * xa.abs().max().item(), b
         shared = len(set(torch.topk(fa, 30).indices.tolist()) & set(torch.topk(xa, 30).indices.tolist()))
         assert shared >= 25, (b, shared)
+
+
+def test_eager_long_prompt_golden_exact(eager_engine):
+    """A 601-code prompt (a 602-token eager prefill: q.k^T / P.V at 602 x 602, E/O-32 with
+    no K split) then 16 decode steps == the reference's own eager run
+    (golden_2b2b_eager_long), alone and as row 1 of a batch with a short eager row."""
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import T5GemmaTTSEngine, Utterance
+    from t5gemma_tts_amd.weights import synthetic_weights
+    meta, p, _ = eager_engine
+    with open(os.path.join(GOLDEN, "golden_2b2b_eager_long.json")) as f:
+        lm = json.load(f)
+    assert lm["weight_sha256"] == meta["weight_sha256"] and lm["config_kw"]["attn_implementation"] == "eager"
+    cfg = named_config(lm["config"], **lm["config_kw"])   # its own generation budget
+    eng = T5GemmaTTSEngine(cfg, synthetic_weights(cfg, lm["weight_seed"]), device="cuda:0", max_batch=2,
+                           max_text=64, max_audio=1024, max_gen=200)
+    c = lm["cases"][0]
+    short = meta["cases"][1]
+    for utts, seeds, slot in (([Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"])], [c["seed"]], 0),
+                              ([Utterance(x=short["x"], y=short["y"], tgt_y_len=short["tgt"]),
+                                Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"])], [short["seed"], c["seed"]], 1)):
+        out = eng.generate(utts, p, seeds=seeds, parity=True, record_logits=True)
+        n = len(c["gen"])
+        shas = [hashlib.sha256(lg[slot].cpu().view(torch.int16).numpy().tobytes()).hexdigest()[:16]
+                for lg in out["logits"][:n]]
+        assert out["gen"][slot].tolist() == c["gen"], slot
+        assert shas == c["logit_sha"], (slot, sum(a == b for a, b in zip(shas, c["logit_sha"])))
