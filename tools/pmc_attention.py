@@ -25,6 +25,7 @@ def algorithmic_bytes():
 
 
 def main():
+    flash = "--flash" in sys.argv   # the fast path's one-launch form (t5g_attention_decode_flash)
     L = _lib.lib()
     dev = torch.device("cuda:0")
     caches = [(torch.randn(B, HKV, CAP, D, device=dev).to(torch.bfloat16),
@@ -32,7 +33,8 @@ def main():
     q = torch.randn(B, HQ, D, device=dev).to(torch.bfloat16)
     lens = torch.tensor(LENS, dtype=torch.int32, device=dev)
     out = torch.empty(B, HQ * D, dtype=torch.bfloat16, device=dev)
-    work = torch.empty(L.t5g_attention_decode_work_bytes(B, HQ, HKV, D, CAP) // 4, dtype=torch.float32, device=dev)
+    work = torch.zeros(L.t5g_attention_decode_work_bytes(B, HQ, HKV, D, CAP) // 4, dtype=torch.float32, device=dev)
+    fn = L.t5g_attention_decode_flash if flash else L.t5g_attention_decode
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for it in range(3):
@@ -42,12 +44,13 @@ def main():
             a = _lib.AttnDecodeArgs(B=B, n_heads=HQ, n_kv_heads=HKV, head_dim=D, q=q.data_ptr(), k_cache=K.data_ptr(),
                                     v_cache=V.data_ptr(), cap=CAP, kv_len=lens.data_ptr(), causal=1, window=0,
                                     scale=D ** -0.5, out=out.data_ptr(), work=work.data_ptr())
-            _lib.check(L.t5g_attention_decode(C.byref(a), st), "attention_decode")
+            _lib.check(fn(C.byref(a), st), "attention_decode")
     ev1.record()
     torch.cuda.synchronize()
     us = ev0.elapsed_time(ev1) * 1e3 / (2 * N_CACHES)
     alg = algorithmic_bytes()
-    print(f"attention avg {us:.2f} us/call (3 launches), algorithmic {alg} B -> {alg / us / 1e3:.1f} GB/s", flush=True)
+    print(f"attention{' (flash, 1 launch)' if flash else ' (2 launches)'} avg {us:.2f} us/call, algorithmic {alg} B -> "
+          f"{alg / us / 1e3:.1f} GB/s", flush=True)
 
 
 if __name__ == "__main__":

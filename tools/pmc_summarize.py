@@ -33,6 +33,12 @@ OPS = {
                   "algorithmic": None,
                   "what": "decode self attention (scores + P.V/combine launches), 8 rows x 8/4 heads x 256, L ~ 527 "
                           "(tools/pmc_attention.py: 26 KV caches, 436 MB > 256 MiB Infinity Cache)"},
+    "attention_flash": {"kernels": ["attn_decode_kernel<256, 2, true, true>"],
+                        "algorithmic": None,
+                        "what": "decode self attention, the fast path's one-launch flash form (per-chunk "
+                                "online-softmax partials, last-arriving chunk combines), 8 rows x 8/4 heads x 256, "
+                                "L ~ 527 (tools/pmc_attention.py --flash: 26 KV caches, 436 MB > 256 MiB Infinity "
+                                "Cache)"},
 }
 
 
