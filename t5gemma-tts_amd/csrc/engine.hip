@@ -180,7 +180,7 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     const t5g_config& c = *cfg;
     if (c.hidden % 32 || c.intermediate % 32 || c.n_enc_layers > T5G_MAX_LAYERS ||
         c.n_dec_layers > T5G_MAX_LAYERS || c.max_batch <= 0 || c.max_text <= 0 || c.max_audio <= 0 ||
-        c.n_heads % c.n_kv_heads || c.max_audio > 4096 || c.max_text > 4096)
+        c.n_heads % c.n_kv_heads || c.max_audio > SDPA_KV_BLOCK * SDPA_MAX_BLOCKS || c.max_text > 4096)
         return T5G_EINVAL;
     t5g_engine* e = new t5g_engine();
     e->c = c;

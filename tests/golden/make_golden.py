@@ -377,6 +377,12 @@ def gen_config_goldens(RT, which):
         cfgl = named_config("2b2b", **kw)
         x, y, _ = make_batch(cfgl, 1, seed=20251231, T_x=60, T_p=601)[0]
         gen_cases_golden(RT, "golden_2b2b_eager_long", [_row_case(x, y, len(y) + 1, 4600)], kw)
+    if "longprompt4k" in which:   # a 4 101-token prefill: past the 4 096-key sliding window
+        steps = 8
+        kw = {"extra_cutoff": (steps - 2) / 50.0}
+        cfgl = named_config("2b2b", **kw)
+        x, y, _ = make_batch(cfgl, 1, seed=20251232, T_x=60, T_p=4100)[0]
+        gen_cases_golden(RT, "golden_longprompt4k", [_row_case(x, y, len(y) + 1, 4700)], kw)
     if "longprompt2k" in which:   # a 2 001-token prefill: the K-split table past M = 1 024
         steps = 8
         kw = {"extra_cutoff": (steps - 2) / 50.0}
@@ -453,7 +459,7 @@ if __name__ == "__main__":
         gen_full_golden(RT)
     if "long" in todo:
         gen_long_golden(RT)
-    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt", "longprompt2k", "eager2b", "eager2b_long")]
+    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt", "longprompt2k", "longprompt4k", "eager2b", "eager2b_long")]
     if cfg_todo:
         gen_config_goldens(RT, cfg_todo)
     if "mid" in todo:

@@ -293,3 +293,46 @@ def test_config_golden_exact(name, batch, slot):
     _write(f"parity_{name}_b{batch}.json", rep)
     print(json.dumps(rep))
     assert rep["tokens_equal"] and rep["logit_rows_equal"] == n, rep
+
+
+@pytest.mark.timeout(600)
+def test_sliding_window_long_prompt_golden():
+    """golden_longprompt4k: a 4 100-code prompt (a 4 101-token prefill, past the 2b-2b
+    sliding layers' 4 096-key window: the explicit prefill mask, then the
+    DynamicSlidingWindowLayer trim at every decode step) and 8 steps, against the reference's
+    own run. Measured (tools/diag_window.py): every token equal; the prefill's logits row
+    (step 0) and decode steps 3..7 bitwise; steps 1 and 2 differ by one bf16 ulp in 3 / 11 of
+    the reference's top-64 logits. The decode attention launches are bit-equal to the
+    oracle at these lengths (test_gpu_exact.py, 4 102 / 4 103 keys, windowed), so the 1-ulp
+    rows are not yet explained: parity at this length is PARTIAL and the test pins exactly
+    that (tokens, step-0 row, <= 1 ulp on the top-64 everywhere)."""
+    _need_gpu()
+    import hashlib
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import SamplingParams, T5GemmaTTSEngine, Utterance
+    from t5gemma_tts_amd.weights import state_dict_digest, synthetic_weights
+    with open(os.path.join(GOLDEN, "golden_longprompt4k.json")) as f:
+        meta = json.load(f)
+    z = np.load(os.path.join(GOLDEN, "golden_longprompt4k.npz"))
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    assert cfg.backbone.sliding_window == 4096
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    assert state_dict_digest(sd) == meta["weight_sha256"]
+    c = meta["cases"][0]
+    assert len(c["y"]) + 1 > cfg.backbone.sliding_window
+    p = SamplingParams(top_k=c["top_k"], top_p=c["top_p"], min_p=c["min_p"], temperature=c["temperature"],
+                       stop_repetition=c["stop_repetition"])
+    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=1, max_text=64,
+                           max_audio=len(c["y"]) + len(c["gen"]) + 16, max_gen=len(c["gen"]) + 8)
+    out = eng.generate([Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"])], p, seeds=[c["seed"]], parity=True,
+                       record_logits=True)
+    rows = []
+    for s_, lg in enumerate(out["logits"][:len(c["gen"])]):
+        bits = lg[0].cpu().view(torch.int16).numpy()
+        d = np.abs(bits[z["top_idx_0"][s_]].astype(np.int32) - z["top_vals_0"][s_].astype(np.int32))
+        rows.append((hashlib.sha256(bits.tobytes()).hexdigest()[:16] == c["logit_sha"][s_], int(d.max())))
+    rep = {"tokens_equal": out["gen"][0].tolist() == c["gen"], "rows_bitwise": sum(r[0] for r in rows),
+           "of": len(rows), "max_top64_ulps": max(r[1] for r in rows)}
+    _write("parity_golden_longprompt4k_b1.json", rep)
+    print(json.dumps(rep))
+    assert rep["tokens_equal"] and rows[0][0] and rep["max_top64_ulps"] <= 1, rep
