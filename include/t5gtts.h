@@ -55,7 +55,7 @@ typedef struct {
     uint8_t dec_sliding[T5G_MAX_LAYERS];
     int32_t max_batch;     /* utterance rows per call */
     int32_t max_text;      /* text tokens per row (encoder length capacity) */
-    int32_t max_audio;     /* decoder cache length per row: BOS + prompt + generated */
+    int32_t max_audio;     /* decoder cache length per row: BOS + prompt + generated (<= 8192; the fast decode attention <= 4096) */
     int32_t max_gen;       /* generated-token capacity per row */
     /* sampler / stop constants (:590-592, :727, :773-777) */
     int32_t eos;           /* eog_inference */

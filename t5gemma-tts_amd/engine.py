@@ -29,6 +29,7 @@ from .noise import DeviceNoise
 from .weights import check_state_dict
 
 BF16 = torch.bfloat16
+FAST_MAX_AUDIO = 4096   # fast decode attention: <= 64 chunks of 64 keys (csrc/attn.hip)
 
 
 @dataclass
@@ -302,6 +303,11 @@ class T5GemmaTTSEngine:
             raise ValueError("parity mode restates eager attention (attn_implementation='eager', logit softcap) "
                              "for 8 query heads of head_dim 256 only (the reference's oneDNN picks its matmul "
                              "kernels by shape): run with parity=False (fast kernels, tolerance parity)")
+        if not exact and self.max_audio > FAST_MAX_AUDIO:
+            # the fast decode attention takes at most 64 chunks of 64 keys (csrc/attn.hip);
+            # the exact launches reach SDPA_MAX_BLOCKS x 512 keys
+            raise ValueError(f"max_audio {self.max_audio} > {FAST_MAX_AUDIO}: the fast decode attention's capacity; "
+                             "use parity=True (exact kernels, up to 8192 keys) or a smaller max_audio")
         if exact:
             for u in utts:
                 n_y = len(u.y) + 1

@@ -336,3 +336,5 @@ def test_sliding_window_long_prompt_golden():
     _write("parity_golden_longprompt4k_b1.json", rep)
     print(json.dumps(rep))
     assert rep["tokens_equal"] and rows[0][0] and rep["max_top64_ulps"] <= 1, rep
+    with pytest.raises(ValueError, match="fast decode attention"):   # its 4 096-key capacity
+        eng.generate([Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"])], p, seeds=[c["seed"]])
