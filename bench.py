@@ -50,8 +50,6 @@ WORKLOADS = {
 T_X, T_P = 60, 151          # c3 (kept for tools that import them)
 B_PER_GPU = 8
 B_PER_GPU_E2E = 32
-CPU_SAMPLE_STEPS = 8        # decode steps timed at each sampled cache length
-CPU_SAMPLE_LENS = (450, 750, 900)
 
 
 def make_batch(cfg, n: int, seed: int, T_x: int = T_X, T_p: int = T_P):
@@ -102,16 +100,14 @@ def cpu_model() -> str:
 
 def cpu_baseline(cfg, sd_gpu, utt, n_budget: int):
     """The CPU oracle (the reference's algorithm in PyTorch CPU ops, pinned bitwise to the
-    reference's golden vectors) on one utterance of the workload, batch 1 as the reference.
-    Bounded sample of the whole generate(): encoder + prefill and CPU_SAMPLE_STEPS decode
-    steps right after it are timed on the utterance itself; the per-step time further into
-    the row (larger self-attention cache) is timed at CPU_SAMPLE_LENS keys, each on the same
-    utterance with its prompt extended to that length (prefill untimed). A least-squares
-    line through the step times over the cache length gives the time of all ``n_budget``
-    steps; rate = n_budget / (prefill + steps), the reference's [Speed] definition
-    (inference_tts_utils.py:308-321)."""
+    reference's golden vectors) timed on ONE whole utterance of the workload, batch 1 as the
+    reference runs it: encoder + prefill + every one of the row's ``n_budget`` AR steps
+    (head, sampler with its noise draw, decoder step), EOS disabled so the row runs its full
+    time budget like the GPU rows. rate = tokens / wall, the reference's [Speed] definition
+    (inference_tts_utils.py:308-321). Threads: OMP_NUM_THREADS (16 on the GPU box: the
+    box's CPU share per GPU, which the harness sets and asks jobs to keep)."""
     import torch
-    from oracle.t5g_oracle import SamplerParams, T5GemmaTTSOracle, draw_noise, sample_helper
+    from oracle.t5g_oracle import SamplerParams, T5GemmaTTSOracle
     threads = int(os.environ.get("OMP_NUM_THREADS", torch.get_num_threads()))
     torch.set_num_threads(threads)
     sd = {k: v.cpu() for k, v in sd_gpu.items()}
@@ -119,47 +115,15 @@ def cpu_baseline(cfg, sd_gpu, utt, n_budget: int):
     x, y, tgt = utt
     p = SamplerParams(top_k=30, top_p=0.9, temperature=0.8, eos_disabled=True)
     t0 = time.perf_counter()
-    ctx = orc.prepare(x, y, tgt)
-    t_pre = time.perf_counter() - t0
-    rng = np.random.default_rng(5)
-    pts = []
-    L0 = len(y) + 1
-
-    gen = torch.Generator().manual_seed(1)
-
-    def time_steps(c):
-        # one AR step as generate() runs it: head, sample_helper (+ its noise draw), embed +
-        # decoder step
-        st = c["state"]
-        t1 = time.perf_counter()
-        for _ in range(CPU_SAMPLE_STEPS):
-            logits = orc.step_logits(c)
-            tok, _ = sample_helper(logits, p, st, draw_noise(gen, logits.shape[-1]), eos=cfg.eog_inference,
-                                   encodec_sr=cfg.encodec_sr, extra_cutoff=cfg.extra_cutoff)
-            st.cur_num_gen += 1
-            st.current_length += 1
-            orc.advance(c, tok)
-        return (time.perf_counter() - t1) / CPU_SAMPLE_STEPS
-
-    pts.append((L0, time_steps(ctx)))
-    for L in CPU_SAMPLE_LENS:
-        # the same text, a prompt of L - 2 codes + y_sep: the step then attends over L keys
-        yl = rng.integers(0, cfg.audio_vocab_size, size=L - 2).tolist() + [cfg.y_sep_token]
-        c = orc.prepare(x, yl, len(yl) + DUR_FRAMES)
-        pts.append((len(yl) + 1, time_steps(c)))
-    Ls = np.array([q[0] for q in pts], float)
-    ts = np.array([q[1] for q in pts], float)
-    b, a = np.polyfit(Ls, ts, 1)
-    steps = a * n_budget + b * sum(L0 + i for i in range(n_budget))
-    total = t_pre + steps
-    return {"value": round(n_budget / total, 3), "unit": "audio tokens/s", "cores": threads, "kind": "port",
+    out = orc.generate(x, y, tgt, p, seed=1, max_steps=n_budget)
+    wall = time.perf_counter() - t0
+    n = int(out["gen"].numel())
+    return {"value": round(n / wall, 3), "unit": "audio tokens/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(),
-            "sample": f"1 utterance of this workload (T_x {len(x)}, T_p {len(y)}), batch 1 (reference semantics): "
-                      f"encoder + prefill {t_pre:.1f} s timed; decode step times at cache lengths "
-                      + ", ".join(f"{int(l)}: {t * 1e3:.0f} ms" for l, t in pts)
-                      + f" ({CPU_SAMPLE_STEPS} steps each), fitted linearly over all {n_budget} steps "
-                      f"(L {L0}..{L0 + n_budget - 1}): {steps:.1f} s; the reference itself measured 7.04 tok/s "
-                      f"on 8 cores in the build container (SURVEY 6)"}
+            "sample": f"1 utterance of this workload (T_x {len(x)}, T_p {len(y)}), batch 1 (reference semantics), "
+                      f"timed whole: encoder + prefill + {n} AR steps (L {len(y) + 1}..{len(y) + n}) in {wall:.1f} s "
+                      f"on {threads} threads (the GPU box's per-GPU CPU share); the reference itself measured "
+                      f"7.04 tok/s on 8 cores in the build container (SURVEY 6)"}
 
 
 def main():

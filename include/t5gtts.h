@@ -55,7 +55,7 @@ typedef struct {
     uint8_t dec_sliding[T5G_MAX_LAYERS];
     int32_t max_batch;     /* utterance rows per call */
     int32_t max_text;      /* text tokens per row (encoder length capacity) */
-    int32_t max_audio;     /* decoder cache length per row: BOS + prompt + generated (<= 8192; the fast decode attention <= 4096) */
+    int32_t max_audio;     /* decoder cache length per row: BOS + prompt + generated (<= 12 288: a 100 s prompt + the 120 s duration cap) */
     int32_t max_gen;       /* generated-token capacity per row */
     /* sampler / stop constants (:590-592, :727, :773-777) */
     int32_t eos;           /* eog_inference */
@@ -320,6 +320,13 @@ int t5g_engine_set_fused(t5g_engine* e, int32_t enable);
  * calls run (0: assume max_text). The persistent decode launch reads at most 64 cross keys
  * per row, so it is chosen when the batch's texts fit, whatever the engine's max_text. */
 int t5g_engine_set_text_max(t5g_engine* e, int32_t n);
+/* Host hint: a bound on every row's self-attention keys in the next t5g_sampler_setup /
+ * t5g_decode calls (0: max_audio) -- the largest prompt + time budget of the batch. The
+ * decode attention grids cover that many keys, not the cache capacity, and the sampler
+ * force-stops a row there (its capacity rule, :773-779 budget semantics unchanged when the
+ * bound is at or above every row's prompt + budget). Replaces no reference interface: the
+ * reference's DynamicCache grows per call ([tf] cache_utils.py:127-144). */
+int t5g_engine_set_audio_max(t5g_engine* e, int32_t n);
 /* Test hook: store `code` (non-zero) in the fused launch's sticky timeout word, as a
  * hand-off that gave up waiting would: every later in-launch wait gives up at once, the next
  * t5g_read_tokens returns T5G_EHANDOFF and clears the counters (tests/test_gpu_fused.py:

@@ -218,21 +218,26 @@ def even_div_chunk(K: int) -> int:
 
 
 def sdpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, is_causal: bool = False,
-         mask: Optional[torch.Tensor] = None, Hq: Optional[int] = None, threads: int = 8) -> torch.Tensor:
+         mask: Optional[torch.Tensor] = None, Hq: Optional[int] = None, threads: int = 8,
+         row_from: int = 0, row_to: Optional[int] = None) -> torch.Tensor:
     """F.scaled_dot_product_attention on CPU bf16 as the reference host computes it.
     q [H, Tq, D], k / v [H, Tk, D] (GQA already expanded), mask bool [Tq, Tk] (True =
-    attend) or None. Returns bf16 [H, Tq, D]."""
+    attend) or None. Returns bf16 [H, Tq, D]. ``row_from`` / ``row_to``: only the q blocks
+    holding rows in [row_from, row_to) are computed (aten's q blocks are independent; the
+    other rows are left 0)."""
     H, Tq, D = q.shape
     Tk = k.shape[1]
     causal = bool(is_causal and mask is None and Tq > 1)
     pk = need_pack(Tq, Tk, Hq or H, D, threads, causal)
-    out = torch.empty(H, Tq, D, dtype=BF16)
+    out = torch.zeros(H, Tq, D, dtype=BF16)
     qsz = E.qsplit(Tq)
     scale_t = torch.tensor(scale, dtype=torch.float32)
     for h in range(H):
         qh, kh, vh = q[h].float().numpy(), k[h].float().numpy(), v[h].float().numpy()
         for r0 in range(0, Tq, qsz):
             r1 = min(r0 + qsz, Tq)
+            if r1 <= row_from or (row_to is not None and r0 >= row_to):
+                continue
             M = r1 - r0
             nk = min(Tk - Tq + r1, Tk) if causal else Tk
             gemv = M == 1 and not pk

@@ -134,6 +134,7 @@ SIGNATURES = {
     "t5g_engine_set_sampler_path": (C.c_int, [_P, _I]),
     "t5g_engine_set_fused": (C.c_int, [_P, _I]),
     "t5g_engine_set_text_max": (C.c_int, [_P, _I]),
+    "t5g_engine_set_audio_max": (C.c_int, [_P, _I]),
     "t5g_engine_poison_handoff": (C.c_int, [_P, C.c_uint32]),
     "t5g_time_decode_mlp": (C.c_int, [_P, _I, _I, _P, C.POINTER(_F)]),
     "t5g_exact_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
@@ -155,9 +156,11 @@ SIGNATURES = {
 GELU_ERF_TABLE = os.path.join(_PKG, "data", "gelu_erf_bf16.bin")
 # RoPE cos / sin angles where the reference host's MKL differs from the correctly rounded
 # value after the bf16 cast (tools/cpu_order/make_rope_table.py); covers every position
-# of an utterance whose estimated total length is <= ROPE_EXC_MAX_LEN
+# of an utterance whose estimated total length is <= ROPE_EXC_MAX_LEN (12 288: a 100 s
+# prompt + the 120 s duration cap; extending the search from 8 192 found no new angle,
+# profiles/r05_s1_rope_table_extend_12288.log)
 ROPE_EXC_TABLE = os.path.join(_PKG, "data", "rope_trig_exc.bin")
-ROPE_EXC_MAX_LEN = 8192
+ROPE_EXC_MAX_LEN = 12288
 
 
 def rope_exc_table():

@@ -318,7 +318,7 @@ __device__ __forceinline__ void attn_flash_finish(const AttnArgs& a, float (&sm)
     constexpr int FB = 16;  // chunk partials per combine batch (one batch up to 1 024 keys)
     __shared__ f32x4 ored[4][G][LPK][2];
     __shared__ float cstat[G][2];
-    __shared__ float wts[G][64];
+    __shared__ float wts[G][DEC_MAX_CHUNKS];
     __shared__ float lsum[G];
     __shared__ int last;
     const int tid = (int)threadIdx.x;
@@ -412,17 +412,31 @@ __device__ __forceinline__ void attn_flash_finish(const AttnArgs& a, float (&sm)
     f32x4 pv[FB];
     pload(pv, 0);
     if (wave < G) {
+        // lane owns chunks lane + 64 i (rows of up to DEC_MAX_CHUNKS chunks)
+        constexpr int CPL = DEC_MAX_CHUNKS / 64;
         const int g = wave;
-        float m = -INFINITY, l = 0.f;
-        if (lane < nch) {
-            const u32x2_t st = __builtin_amdgcn_raw_buffer_load_b64(srs, (int)((((rec + lane) * G + g) * 2) * 4), 0, 16);
-            m = __uint_as_float(st[0]);
-            l = __uint_as_float(st[1]);
+        float m[CPL], l[CPL];
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+            const int c = lane + 64 * i;
+            int off = c < nch ? (int)((((rec + c) * G + g) * 2) * 4) : (int)0x7ffffff0;
+            asm volatile("" : "+v"(off));
+            const u32x2_t st = __builtin_amdgcn_raw_buffer_load_b64(srs, off, 0, 16);
+            m[i] = c < nch ? __uint_as_float(st[0]) : -INFINITY;
+            l[i] = c < nch ? __uint_as_float(st[1]) : 0.f;
         }
-        const float M = wave_max(m);
-        const float w = lane < nch ? __expf(m - M) : 0.f;
-        const float L = xsum<64>(w * l);
-        wts[g][lane] = w;
+        float mm = m[0];
+#pragma unroll
+        for (int i = 1; i < CPL; ++i) mm = fmaxf(mm, m[i]);
+        const float M = wave_max(mm);
+        float wl = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+            const float w = lane + 64 * i < nch ? __expf(m[i] - M) : 0.f;
+            wts[g][lane + 64 * i] = w;
+            wl += w * l[i];
+        }
+        const float L = xsum<64>(wl);
         if (lane == 0) lsum[g] = L;
     }
     __syncthreads();
@@ -846,15 +860,23 @@ __global__ __launch_bounds__(256) void attn_pvc_kernel(AttnArgs a) {
     float scn[G][PPT], sc1[G][PPT];
     sload(scn, 0);
     if constexpr (RPB == 1) sload(sc1, 1);
-    const float cmv = a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + min(lane, a.nsplit - 1)) * G + min(wave, G - 1)];
+    constexpr int CPL = DEC_MAX_CHUNKS / 64;    // chunk maxima per lane (chunk lane + 64 i)
+    float cmv[CPL];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+        cmv[i] = a.mbuf[(((long)qi * a.Hkv + kvh) * a.nsplit + min(lane + 64 * i, a.nsplit - 1)) * G + min(wave, G - 1)];
     u32x4 vn[NIT], v1[NIT];
     vload(vn, 0);
     if constexpr (RPB == 1) vload(v1, 1);   // the second block's slice (zeros if none)
     if (wave < G) {   // running maxima through each block, from the chunk maxima
         const int g = wave;
-        const float cm = lane < nch ? cmv : -INFINITY;
         for (int b = 0; b < nblk; ++b) {
-            const float mb = wave_max(lane < min(nch, (b + 1) * CPB) ? cm : -INFINITY);
+            const int lim = min(nch, (b + 1) * CPB);
+            float cm = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < CPL; ++i)
+                if (lane + 64 * i < lim) cm = fmaxf(cm, cmv[i]);
+            const float mb = wave_max(cm);
             if (lane == 0) mrun[g][b] = mb;
         }
         if (lane < 16) {
@@ -1108,8 +1130,10 @@ static int launch_decode(const AttnArgs& a_in, hipStream_t st) {
 int attention_decode(const AttnArgs& a, hipStream_t st) {
     if (a.Mq <= 0) return 0;
     if (a.eager || a.kv_cap <= 0 || a.kv_cap > SDPA_KV_BLOCK * SDPA_MAX_BLOCKS) return -1;
-    if (a.nsplit != (a.kv_cap + DCH - 1) / DCH) return -1;   // 64-key chunks from the row start
-    if (a.nsplit > 1 && (!a.sbuf || !a.mbuf || a.nsplit > 64)) return -1;
+    // 64-key chunks from the row start; the grid covers nsplit of them (the call's longest
+    // row, <= the cache capacity: rows longer than nsplit * 64 keys are refused on the host)
+    if (a.nsplit < 1 || a.nsplit > (a.kv_cap + DCH - 1) / DCH) return -1;
+    if (a.nsplit > 1 && (!a.sbuf || !a.mbuf || a.nsplit > DEC_MAX_CHUNKS)) return -1;
     if (a.flash && a.nsplit > 1 && (!a.fpart || !a.fstat || !a.fticket || a.G * a.D / 4 > 256 - 64 * a.G ||
                                     (long)a.Mq * a.Hkv * a.nsplit * a.G * a.D * 4 > 0x7fff0000L))
         return -1;
@@ -1126,6 +1150,16 @@ template <int D, int G>
 static int launch_attn(const AttnArgs& a, hipStream_t st) {
     dim3 grid((unsigned)a.Mq, (unsigned)a.Hkv, 1u);
     size_t shm = (size_t)G * a.chunk * sizeof(float);
+    if (shm > 64 * 1024) {   // rows of > 8 192 keys (G = 2): opt in to 96 KiB, once per device
+        static bool attr[T5G_MAX_DEVICES][2] = {};
+        const int dev = t5g_cur_device();
+        if (dev < 0) return -2;
+        if (!attr[dev][a.eager ? 1 : 0]) {
+            (void)hipFuncSetAttribute(a.eager ? (const void*)attn_kernel<D, G, true> : (const void*)attn_kernel<D, G, false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            attr[dev][a.eager ? 1 : 0] = true;
+        }
+    }
     if (a.eager)
         hipLaunchKernelGGL((attn_kernel<D, G, true>), grid, dim3(256), shm, st, a);
     else

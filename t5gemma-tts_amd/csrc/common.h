@@ -24,6 +24,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define WAVE 64
 
+// Host launchers: function attributes (dynamic LDS opt-in) and device properties are per
+// device, so one-time setup is tracked per device, never in a process-global flag (an
+// engine per GPU in one process must not skip the second device's setup).
+constexpr int T5G_MAX_DEVICES = 64;
+static inline int t5g_cur_device() {
+    int d = 0;
+    return (hipGetDevice(&d) == hipSuccess && d >= 0 && d < T5G_MAX_DEVICES) ? d : -1;
+}
+
 __device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float(h << 16); }
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }

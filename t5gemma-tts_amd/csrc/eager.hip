@@ -27,7 +27,7 @@ namespace t5g {
 constexpr int EA_D = 256;      // head_dim of the measured call shape
 constexpr int EA_CH = 64;      // keys per scores workgroup
 constexpr int EA_DZ = 32;      // output dims per P.V workgroup
-constexpr int EA_MAXK = 6144;  // keys per call (parity mode: <= 5 001 tokens)
+constexpr int EA_MAXK = SDPA_KV_BLOCK * SDPA_MAX_BLOCKS;   // keys per call: the engine's cache capacity
 
 struct EaRow {
     int row, Tq, Tk, lo, abs_t;
@@ -430,10 +430,12 @@ int eager_attention(const ExactAttnArgs& a, float* sbuf, int cap, hipStream_t st
     // the measured call shape (tools/cpu_order/eager_table_2b2b.jsonl): 8 query heads of 256
     if (a.D != EA_D || a.Hq != 8 || a.Hq % a.Hkv || cap <= 0 || cap > EA_MAXK) return -3;
     const int G = a.Hq / a.Hkv;
-    const dim3 gs((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)((cap + EA_CH - 1) / EA_CH));
-    const dim3 gp((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(EA_D / EA_DZ));
-    const size_t shm = (size_t)G * cap * sizeof(float);
+    // span_max (host bound on every row's keys, 0: cap) sizes the scores grid and the P.V
+    // launch's LDS rows (G x keys fp32: 96 KiB at 12 288 keys)
     const int span_max = a.span_max > 0 ? min(a.span_max, cap) : cap;
+    const dim3 gs((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)((span_max + EA_CH - 1) / EA_CH));
+    const dim3 gp((unsigned)a.Mq, (unsigned)a.Hkv, (unsigned)(EA_D / EA_DZ));
+    const size_t shm = (size_t)G * span_max * sizeof(float);
     if ((a.rope_tab || a.kv_new) && (a.q_pos || a.q_len)) return -1;   // the fused RoPE / append: decode only
     if (a.kv_new && !a.rope_tab) return -1;
     if (!a.q_pos && !a.q_len && span_max <= EA_CH && !a.kv_new) {   // decode rows of <= 64 keys: one launch
@@ -443,9 +445,9 @@ int eager_attention(const ExactAttnArgs& a, float* sbuf, int cap, hipStream_t st
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     if (G == 2) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
-        static bool attr[64] = {};   // function attributes are per device
+        const int dev = t5g_cur_device();
+        if (dev < 0) return -2;
+        static bool attr[T5G_MAX_DEVICES] = {};   // function attributes are per device
         if (!attr[dev]) {
             (void)hipFuncSetAttribute((const void*)eager_pv_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)(2 * EA_MAXK * sizeof(float)));

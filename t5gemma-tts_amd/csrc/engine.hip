@@ -93,6 +93,7 @@ struct t5g_engine {
     unsigned* aftick = nullptr; // [B][Hkv]
     int B = 0;            // rows of the current call
     int text_max = 0;     // longest text of the current call (host hint; 0: max_text)
+    int audio_max = 0;    // key bound of the current call's rows (host hint; 0: max_audio)
     const bf16_t* noise = nullptr;
     int noise_steps = 0;
     const uint32_t* noise_mt = nullptr;   // parity mode: raw MT19937 outputs [B][noise_mt_steps][2 V] (noise.hip)
@@ -409,32 +410,6 @@ static int xlin16_dec_parts(t5g_engine* e, const bf16_t* X16, int M, const bf16_
     return T5G_OK;
 }
 
-// VALU exact Linear (exact.hip), kept for the A/B entry point t5g_exact_linear
-[[maybe_unused]] static int xlin(t5g_engine* e, const bf16_t* X, int ldx, int M, const void* W, int N, int K, const void* bias,
-                void* Y, int ldy, int epi, const int* tok_row, const int* row_len, int nref_a, int nref_b,
-                int nsplit_col, hipStream_t st) {
-    ExactLinArgs a;
-    memset(&a, 0, sizeof(a));
-    a.X = X;
-    a.ldx = ldx;
-    a.M = M;
-    a.W = (const bf16_t*)W;
-    a.N = N;
-    a.NG = ng_pad(N);
-    a.KB = K / 32;
-    a.bias = (const bf16_t*)bias;
-    a.Y = Y;
-    a.ldy = ldy;
-    a.tok_row = tok_row;
-    a.row_len = row_len;
-    a.kb_a = ksplit_tab(e, nref_a, K);
-    a.kb_b = nref_b ? ksplit_tab(e, nref_b, K) : nullptr;
-    a.nsplit_col = nsplit_col;
-    a.kb_len = REF_KSPLIT_MAX_M;
-    a.gelu_lut = e->gelu_lut_dev;
-    return exact_linear(a, epi, st);
-}
-
 // fr (decode only, exact_attention_decode_supported): RoPE fused into the scores launch --
 // Q un-rotated, rotated with the step's table; with kv_new also the new key / value appended
 struct XattnFuse {
@@ -666,6 +641,7 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
             XattnFuse fr;
             fr.rope_tab = e->rope_tab;
             fr.kv_new = e->qkv;
+            fr.span_max = e->audio_max;   // the call's key bound (0: max_audio)
             fr.ld_new = e->qkv_dim;
             fr.k_col0 = e->q_dim;
             fr.v_col0 = e->q_dim + e->kv_dim;
@@ -860,6 +836,20 @@ extern "C" int t5g_encode(t5g_engine* e, int32_t B, int32_t ntok, const int32_t*
     hipStream_t st = (hipStream_t)stream;
     const int d = c.hidden, f = c.intermediate, D = c.head_dim;
     HIPCHK(hipMemcpyAsync(e->enc_len, text_len, B * sizeof(int), hipMemcpyDeviceToDevice, st));
+    if (e->text_max > 0) {
+        // t5g_engine_set_text_max is a host hint that selects one-launch cross attention
+        // over <= 64 keys: a stale hint below a row's real text length would silently
+        // truncate that row's keys, so check it against the lengths once per call
+        std::vector<int> lens(B);
+        HIPCHK(hipMemcpyAsync(lens.data(), text_len, B * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int b = 0; b < B; ++b)
+            if (lens[b] > e->text_max) {
+                fprintf(stderr, "[t5gtts] text length %d of row %d > t5g_engine_set_text_max hint %d\n", lens[b], b,
+                        e->text_max);
+                return T5G_EINVAL;
+            }
+    }
     if (e->exact) return encode_exact(e, ntok, ids, tok_row, tok_t, pos, st);
     for (int l = 0; l < c.n_enc_layers; ++l) {
         const t5g_layer_weights& L = e->enc[l];
@@ -978,6 +968,7 @@ static int decode_attention(t5g_engine* e, int M, const bf16_t* K, const bf16_t*
     a.ldo = e->q_dim;
     a.chunk = 64;
     a.nsplit = (cap + 63) / 64;
+    if (append && e->audio_max > 0 && e->audio_max < cap) a.nsplit = (e->audio_max + 63) / 64;   // self: the call's rows
     a.kv_cap = cap;
     a.sbuf = e->asbuf;
     a.mbuf = e->ambuf;
@@ -1435,7 +1426,10 @@ static SamplerArgs sampler_args(t5g_engine* e, const bf16_t* logits, int ld, int
     s.progress_scale = e->c.progress_scale;
     s.out_tokens = e->out_tokens;
     s.max_gen = e->c.max_gen;
-    s.max_len = e->c.max_audio;
+    // rows are force-stopped at the call's key bound (the decode attention grid covers
+    // exactly that many keys); the host sets it at or above every row's prompt + budget,
+    // so it never stops a row the reference would have run on
+    s.max_len = e->audio_max > 0 ? e->audio_max : e->c.max_audio;
     s.kv_len = e->kv_len;
     s.next_pos = e->next_pos;
     s.next_token = e->next_token;
@@ -1550,6 +1544,15 @@ extern "C" int t5g_engine_set_text_max(t5g_engine* e, int32_t n) {
     const int after = n > 0 ? n : e->c.max_text;
     if ((before <= 64) != (after <= 64)) drop_graphs(e);   // the decode layout baked into the graphs follows it
     e->text_max = n;
+    return T5G_OK;
+}
+
+extern "C" int t5g_engine_set_audio_max(t5g_engine* e, int32_t n) {
+    if (!e || n < 0 || n > e->c.max_audio) return T5G_EINVAL;
+    const int before = e->audio_max > 0 ? e->audio_max : e->c.max_audio;
+    const int after = n > 0 ? n : e->c.max_audio;
+    if ((before + 63) / 64 != (after + 63) / 64 || before != after) drop_graphs(e);   // grid + stop rule in the graphs
+    e->audio_max = n;
     return T5G_OK;
 }
 
@@ -1803,7 +1806,8 @@ extern "C" int t5g_attention_decode_flash(const t5g_attn_decode_args* g, void* s
 
 static int attention_decode_abi(const t5g_attn_decode_args* g, bool flash, void* stream) {
     if (!g || !g->q || !g->k_cache || !g->v_cache || !g->kv_len || !g->out || !g->work) return T5G_EINVAL;
-    if (g->B <= 0 || g->n_kv_heads <= 0 || g->n_heads % g->n_kv_heads || g->cap <= 0 || g->cap > 4096)
+    if (g->B <= 0 || g->n_kv_heads <= 0 || g->n_heads % g->n_kv_heads || g->cap <= 0 ||
+        g->cap > SDPA_KV_BLOCK * SDPA_MAX_BLOCKS)
         return T5G_EINVAL;
     AttnArgs a;
     memset(&a, 0, sizeof(a));

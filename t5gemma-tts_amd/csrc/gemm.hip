@@ -695,11 +695,13 @@ static int try_dx(const GemmArgs& a, int epi, hipStream_t st, int* rc) {
     if (per < 18 || a.M * per * 4 > 256 * RG * ((DX_XCH + RG - 1) / RG) || a.NG % RG) return 0;
     const size_t shm = (size_t)a.M * (per * 32 + 8) * sizeof(bf16_t);
     auto* fn = gemm_dx_kernel<2, RG, EPI_F32>;
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[T5G_MAX_DEVICES] = {};
+    const int dev = t5g_cur_device();
+    if (dev < 0) return 0;
+    if (!attr[dev]) {
         if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) != hipSuccess)
             return 0;
-        attr = true;
+        attr[dev] = true;
     }
     if (shm > 96 * 1024) return 0;
     hipLaunchKernelGGL(fn, dim3((unsigned)(a.NG / RG), (unsigned)a.splits), dim3(256 * RG), shm, st, a);

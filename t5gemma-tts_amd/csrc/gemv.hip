@@ -322,14 +322,15 @@ __global__ __launch_bounds__(NW * 64) void gemv_rx_kernel(DecGemmArgs a) {
 constexpr size_t GD_LDS_MAX = 160 * 1024;   // gfx950: 160 KB LDS per workgroup
 
 static int cu_count() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
+    static int n[T5G_MAX_DEVICES] = {};
+    const int dev = t5g_cur_device();
+    if (dev < 0) return 256;
+    if (!n[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        n[dev] = v;
     }
-    return n;
+    return n[dev];
 }
 
 // blocks of one launch: <= one per CU (the X rows are staged once per block)
@@ -343,10 +344,11 @@ static int gd_grid(const DecGemmArgs& a, int rg) {
 template <int NW, int RG, int EPI, int UN>
 static void launch_gd_un(const DecGemmArgs& a, size_t shm, hipStream_t st) {
     auto* fn = gemv_dec_kernel<NW, RG, EPI, UN>;
-    static bool attr = false;   // one opt-in per instantiation (not a stream operation)
-    if (!attr) {
+    static bool attr[T5G_MAX_DEVICES] = {};   // one opt-in per instantiation and device
+    const int dev = t5g_cur_device();
+    if (dev >= 0 && !attr[dev]) {
         (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GD_LDS_MAX);
-        attr = true;
+        attr[dev] = true;
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)gd_grid(a, RG), (unsigned)a.splits), dim3(NW * 64), shm, st, a);
 }
@@ -399,10 +401,11 @@ static int launch_rx_nw(const DecGemmArgs& a, hipStream_t st) {
         all = a.un == -1 && umax <= 5;
         if (all) fn = gemv_rx_kernel<NW, MT, EPI, SPU, 5>;
     }
-    static bool attr[2] = {false, false};
-    if (!attr[all]) {
+    static bool attr[T5G_MAX_DEVICES][2] = {};
+    const int dev = t5g_cur_device();
+    if (dev >= 0 && !attr[dev][all]) {
         (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GD_LDS_MAX);
-        attr[all] = true;
+        attr[dev][all] = true;
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid, (unsigned)a.splits), dim3(NW * 64), shm, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;

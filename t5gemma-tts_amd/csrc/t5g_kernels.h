@@ -277,9 +277,12 @@ __host__ __device__ inline long x16_off(long m, int k, int KB) {
     const int kb = k >> 5, e = k & 31, p = e >> 1, t = p >> 2, q = p & 3;
     return ((((m >> 4) * KB + kb) * 4 + q) * 16 + (m & 15)) * 8 + t * 2 + (e & 1);
 }
-// torch CPU SDPA kv blocks (common.h sdpa_*): keys per block, blocks per row (kv_cap <= 4096)
+// torch CPU SDPA kv blocks (common.h sdpa_*): keys per block, blocks per row. 24 blocks =
+// 12 288 keys: the reference's longest call -- a 100 s prompt (5 003 prefill tokens,
+// inference_commandline_hf.py:91) plus the 120 s duration cap (duration_estimator.py:79)
 constexpr int SDPA_KV_BLOCK = 512;
-constexpr int SDPA_MAX_BLOCKS = 16;   // 8 192 keys
+constexpr int SDPA_MAX_BLOCKS = 24;   // 12 288 keys
+constexpr int DEC_MAX_CHUNKS = SDPA_KV_BLOCK * SDPA_MAX_BLOCKS / 64;   // 64-key decode chunks per row
 
 struct ExactAttnArgs {
     const bf16_t* Q;          // [Mq][ldq] RoPE'd queries

@@ -441,7 +441,10 @@ int exact_attention_decode(const ExactAttnArgs& a, float* sbuf, float* mbuf, int
     if (a.q_pos || a.q_len) return -1;   // one query per row, at its last key
     if (a.kv_new && !a.rope_tab) return -1;
     const int G = a.Hq / a.Hkv;
-    const int nsplit = (cap + XD_CH - 1) / XD_CH;
+    // the grid covers the call's key bound (span_max: host hint on every row's keys, the
+    // sampler force-stops rows there; 0: the cache capacity)
+    const int span_b = a.span_max > 0 ? min(a.span_max, cap) : cap;
+    const int nsplit = (span_b + XD_CH - 1) / XD_CH;
     if ((cap + SDPA_KV_BLOCK - 1) / SDPA_KV_BLOCK > SDPA_MAX_BLOCKS) return -1;
     if (G == 2 && a.D == 256) launch_xd<2, 256>(a, sbuf, mbuf, cap, nsplit, st);
     else if (G == 2 && a.D == 128) launch_xd<2, 128>(a, sbuf, mbuf, cap, nsplit, st);

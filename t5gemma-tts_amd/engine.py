@@ -29,7 +29,7 @@ from .noise import DeviceNoise
 from .weights import check_state_dict
 
 BF16 = torch.bfloat16
-FAST_MAX_AUDIO = 4096   # fast decode attention: <= 64 chunks of 64 keys (csrc/attn.hip)
+MAX_AUDIO = 12288   # cache capacity of both kernel sets: 24 aten kv blocks of 512 keys (t5g_kernels.h)
 
 
 @dataclass
@@ -99,6 +99,9 @@ class T5GemmaTTSEngine:
         self.bb = bb = cfg.backbone
         self.device = torch.device(device)
         self.V = cfg.n_audio_tokens
+        if not 0 < max_audio <= MAX_AUDIO:
+            raise ValueError(f"max_audio {max_audio} outside 1..{MAX_AUDIO} (the decode attention kernels' capacity: "
+                             "a 100 s prompt plus the 120 s duration cap)")
         self.max_batch, self.max_text, self.max_audio = max_batch, max_text, max_audio
         self.max_gen = max_gen or max_audio
         dev = self.device
@@ -303,11 +306,6 @@ class T5GemmaTTSEngine:
             raise ValueError("parity mode restates eager attention (attn_implementation='eager', logit softcap) "
                              "for 8 query heads of head_dim 256 only (the reference's oneDNN picks its matmul "
                              "kernels by shape): run with parity=False (fast kernels, tolerance parity)")
-        if not exact and self.max_audio > FAST_MAX_AUDIO:
-            # the fast decode attention takes at most 64 chunks of 64 keys (csrc/attn.hip);
-            # the exact launches reach SDPA_MAX_BLOCKS x 512 keys
-            raise ValueError(f"max_audio {self.max_audio} > {FAST_MAX_AUDIO}: the fast decode attention's capacity; "
-                             "use parity=True (exact kernels, up to 8192 keys) or a smaller max_audio")
         if exact:
             for u in utts:
                 n_y = len(u.y) + 1
@@ -451,13 +449,19 @@ class T5GemmaTTSEngine:
         d_alen, d_last = torch.tensor(alen, **i32), torch.tensor(last, **i32)
         L = self.L
         _lib.check(L.t5g_engine_set_text_max(self.h, max(tlen)), "set_text_max")
+        # the call's key bound (every row's prompt + budget, in 512-key steps so repeated
+        # calls keep the captured graphs): the decode attention grids cover it, not max_audio
+        key_bound = min(self.max_audio, -(-(max(a + b for a, b in zip(alen, budgets)) + 1) // 512) * 512)
+        _lib.check(L.t5g_engine_set_audio_max(self.h, key_bound), "set_audio_max")
         if parity:
             # the reference's multinomial draws, one stream step per sampler call (up to the row
             # budget, plus the step at which a cap forces EOS): MT19937 streams generated on a
             # side stream (csrc/noise.hip) while the encoder and prefill run
-            self._noise.generate(seeds[:B], max_steps + 1, self.max_gen + 1,
-                                 snapshots=isinstance(seeds[0], torch.Generator))
-            _lib.check(L.t5g_engine_set_noise_mt(self.h, C.c_void_p(self._noise.raw.data_ptr()), self.max_gen + 1),
+            # buffer rows sized from this call's steps (2 V int32 per step and row: 0.5 MB),
+            # in power-of-two buckets so repeated calls keep the captured graphs' pointer
+            cap = min(self.max_gen + 1, max(64, 1 << (max_steps + 1 - 1).bit_length()))
+            self._noise.generate(seeds[:B], max_steps + 1, cap, snapshots=isinstance(seeds[0], torch.Generator))
+            _lib.check(L.t5g_engine_set_noise_mt(self.h, C.c_void_p(self._noise.raw.data_ptr()), cap),
                        "set_noise_mt")
         else:
             _lib.check(L.t5g_engine_set_noise_mt(self.h, None, 0), "set_noise_mt")
@@ -473,7 +477,7 @@ class T5GemmaTTSEngine:
                                        None, 0, stream), "sampler_setup")
         if parity:
             self._noise.wait()   # the first sampler call reads the draws
-        return {"B": B, "rows": rows, "tk": tk, "sl": sl, "y_rows": y_rows, "budgets": budgets,
+        return {"B": B, "rows": rows, "tk": tk, "sl": sl, "y_rows": y_rows, "budgets": budgets, "key_bound": key_bound,
                 "max_steps": max_steps, "steps": 0, "ambiguous_fixed": 0, "rec": None,
                 "cur": (_lib.SamplerState * B)(), "keep": (d_ids, d_trow, d_tt, d_tpos, d_tlen, d_aid, d_arow, d_at,
                                                           d_apos, d_alen, d_last)}
@@ -528,7 +532,7 @@ class T5GemmaTTSEngine:
                     _lib.check(L.t5g_host_sample(
                         _ptr(lg[b].contiguous()), self.V, C.byref(rows[b]), tk, sl, C.byref(st_in), _ptr(nz), eos,
                         self._cfg.eos_guard, self._cfg.budget_extra, self._cfg.text_guard,
-                        self._cfg.progress_scale, self.max_gen, self.max_audio, C.byref(out_st), C.byref(tok)),
+                        self._cfg.progress_scale, self.max_gen, ctx["key_bound"], C.byref(out_st), C.byref(tok)),
                         "host_sample")
                     out_st.ambiguous_steps = st_in.ambiguous_steps + 1
                     _lib.check(L.t5g_write_state(self.h, C.byref(out_st), b, st_in.cur_num_gen, tok.value, stream),

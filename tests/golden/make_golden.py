@@ -383,6 +383,15 @@ def gen_config_goldens(RT, which):
         cfgl = named_config("2b2b", **kw)
         x, y, _ = make_batch(cfgl, 1, seed=20251232, T_x=60, T_p=4100)[0]
         gen_cases_golden(RT, "golden_longprompt4k", [_row_case(x, y, len(y) + 1, 4700)], kw)
+    if "longprompt5k" in which:
+        # the reference CLI's longest prompt: cut_off_sec = 100 (inference_commandline_hf.py:91,
+        # 181) -> 5 001 codes + y_sep (a 5 003-token prefill), with a 90 s target
+        # (tgt_y_lens = T_p + 4 500: estimated length 9 503, past round 4's RoPE table) and a
+        # negative extra_cutoff (exact in binary) so the time budget stops the row after 7 steps
+        kw = {"extra_cutoff": -89.875}
+        cfgl = named_config("2b2b", **kw)
+        x, y, _ = make_batch(cfgl, 1, seed=20251233, T_x=60, T_p=5002)[0]
+        gen_cases_golden(RT, "golden_longprompt5k", [_row_case(x, y, len(y) + 4500, 4800)], kw)
     if "longprompt2k" in which:   # a 2 001-token prefill: the K-split table past M = 1 024
         steps = 8
         kw = {"extra_cutoff": (steps - 2) / 50.0}
@@ -459,7 +468,8 @@ if __name__ == "__main__":
         gen_full_golden(RT)
     if "long" in todo:
         gen_long_golden(RT)
-    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt", "longprompt2k", "longprompt4k", "eager2b", "eager2b_long")]
+    cfg_todo = [t for t in todo if t in ("c1", "c2", "c4", "longprompt", "longprompt2k", "longprompt4k", "longprompt5k",
+                                        "eager2b", "eager2b_long")]
     if cfg_todo:
         gen_config_goldens(RT, cfg_todo)
     if "mid" in todo:

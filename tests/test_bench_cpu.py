@@ -57,18 +57,14 @@ def test_cli_flags(monkeypatch):
 
 
 def test_cpu_baseline_tiny():
-    """The stratified CPU sample runs end to end on a tiny model (and reports its sample)."""
+    """The CPU baseline times one whole utterance end to end on a tiny model (and reports its
+    sample)."""
     import bench
     from t5gemma_tts_amd.config import named_config
     from t5gemma_tts_amd.weights import synthetic_weights
     cfg = named_config("tiny")
     sd = synthetic_weights(cfg, 7)
-    old = bench.CPU_SAMPLE_LENS
-    bench.CPU_SAMPLE_LENS = (40, 60)
-    try:
-        x = [5, 6, 7, 8, 9]
-        y = [1, 2, 3, cfg.y_sep_token]
-        r = bench.cpu_baseline(cfg, sd, (x, y, len(y) + 20), 30)
-    finally:
-        bench.CPU_SAMPLE_LENS = old
-    assert r["value"] > 0 and r["kind"] == "port" and "fitted" in r["sample"]
+    x = [5, 6, 7, 8, 9]
+    y = [1, 2, 3, cfg.y_sep_token]
+    r = bench.cpu_baseline(cfg, sd, (x, y, len(y) + 20), 30)
+    assert r["value"] > 0 and r["kind"] == "port" and "timed whole" in r["sample"]

@@ -230,7 +230,8 @@ def test_rope_trig_matches_reference_host(rope_lib):
     inv = (1.0 / (10000.0 ** (torch.arange(0, 256, 2, dtype=torch.float) / 256))).numpy()
     rng = np.random.default_rng(5)
     pos = [np.array([0.0, 2000.0], np.float32)]
-    for e in [603, 2, 3, 4096] + rng.integers(2, 4097, size=40).tolist():
+    # lengths across the table's whole coverage (ROPE_EXC_MAX_LEN: 12 288)
+    for e in [603, 2, 3, 4096, 9503, _lib.ROPE_EXC_MAX_LEN] + rng.integers(2, _lib.ROPE_EXC_MAX_LEN + 1, size=40).tolist():
         t = torch.arange(e, dtype=torch.float32)
         pos.append(((t / (e - 1)) * 2000.0).numpy())
         pos.append(np.minimum(np.arange(e, dtype=np.float64) / float(e - 1) * 2000.0, 2000.0).astype(np.float32))

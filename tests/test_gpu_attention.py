@@ -72,7 +72,7 @@ def _run(L, B, lens, Hq=8, Hkv=4, D=256, causal=1, seed=0, flash=False):
     return got, q, K, V
 
 
-@pytest.mark.parametrize("L", [1, 63, 64, 65, 152, 527, 903, 1500, 2100])
+@pytest.mark.parametrize("L", [1, 63, 64, 65, 152, 527, 903, 1500, 2100, 6000])
 def test_self_attention_decode_vs_cpu_sdpa(L):
     """8 rows x 8 q heads / 4 kv heads x 256 (2b-2b), ragged lengths up to L: rows of > 64
     keys go through the two-launch path (scores, then P.V / combine: one pass for rows of
@@ -123,7 +123,10 @@ def test_cross_attention_decode_tx60():
     assert same >= 0.998, same
 
 
-@pytest.mark.parametrize("L,B", [(65, 8), (152, 8), (527, 8), (903, 8), (2100, 8), (527, 32)])
+@pytest.mark.parametrize("L,B", [(65, 8), (152, 8), (527, 8), (903, 8), (2100, 8), (527, 32),
+                                 # past 64 chunks of 64 keys: the combine's lanes own several
+                                 # chunks (a 100 s prompt + a 120 s target is ~11 250 keys)
+                                 (6000, 8), (12288, 4)])
 def test_self_attention_decode_flash(L, B):
     """The fast path's one-launch form (t5g_attention_decode_flash: per-chunk online-softmax
     partials, combined by the last chunk to arrive) against exact fp64 attention over the

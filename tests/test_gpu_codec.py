@@ -150,3 +150,36 @@ def test_full_size_batch_row_matches_oracle():
     assert rms <= RMS_TOL and mx <= MAX_TOL
     assert torch.equal(out[3], codec.decode(codes[3:4])[0])
     codec.close()
+
+
+@pytest.mark.timeout(600)
+def test_c5_codec_44k_at_size():
+    """BASELINE configs[4]'s codec leg at its own size (VERDICT r4 missing #3): the 44.1 kHz
+    head (882 samples per token, codec_44k) at full width, 32 ragged rows up to 751 frames
+    (a 10 s target + the extra_cutoff budget) in one decode. One row against the fp32 CPU
+    oracle (RMS <= 1e-4), every row against its own single-row decode (bitwise: the
+    batch never changes a row's samples), padding past each row's length zero."""
+    from oracle import xc2_oracle as xo
+    from t5gemma_tts_amd.codec import XCodec2Decoder, codec_44k, synthetic_codec_weights
+    cfg = codec_44k()
+    assert cfg.hop_length == 882
+    sd = synthetic_codec_weights(cfg, 44)
+    B, T = 32, 751
+    codec = XCodec2Decoder(cfg, sd, device="cuda:0", max_batch=B, max_frames=T)
+    g = torch.Generator().manual_seed(441)
+    codes = torch.randint(0, 65536, (B, T), generator=g)
+    lens = [T] + torch.randint(200, T + 1, (B - 1,), generator=g).tolist()
+    out = codec.decode(codes, lens=lens).cpu()
+    assert out.shape == (B, 1, T * 882) and torch.isfinite(out).all()
+    for b in range(B):
+        n = lens[b]
+        alone = codec.decode(codes[b:b + 1, :n])[0].cpu()
+        assert torch.equal(out[b, :, :n * 882], alone), b
+        assert torch.all(out[b, :, n * 882:] == 0), b
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    r = 5
+    ref = xo.decode(sd, codes[r:r + 1, :lens[r]], cfg)
+    rms, mx = _errs(out[r, :, :lens[r] * 882].numpy(), ref[0].numpy())
+    print(f"c5 codec 44k B{B}x{T} row {r} ({lens[r]} frames): RMS err {rms:.3e}, max {mx:.3e}")
+    assert rms <= RMS_TOL and mx <= MAX_TOL
+    codec.close()

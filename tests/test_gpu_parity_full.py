@@ -336,5 +336,36 @@ def test_sliding_window_long_prompt_golden():
     _write("parity_golden_longprompt4k_b1.json", rep)
     print(json.dumps(rep))
     assert rep["tokens_equal"] and rows[0][0] and rep["max_top64_ulps"] <= 1, rep
-    with pytest.raises(ValueError, match="fast decode attention"):   # its 4 096-key capacity
-        eng.generate([Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"])], p, seeds=[c["seed"]])
+    # the fast path serves the same 4 101-token prompt (its decode attention covers up to
+    # 192 chunks of 64 keys) and stops at the same budget
+    fast = eng.generate([Utterance(x=c["x"], y=c["y"], tgt_y_len=c["tgt"])], p, seeds=[c["seed"]])
+    assert len(fast["gen"][0]) == len(c["gen"]) and fast["gen"][0][-1].item() == cfg.eog_inference
+
+
+@pytest.mark.timeout(600)
+def test_fast_path_capacity_is_per_call():
+    """the fast path's capacity is the call's, not the engine's. An engine
+    sized for the reference's longest request (12 288 keys: a 100 s prompt + the 120 s
+    duration cap) serves a C3 batch of 8 (T_x 60, T_p 151, 751 tokens per row) on the fast
+    kernels with tokens identical to an engine of 1 024 keys (the decode grids and the stop
+    rule follow the call's key bound, t5g_engine_set_audio_max)."""
+    _need_gpu()
+    import bench
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import SamplingParams, T5GemmaTTSEngine, Utterance
+    from t5gemma_tts_amd.weights import synthetic_weights
+    cfg = named_config("2b2b", extra_cutoff=5.0)
+    sd = synthetic_weights(cfg, 13, device="cuda")
+    rows = bench.make_batch(cfg, 8, seed=20251226)
+    utts = [Utterance(x=x, y=y, tgt_y_len=t) for x, y, t in rows]
+    p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, eos_disabled=True)
+    outs = []
+    for cap in (1024, 12288):
+        eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=8, max_text=64, max_audio=cap, max_gen=800)
+        outs.append(eng.generate(utts, p, seeds=list(range(100, 108))))
+        eng.close()
+        del eng
+        torch.cuda.empty_cache()
+    for b in range(8):
+        assert len(outs[0]["gen"][b]) == 751
+        assert torch.equal(outs[0]["gen"][b], outs[1]["gen"][b]), b

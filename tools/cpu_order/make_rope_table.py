@@ -26,13 +26,13 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 OUT = os.path.join(REPO, "t5gemma-tts_amd", "data", "rope_trig_exc.bin")
-E_MAX = 8192
+E_MAX = 12288   # a 100 s prompt (5 003 tokens) + the 120 s duration cap (duration_estimator.py:79)
 SCALE = 2000.0
 
 
-def positions(e_max: int) -> np.ndarray:
+def positions(e_max: int, e_min: int = 2) -> np.ndarray:
     out = [np.array([0.0, SCALE], np.float32)]
-    for e in range(2, e_max + 1):
+    for e in range(max(2, e_min), e_max + 1):
         t = torch.arange(e, dtype=torch.float32)
         out.append(((t / (e - 1)) * SCALE).numpy())                       # encoder / prefill
         d = np.arange(e, dtype=np.float64) / float(e - 1) * SCALE          # decode (Python double)
@@ -49,9 +49,16 @@ def main():
     D, theta = bb.head_dim, bb.rope_theta
     inv = (1.0 / (theta ** (torch.arange(0, D, 2, dtype=torch.float) / D))).numpy()
     t0 = time.time()
-    pos = positions(E_MAX)
-    print(f"{pos.size} distinct positions ({time.time() - t0:.0f} s)", flush=True)
+    # --extend E0: keep the existing table (lengths <= E0) and add the angles of the lengths
+    # E0 < e <= E_MAX (the union is the table of every length <= E_MAX)
+    e0 = int(sys.argv[sys.argv.index("--extend") + 1]) if "--extend" in sys.argv else 0
     exc = {}
+    if e0:
+        old = np.fromfile(OUT, dtype="<u4").reshape(-1, 2)
+        exc = {int(k): int(v) for k, v in old}
+        print(f"extending the table of lengths <= {e0} ({len(exc)} exceptions)", flush=True)
+    pos = positions(E_MAX, e0 + 1 if e0 else 2)
+    print(f"{pos.size} distinct positions ({time.time() - t0:.0f} s)", flush=True)
     n_ang = 0
     for i, f in enumerate(inv):
         ang = np.unique((np.float32(f) * pos).astype(np.float32))   # fp32 products

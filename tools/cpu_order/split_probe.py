@@ -95,9 +95,13 @@ def main():
     ap.add_argument("--shapes", default="2b2b")
     ap.add_argument("--ms", default="1,2,8,13,20,32,40,42,43,48,60,64,65,100,128,152,200,256,257,300,512",
                     help="comma list, or lo-hi for a range")
+    ap.add_argument("--only", default="", help="N,K of one shape of the set (resume a run)")
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
-    for N, K in SHAPES[args.shapes]:
+    shapes = SHAPES[args.shapes]
+    if args.only:
+        shapes = [tuple(int(v) for v in args.only.split(","))]
+    for N, K in shapes:
         cands = sorted({K} | {K // d for d in (2, 3, 4, 6, 8, 9, 12, 16) if K % d == 0 and (K // d) % 32 == 0}, reverse=True)
         if "-" in args.ms:
             lo, hi = (int(v) for v in args.ms.split("-"))
