@@ -302,6 +302,27 @@ def main():
         torch.cuda.synchronize(dev)
         dtp = time.perf_counter() - tp0
         gen_tokens[0] = saved
+        # roofline of the parity path's dominant kernel: the exact decode Linear (xmm_dec_kernel,
+        # 62 % of a parity step), the six launches of one layer timed with HIP events on the
+        # launching stream, layers rotated (every launch streams its weights from HBM)
+        import ctypes as C
+        from t5gemma_tts_amd import _lib
+        us_x = C.c_float()
+        _lib.check(_lib.lib().t5g_time_exact_linears(eng.h, B, 26 * 8,
+                                                     C.c_void_p(torch.cuda.current_stream(dev).cuda_stream),
+                                                     C.byref(us_x)), "time_exact_linears")
+        xbytes = _lib.exact_linears_bytes(B, cfg.backbone)
+        pmc_x = os.path.join(REPO, "profiles", "r05_pmc_exact_linears.json")
+        traffic_x = None
+        if os.path.exists(pmc_x) and B == 8:
+            traffic_x = json.load(open(pmc_x)).get("hbm_bytes_per_layer")
+        ach_x = xbytes / (us_x.value * 1e-6) / 1e9
+        parity_roof = {"bound": "hbm", "achieved": round(ach_x, 1), "peak": 8000.0, "unit": "GB/s",
+                       "frac": round(ach_x / 8000.0, 4), "traffic": traffic_x,
+                       "kernel": "xmm_dec_kernel: one layer's six exact decode Linears (q|k|v, o, cross-q, cross-o, "
+                                 "gate/up + GeGLU, down in the reference's K parts; f32 MFMA in the reference "
+                                 "host's fp32 orders), 174.6 MB of weights",
+                       "algorithmic_bytes": int(xbytes), "avg_us": round(us_x.value, 2)}
         parity_line = {
             "value": round(parity_stats["tokens"] / dtp, 2), "unit": "audio tokens/s",
             "ms_per_step": round(dtp / args.parity_steps * 1e3, 2), "steps": args.parity_steps,
@@ -310,6 +331,7 @@ def main():
             "mode": "parity (the drop-in default of inference_tts): exact-order kernels (logits bitwise the "
                     "reference CPU run's), the reference's MT19937 multinomial draws generated on the GPU, "
                     "torch.sort tie order on the GPU, EOS accepted; same workload and rows",
+            "roofline": parity_roof,
         }
 
     # ---- roofline of the dominant kernel: the fused decode-MLP launch (norm + gate/up +

@@ -335,6 +335,11 @@ int t5g_engine_poison_handoff(t5g_engine* e, uint32_t code);
 /* Average device time (us, hipEvents on `stream`) of the fused decode-MLP launch at B rows,
  * rotating over the decoder layers (bench.py roofline leg; no reference equivalent). */
 int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us);
+/* Parity mode (after t5g_engine_set_exact(e, 1, ...) and one parity call): average device time
+ * (us, hipEvents on `stream`) of one decoder layer's six exact decode Linear launches at B
+ * rows (q|k|v, o, cross-q, cross-o, gate/up + GeGLU, down in the reference's K parts), layers
+ * rotated (bench.py's parity roofline; no reference equivalent). */
+int t5g_time_exact_linears(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us);
 
 /* --- parity mode (csrc/exact.hip) ------------------------------------------------
  * Switch an engine to the exact-order kernels: every Linear, RMSNorm mean, q.k / P.V of
@@ -416,6 +421,10 @@ int t5g_engine_set_tanh_lut(t5g_engine* e, const uint16_t* lut_host);
 int t5g_mt_stream(const uint32_t* init_dev, int32_t B, int64_t n_out, int64_t out_stride, uint32_t* out_dev,
                   int64_t snap_every, int32_t n_snap, uint32_t* snap_dev, void* stream);
 int t5g_mt_exponential(const uint32_t* raw_dev, int64_t n, void* q_dev, void* stream);
+/* Test hook: y_dev[i] = std::exp(x_dev[i]) as the exact attention kernels evaluate it -- the
+ * reference host's glibc 2.35 expf (aten's flash-attention rescale exp(m_old - m) and block
+ * tails), restated in csrc/common.h sdpa_expf; fp32 device arrays of n values. */
+int t5g_sdpa_expf(const float* x_dev, float* y_dev, int64_t n, void* stream);
 int t5g_engine_set_noise_mt(t5g_engine* e, const uint32_t* raw_dev, int32_t steps);
 /* Host build of the sampler's sparse emulation of torch.sort's tie order (csrc/sort_emu.h;
  * replaces the reference's torch.sort in top_k_top_p_filtering, :107-108, for the order of

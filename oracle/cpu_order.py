@@ -260,7 +260,7 @@ def sdpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, is_cau
                 mn = torch.maximum(mt, S.max(-1).values)
                 p = E.block_p(S - mn[:, None], blen)
                 ts = E.block_sum(p)
-                et = torch.where(torch.isinf(mt), torch.zeros_like(mt), torch.exp((mt - mn).double()).float())
+                et = torch.where(torch.isinf(mt), torch.zeros_like(mt), E.expf(mt - mn))
                 l = E._fma(et, torch.from_numpy(l), ts).numpy()
                 pb = p.to(BF16).float().numpy()
                 init = None if dst is None else (dst * et.numpy()[:, None]).astype(f32)

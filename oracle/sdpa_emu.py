@@ -12,7 +12,9 @@ against torch 2.10 here (tests/test_sdpa_emu_cpu.py):
   with qs = 32 / 64 / 256 for Tq < 192 / < 768 / >= 768 (keys > t masked to -inf);
 * p = exp(s - m): the first (blen & ~15) keys of each block through at::vec's fast exp
   (``fexp`` below: x*log2e, floor, a cubic correction, exponent bits built by one
-  fma + truncation), the tail through double exp;
+  fma + truncation), the tail through std::exp(float) -- the host's glibc expf (``expf``
+  below, restated in oracle/glibc_expf.c; not correctly rounded: round 4 used the
+  correctly rounded value, which differed at one element of a 4 101-token prefill);
 * tmp_sum = 16 lane accumulators (key % 16, in order), xor-8/4/2/1 tree, then the tail in
   order; l = fma(expf(m_old - m), l_old, tmp_sum); dst = dst * expf(m_old - m) + bf16(p) . V;
 * out = bf16(dst * (1 / l)).
@@ -22,6 +24,11 @@ order differs in the last fp32 bit, which moves ~1e-4 of the bf16 outputs by one
 """
 from __future__ import annotations
 
+import ctypes
+import os
+import subprocess
+
+import numpy as np
 import torch
 
 BF16 = torch.bfloat16
@@ -29,6 +36,32 @@ F32, F64 = torch.float32, torch.float64
 _C = [torch.tensor(v, dtype=F32).double() for v in
       (-0.07920423895120621, -0.2243383675813675, 0.3035426139831543, 0.00010703434963943437)]
 _LOG2E = torch.tensor([0x3fb8aa3b], dtype=torch.int32).view(F32)[0]
+
+
+_EXPF = None
+
+
+def _expf_lib():
+    global _EXPF
+    if _EXPF is None:
+        here = os.path.dirname(os.path.abspath(__file__))
+        src, lib = os.path.join(here, "glibc_expf.c"), os.path.join(here, "lib", "liboracle_expf.so")
+        if not os.path.exists(lib) or os.path.getmtime(lib) < os.path.getmtime(src):
+            os.makedirs(os.path.dirname(lib), exist_ok=True)
+            subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-shared", "-fPIC", "-o", lib, src], check=True)
+        L = ctypes.CDLL(lib)
+        L.oracle_glibc_expf_v.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
+        _EXPF = L
+    return _EXPF
+
+
+def expf(x) -> torch.Tensor:
+    """std::exp on fp32 values as the reference host computes it (glibc 2.35 expf,
+    oracle/glibc_expf.c); fp32 tensor in, fp32 tensor out."""
+    a = np.ascontiguousarray(torch.as_tensor(x, dtype=F32).numpy(), dtype=np.float32)
+    out = np.empty_like(a)
+    _expf_lib().oracle_glibc_expf_v(a.ctypes.data, out.ctypes.data, a.size)
+    return torch.from_numpy(out)
 
 
 def _fma(a, b, c):
@@ -55,7 +88,7 @@ def block_p(d: torch.Tensor, blen: int) -> torch.Tensor:
     """p of one kv block: d = s - m [..., blen] (masked keys -inf)."""
     n16 = blen & ~15
     head = fexp(d[..., :n16])
-    tail = torch.exp(d[..., n16:].double()).float()
+    tail = expf(d[..., n16:].contiguous())
     return torch.cat([head, tail], dim=-1)
 
 
@@ -108,7 +141,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, i
             mn = torch.maximum(m, sb.max(dim=-1).values)
             p = block_p(sb - mn[..., None], blen)
             ts = block_sum(p)
-            et = torch.where(torch.isinf(m), torch.zeros_like(m), torch.exp((m - mn).double()).float())
+            et = torch.where(torch.isinf(m), torch.zeros_like(m), expf(m - mn))
             l = _fma(et, l, ts)
             pv = (p.to(BF16).double() @ v[:, bs:bs + blen].double()).float()
             dst = dst * et[..., None] + pv

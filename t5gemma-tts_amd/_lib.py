@@ -137,6 +137,7 @@ SIGNATURES = {
     "t5g_engine_set_audio_max": (C.c_int, [_P, _I]),
     "t5g_engine_poison_handoff": (C.c_int, [_P, C.c_uint32]),
     "t5g_time_decode_mlp": (C.c_int, [_P, _I, _I, _P, C.POINTER(_F)]),
+    "t5g_time_exact_linears": (C.c_int, [_P, _I, _I, _P, C.POINTER(_F)]),
     "t5g_exact_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
     "t5g_xmm_linear": (C.c_int, [_P, _I, _I, _P, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
     "t5g_pack_e16": (C.c_int, [_P, _P, _L, _P]),
@@ -145,6 +146,7 @@ SIGNATURES = {
     "t5g_exact_attention": (C.c_int, [_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
     "t5g_mt_stream": (C.c_int, [_P, _I, _L, _L, _P, _L, _I, _P, _P]),
     "t5g_mt_exponential": (C.c_int, [_P, _L, _P, _P]),
+    "t5g_sdpa_expf": (C.c_int, [_P, _P, _L, _P]),
     "t5g_engine_set_noise_mt": (C.c_int, [_P, _P, _I]),
     "t5g_sort_emu": (C.c_int, [_I, _I, _P, _P, _P]),
     "t5g_sort_emu_wave": (C.c_int, [_I, _I, _P, _P, _P, _P, _P]),
@@ -210,7 +212,7 @@ def gelu_erf_table():
 # the K-split table of the reference host's F.linear was measured for this many threads
 # and per-utterance token counts up to EXACT_MAX_TOKENS (csrc/ref_ksplit.h)
 EXACT_THREADS = 8
-EXACT_MAX_TOKENS = 5001
+EXACT_MAX_TOKENS = 6144   # >= 5 003: a 100 s prompt (inference_commandline_hf.py:91, 181) + y_sep + BOS
 
 _lib = None
 
@@ -242,6 +244,19 @@ FUSED_MLP_KERNEL = ("fused_mlp_kernel<1> (decode MLP half in one launch: cross-a
 FUSED_BLOCK_KERNEL = ("fused_block_kernel (decode layer after the self attention in one launch: "
                       "o-proj -> norm -> cross-q -> PM cross attention -> cross-o -> norm -> gate/up GeGLU -> down -> "
                       "norm -> next layer's q|k|v, 174.6 MB of weights)")
+
+
+def exact_linears_bytes(B: int, bb) -> int:
+    """Algorithmic HBM bytes of one decoder layer's six exact decode Linear launches at B rows
+    (bench.py parity roofline): every weight once (bf16) + each launch's B input rows and
+    B output rows (bf16; the down projection's fp32 K-part values)."""
+    d, f, qd, kvd = bb.hidden_size, bb.intermediate_size, bb.num_attention_heads * bb.head_dim, \
+        bb.num_key_value_heads * bb.head_dim
+    shapes = [(qd + 2 * kvd, d), (d, qd), (qd, d), (d, qd), (2 * f, d), (d, f)]
+    w = sum(2 * n * k for n, k in shapes)
+    io = 2 * B * (d + (qd + 2 * kvd)) + 2 * B * (qd + d) + 2 * B * (d + qd) + 2 * B * (qd + d) + 2 * B * (d + f) \
+        + (2 * B * f + 4 * 2 * B * d)
+    return w + io
 
 
 def fused_block_bytes(M: int, T_x: int, d: int = 2304, f: int = 9216, q_dim: int = 2048, kv_dim: int = 1024,

@@ -17,7 +17,7 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "lib", "libt5gtts.so")
 SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "fused.hip", "exact.hip", "xmm.hip", "xattn.hip", "eager.hip", "noise.hip", "xc2.hip", "xc2enc.hip", "whisper.hip", "host_sampler.cpp"]
-HEADERS = ["common.h", "t5g_kernels.h", "xc2_common.h", "exact_math.h", "ref_ksplit.h", "sort_emu.h"]
+HEADERS = ["common.h", "t5g_kernels.h", "xc2_common.h", "exact_math.h", "exact_dev.h", "ref_ksplit.h", "sort_emu.h"]
 ARCH = os.environ.get("T5G_ARCH", "gfx950")
 # -ffp-contract=off: HIP's default (fast-honor-pragmas) fuses a*b+c into one fma even
 # through __fmul_rn / __fsub_rn, which changes roundings the reference's CPU kernels keep
@@ -76,17 +76,25 @@ def build(force: bool = False, verbose: bool = True, dbg: bool = False) -> str:
 
 ORACLE_SRC = os.path.join(REPO, "oracle", "sort_order.cpp")
 ORACLE_LIB = os.path.join(REPO, "oracle", "lib", "liboracle_sort.so")
+ORACLE_EXPF_SRC = os.path.join(REPO, "oracle", "glibc_expf.c")
+ORACLE_EXPF_LIB = os.path.join(REPO, "oracle", "lib", "liboracle_expf.so")
+
+
+def _build_one(src: str, lib: str, cmd: list, force: bool) -> str:
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    if force or not os.path.exists(lib) or os.path.getmtime(lib) < os.path.getmtime(src):
+        r = subprocess.run(cmd + ["-o", lib, src], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"oracle build failed:\n{r.stderr[-4000:]}")
+    return lib
 
 
 def build_oracle(force: bool = False) -> str:
-    """Compile the oracle's C++ restatements (test infrastructure, g++) into oracle/lib/."""
-    os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
-    if force or not os.path.exists(ORACLE_LIB) or os.path.getmtime(ORACLE_LIB) < os.path.getmtime(ORACLE_SRC):
-        r = subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", ORACLE_LIB, ORACLE_SRC],
-                           capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"oracle build failed:\n{r.stderr[-4000:]}")
-    return ORACLE_LIB
+    """Compile the oracle's C / C++ restatements (test infrastructure: the std::sort tie
+    order, glibc's expf) into oracle/lib/. Returns the sort library's path."""
+    # -ffp-contract=off: the expf restatement's fused multiply-adds are explicit fma() calls
+    _build_one(ORACLE_EXPF_SRC, ORACLE_EXPF_LIB, ["gcc", "-O2", "-ffp-contract=off", "-shared", "-fPIC"], force)
+    return _build_one(ORACLE_SRC, ORACLE_LIB, ["g++", "-O2", "-std=c++17", "-shared", "-fPIC"], force)
 
 
 if __name__ == "__main__":

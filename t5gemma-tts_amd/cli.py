@@ -54,10 +54,20 @@ def _none(v) -> bool:
     return v is None or str(v).strip().lower() in {"", "none", "null"}
 
 
+# The reference CLI's extremes: a prompt cut at cut_off_sec = 100 s (inference_commandline_hf.py:91,
+# 181) and a target clamped at 120 s by the duration estimator (duration_estimator.py:79, 251).
+# The engine and codec are sized for them once; every call's work is sized by its own request
+# (the decode attention grids follow the call's key bound, engine.py key_bound).
+MAX_PROMPT_SECONDS = 100.0
+
+
 def load_codec(codec_dir: Optional[str] = None, codec: str = "44k", device="cuda:0", max_batch: int = 4,
-               max_frames: int = 4096, seed: int = 22):
+               max_frames: Optional[int] = None, seed: int = 22, max_encode_seconds: float = MAX_PROMPT_SECONDS):
     """XCodec2 decoder: from a local transformers ``Xcodec2Model`` directory, or seeded
-    synthetic weights of the named size."""
+    synthetic weights of the named size. ``max_frames`` (default: the engine's key capacity,
+    prompt + target codes) bounds one decode; ``max_encode_seconds`` one prompt encode."""
+    from .engine import MAX_AUDIO
+    max_frames = MAX_AUDIO if max_frames is None else max_frames
     from .codec import AudioTokenizer, CodecConfig, codec_16k, codec_44k, codec_tiny, synthetic_codec_weights
     from .codec_enc import EncoderConfig, encoder_16k, encoder_tiny, synthetic_encoder_weights
     if codec_dir:
@@ -76,13 +86,16 @@ def load_codec(codec_dir: Optional[str] = None, codec: str = "44k", device="cuda
         ecfg = encoder_tiny() if codec == "tiny" else encoder_16k()
         esd = synthetic_encoder_weights(ecfg, seed + 1)
     return AudioTokenizer(device=device, cfg=cfg, state_dict=sd, encoder_cfg=ecfg, encoder_state_dict=esd,
-                          max_batch=max_batch, max_frames=max_frames)
+                          max_batch=max_batch, max_frames=max_frames, max_encode_seconds=max_encode_seconds)
 
 
 def load_model(model_dir: Optional[str] = None, synthetic: Optional[str] = None, device="cuda:0",
-               max_text: int = 512, max_audio: int = 4096, seed: int = 7):
-    from .engine import T5GemmaVoiceForConditionalGeneration
-    kw = dict(device=device, max_batch=1, max_text=max_text, max_audio=max_audio)
+               max_text: int = 512, max_audio: Optional[int] = None, seed: int = 7):
+    """The voice model, sized for the reference CLI's longest request by default (max_audio =
+    engine.MAX_AUDIO keys: a 100 s prompt + the 120 s duration cap; 1.3 GB of KV cache at
+    batch 1) -- a shorter request runs on its own key bound, not the capacity."""
+    from .engine import MAX_AUDIO, T5GemmaVoiceForConditionalGeneration
+    kw = dict(device=device, max_batch=1, max_text=max_text, max_audio=MAX_AUDIO if max_audio is None else max_audio)
     if synthetic:
         from .config import named_config
         from .weights import synthetic_weights

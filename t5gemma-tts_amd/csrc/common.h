@@ -190,7 +190,7 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 // Per query row and per kv block of <= 512 keys (running max m over the blocks):
 //   p_j = exp(s_j - m): the first blen & ~15 keys of the block through at::vec's fast exp
 //         (sdpa_fexp, the constants of the shipped kernel), the remaining tail through
-//         double-precision exp;
+//         std::exp(float) = the host's glibc expf (sdpa_expf);
 //   tmp_sum = 16 lane accumulators (key % 16, in key order) -> xor 8/4/2/1 tree -> + tail
 //         in order (sdpa_block_sum); l = fma(expf(m_old - m), l_old, tmp_sum);
 //   out   = bf16(sum_j bf16(p_j) v_j (scaled by expf(m_old - m) per block) * (1 / l)).
@@ -206,7 +206,55 @@ __device__ __forceinline__ float sdpa_fexp(float x) {
     const float y = fmaf(__fsub_rn(t, q), 8388608.0f, 1065353216.0f);
     return __int_as_float((int)y);                          // cvttps2dq: truncate
 }
-__device__ __forceinline__ float sdpa_exp_tail(float x) { return (float)exp((double)x); }
+// std::exp(float) of aten's code = the reference host's glibc 2.35 expf (IFUNC FMA variant
+// of sysdeps/ieee754/flt-32/e_expf.c): 2^(k/32) from a 32-entry table times a cubic in r,
+// in double with fused multiply-adds. NOT correctly rounded (96 956 inputs of (-87, 0]
+// differ), so it is restated operation for operation; oracle/glibc_expf.c is the same
+// function, equal to the host's libm on all 2^32 inputs (tools/cpu_order/check_glibc_expf.c).
+__device__ __forceinline__ float sdpa_expf(float x) {
+    const uint32_t bits = __float_as_uint(x);
+    const uint32_t abstop = (bits >> 20) & 0x7ffu;
+    if (abstop > 0x42au) {   // |x| >= 88
+        if (bits == 0xff800000u) return 0.0f;
+        if (abstop > 0x7f7u) return x + x;
+        if (x > 0x1.62e42ep6f) return __int_as_float(0x7f800000);
+        if (x < -0x1.9fe368p6f) return 0.0f;
+        if (x < -0x1.9d1d9ep6f) return 0x1p-149f;
+    }
+    const double xd = (double)x;
+    const double InvLn2N = 0x1.71547652b82fep+5, SHIFT = 0x1.8p+52;
+    const double z = __fma_rn(InvLn2N, xd, SHIFT);
+    const uint64_t ki = (uint64_t)__double_as_longlong(z);
+    const double kd = __dsub_rn(z, SHIFT);
+    const double r = __fma_rn(InvLn2N, xd, -kd);
+    // 2^(i/32) - (i << 47) table entries (glibc __exp2f_data.tab), i = ki & 31
+    uint64_t tb;
+    switch ((int)(ki & 31)) {
+        case 0: tb = 0x3ff0000000000000ull; break;   case 1: tb = 0x3fefd9b0d3158574ull; break;
+        case 2: tb = 0x3fefb5586cf9890full; break;   case 3: tb = 0x3fef9301d0125b51ull; break;
+        case 4: tb = 0x3fef72b83c7d517bull; break;   case 5: tb = 0x3fef54873168b9aaull; break;
+        case 6: tb = 0x3fef387a6e756238ull; break;   case 7: tb = 0x3fef1e9df51fdee1ull; break;
+        case 8: tb = 0x3fef06fe0a31b715ull; break;   case 9: tb = 0x3feef1a7373aa9cbull; break;
+        case 10: tb = 0x3feedea64c123422ull; break;  case 11: tb = 0x3feece086061892dull; break;
+        case 12: tb = 0x3feebfdad5362a27ull; break;  case 13: tb = 0x3feeb42b569d4f82ull; break;
+        case 14: tb = 0x3feeab07dd485429ull; break;  case 15: tb = 0x3feea47eb03a5585ull; break;
+        case 16: tb = 0x3feea09e667f3bcdull; break;  case 17: tb = 0x3fee9f75e8ec5f74ull; break;
+        case 18: tb = 0x3feea11473eb0187ull; break;  case 19: tb = 0x3feea589994cce13ull; break;
+        case 20: tb = 0x3feeace5422aa0dbull; break;  case 21: tb = 0x3feeb737b0cdc5e5ull; break;
+        case 22: tb = 0x3feec49182a3f090ull; break;  case 23: tb = 0x3feed503b23e255dull; break;
+        case 24: tb = 0x3feee89f995ad3adull; break;  case 25: tb = 0x3feeff76f2fb5e47ull; break;
+        case 26: tb = 0x3fef199bdd85529cull; break;  case 27: tb = 0x3fef3720dcef9069ull; break;
+        case 28: tb = 0x3fef5818dcfba487ull; break;  case 29: tb = 0x3fef7c97337b9b5full; break;
+        case 30: tb = 0x3fefa4afa2a490daull; break;  default: tb = 0x3fefd0765b6e4540ull; break;
+    }
+    const double s = __longlong_as_double((long long)(tb + (ki << 47)));
+    const double p = __fma_rn(r, 0x1.c6af84b912394p-20, 0x1.ebfce50fac4f3p-13);
+    const double r2 = __dmul_rn(r, r);
+    double y = __fma_rn(r, 0x1.62e42ff0c52d6p-6, 1.0);
+    y = __fma_rn(p, r2, y);
+    return __double2float_rn(__dmul_rn(y, s));
+}
+__device__ __forceinline__ float sdpa_exp_tail(float x) { return sdpa_expf(x); }
 // p of block position `pos` of a block with `blen` keys
 __device__ __forceinline__ float sdpa_p(float x, int pos, int blen) {
     return pos < (blen & ~15) ? sdpa_fexp(x) : sdpa_exp_tail(x);
@@ -264,9 +312,10 @@ __device__ __forceinline__ float fast_score(float s, float scale, float softcap)
     }
     return __fmul_rn(s, scale);
 }
-// rescale of the previous blocks' sums when the running max grows (std::expf in aten)
+// rescale of the previous blocks' sums when the running max grows (std::exp(float) in aten:
+// the host's glibc expf, sdpa_expf)
 __device__ __forceinline__ float sdpa_block_rescale(float m_old, float m_new) {
-    return m_old == -INFINITY ? 0.f : (float)exp((double)__fsub_rn(m_old, m_new));
+    return m_old == -INFINITY ? 0.f : sdpa_expf(__fsub_rn(m_old, m_new));
 }
 // q-block split of aten's CPU flash attention: a causal query row t of a Tq-query call
 // sees keys [0, min(q0 + qsplit, Tk)) in its blocks (keys > t masked), q0 = t - t % qsplit

@@ -1399,6 +1399,12 @@ extern "C" int t5g_mt_stream(const uint32_t* init, int32_t B, int64_t n_out, int
     return T5G_OK;
 }
 
+extern "C" int t5g_sdpa_expf(const float* x, float* y, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && (!x || !y))) return T5G_EINVAL;
+    RC(sdpa_expf_array(x, y, (long)n, (hipStream_t)stream));
+    return T5G_OK;
+}
+
 extern "C" int t5g_mt_exponential(const uint32_t* raw, int64_t n, void* q, void* stream) {
     RC(mt_exponential(raw, (long)n, (bf16_t*)q, (hipStream_t)stream));
     return T5G_OK;
@@ -1739,6 +1745,48 @@ extern "C" int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, 
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     return check_handoff(e, st);
+}
+
+// hipEvent-timed exact decode Linears (parity mode's dominant kernel, xmm_dec_kernel): per
+// iteration the six launches of one decoder layer as the parity decode step runs them --
+// q|k|v, o, cross-q, cross-o (bf16 out), gate/up (GeGLU epilogue), down (K parts) -- on
+// the decode X16 buffers of B rows, layers rotated so every launch streams from HBM.
+// Average microseconds per layer (six launches) in *avg_us.
+extern "C" int t5g_time_exact_linears(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us) {
+    if (!e || iters <= 0 || !avg_us || B <= 0 || B > e->c.max_batch || !e->exact || !e->xmm_ready) return T5G_EINVAL;
+    const t5g_config& c = e->c;
+    const int d = c.hidden, f = c.intermediate;
+    hipStream_t st = (hipStream_t)stream;
+    auto layer = [&](int l) -> int {
+        const t5g_engine::XLayer& X = e->dec_x[l];
+        RC(xlin16(e, e->dxn16, B, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, nullptr,
+                  nullptr, e->q_dim, e->kv_dim, e->q_dim, st));
+        RC(xlin16(e, e->datt16, B, X.o, d, e->q_dim, nullptr, e->tmp, d, nullptr, EPI_BF16, nullptr, nullptr, d, 0, 0,
+                  st));
+        RC(xlin16(e, e->dxn16, B, X.cross_q, e->q_dim, d, nullptr, e->dq, e->q_dim, nullptr, EPI_BF16, nullptr,
+                  nullptr, e->q_dim, 0, 0, st));
+        RC(xlin16(e, e->datt16, B, X.cross_o, d, e->q_dim, nullptr, e->tmp, d, nullptr, EPI_BF16, nullptr, nullptr, d,
+                  0, 0, st));
+        RC(xlin16(e, e->dxn16, B, X.gate_up, 2 * f, d, nullptr, nullptr, f, e->dact16, EPI_GEGLU, nullptr, nullptr, f,
+                  0, 0, st));
+        int np = 0;
+        RC(xlin16_dec_parts(e, e->dact16, B, X.down, d, f, e->tmp, d, nullptr, &np, st));
+        return T5G_OK;
+    };
+    RC(layer(0));   // untimed: the first launch's one-time setup
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i) RC(layer(i % c.n_dec_layers));
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    *avg_us = ms * 1000.f / iters;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return T5G_OK;
 }
 
 // hipEvent-timed fused decode-MLP launches (bench.py roofline leg): layers rotated, so every

@@ -13,6 +13,7 @@
 //   out = pre_w ? bf16((h * (1/sqrt(mean(h^2)+eps))) * (1 + pre_w))   -> normed_out
 // Sums reduce in a fixed order, so results are run-to-run deterministic.
 #include "common.h"
+#include "exact_dev.h"
 #include "exact_math.h"
 #include "t5g_kernels.h"
 
@@ -49,81 +50,16 @@ __device__ __forceinline__ float block_sum_once(float v, float* red) {
     return s;
 }
 
-// Sum of squares in the order of torch 2.10's CPU float sum over a contiguous row
-// (exact / parity mode). aten SumKernel.cpp cascade_sum -> vectorized_inner_sum, AVX2
-// kernel (the AVX-512 stub is not registered): the row is a sequence of 8-float vectors
-// (thread c holds vector c); row_sum interleaves 4 vector accumulators (vector c ->
-// accumulator c % 4, row c / 4); multi_row_sum folds each accumulator's rows in a
-// cascade of 4 levels of 16 rows; accumulators 1..3 are added to 0, vectors past the last
-// whole row of 4 go to accumulator 0 first; finally the 8 lanes are summed in order.
-// Verified bit for bit against torch on random rows (tools/cpu_order).
-__device__ __forceinline__ float ref_sumsq(const float (&v)[8], bool active, int nvec, float* sq) {
-    const int c = threadIdx.x;
-    if (active) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sq[c * 8 + j] = __fmul_rn(v[j], v[j]);
-    }
-    __syncthreads();
-    if (c < 32) {
-        const int k = c >> 3, j = c & 7;
-        const int size_ilp = nvec / 4;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        int i = 0;
-        // each level-0 row of 16 is read into registers first (one LDS round trip, not 16
-        // dependent ones), then added in order
-        while (i + 16 <= size_ilp) {
-            float t[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) t[q] = sq[((i + q) * 4 + k) * 8 + j];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) a0 = __fadd_rn(a0, t[q]);
-            i += 16;
-            a1 = __fadd_rn(a1, a0);
-            a0 = 0.f;
-            if (i & 0xF0) continue;
-            a2 = __fadd_rn(a2, a1);
-            a1 = 0.f;
-            if (i & 0xF00) continue;
-            a3 = __fadd_rn(a3, a2);
-            a2 = 0.f;
-        }
-        {
-            float t[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) t[q] = sq[(min(i + q, max(size_ilp - 1, 0)) * 4 + k) * 8 + j];
-#pragma unroll
-            for (int q = 0; q < 16; ++q)
-                if (i + q < size_ilp) a0 = __fadd_rn(a0, t[q]);
-        }
-        a0 = __fadd_rn(__fadd_rn(__fadd_rn(a0, a1), a2), a3);
-        if (k == 0)
-            for (int t = size_ilp * 4; t < nvec; ++t) a0 = __fadd_rn(a0, sq[t * 8 + j]);
-        sq[nvec * 8 + c] = a0;
-    }
-    __syncthreads();
-    float lanes[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        lanes[j] = __fadd_rn(__fadd_rn(__fadd_rn(sq[nvec * 8 + j], sq[nvec * 8 + 8 + j]), sq[nvec * 8 + 16 + j]),
-                             sq[nvec * 8 + 24 + j]);
-    float tot = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) tot = __fadd_rn(tot, lanes[j]);
-    __syncthreads();   // sq is reused by the launch's second RMSNorm
-    return tot;
-}
-
 template <bool EXACT>
 __device__ __forceinline__ void rms8(float (&v)[8], bool active, int d, u32x4 w8, float eps, float* red, float* sq) {
-    float tot;
     if constexpr (EXACT) {
-        tot = ref_sumsq(v, active, d / 8, sq);
-    } else {
-        float ss = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
-        tot = block_sum_once(active ? ss : 0.f, red);
+        rms8_exact(v, active, d, w8, eps, sq);   // exact_dev.h (shared with xlayer.hip)
+        return;
     }
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+    const float tot = block_sum_once(active ? ss : 0.f, red);
     float r = 1.0f / sqrtf(tot / (float)d + eps);
     if (!active) return;
     float wf[8];

@@ -316,6 +316,7 @@ int exact_attention(const ExactAttnArgs& a, hipStream_t st);
 // decode (one query per row, at its last key): scores + P.V launches (xattn.hip) on the
 // scratch sbuf [Mq][Hq][cap] / mbuf [Mq][Hkv][ceil(cap / 64)][G]
 int exact_attention_decode(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, hipStream_t st);
+int sdpa_expf_array(const float* x, float* y, long n, hipStream_t st);
 bool exact_attention_decode_supported(int G, int D);   // head shapes the decode launches are built for
 // eager attention (attn_implementation="eager") in the reference host's order, eager.hip:
 // scores + softmax/P.V launches on the scratch sbuf [Mq][Hq][cap]; -3: not the measured shape

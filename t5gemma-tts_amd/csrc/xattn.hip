@@ -19,6 +19,7 @@
 //   by one thread per (head, dimension); output x 1/l, also written in the X16 layout of
 //   the o-projection (xmm.hip).
 #include "common.h"
+#include "exact_dev.h"
 #include "t5g_kernels.h"
 
 namespace t5g {
@@ -31,13 +32,6 @@ constexpr int XD_DZ = 32;    // output dims per P.V workgroup
 __device__ __forceinline__ void xd_range(const ExactAttnArgs& a, int row, int& lo, int& hi) {
     hi = a.kv_len[row];
     lo = (a.window > 0 && a.causal && hi >= a.window) ? hi - a.window : 0;
-}
-
-// RoPE of one rotation pair as rope_store_kernel computes it (attn.hip): the three bf16
-// tensor ops of apply_rotary_pos_emb
-__device__ __forceinline__ void xd_rope(float x1, float x2, float c, float sn, float& o1, float& o2) {
-    o1 = rbf(rbf(x1 * c) + rbf(-x2 * sn));
-    o2 = rbf(rbf(x2 * c) + rbf(x1 * sn));
 }
 
 // FUSE: the queries arrive un-rotated and are rotated while staged (rope_tab), and, with
@@ -429,6 +423,20 @@ static void launch_xd(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap,
     if (a.rope_tab) hipLaunchKernelGGL((xattn_scores_kernel<G, D, true>), gs, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
     else hipLaunchKernelGGL((xattn_scores_kernel<G, D, false>), gs, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
     hipLaunchKernelGGL((xattn_pv_kernel<G, D>), gp, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
+}
+
+// the softmax's std::exp(float) restatement (common.h sdpa_expf) over an array: the test hook
+// that pins it against the reference host's glibc expf (tests/test_gpu_exact.py)
+__global__ void sdpa_expf_kernel(const float* __restrict__ x, float* __restrict__ y, long n) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        y[i] = sdpa_expf(x[i]);
+}
+int sdpa_expf_array(const float* x, float* y, long n, hipStream_t st) {
+    if (n <= 0) return 0;
+    if (!x || !y) return -1;
+    const long blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(sdpa_expf_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, st, x, y, n);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 bool exact_attention_decode_supported(int G, int D) {

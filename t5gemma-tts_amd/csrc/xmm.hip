@@ -27,12 +27,11 @@
 //   where the reference splits K at M = 1: the down projection), its 8 waves split the
 //   chunks, chunk sums go through LDS, one thread per output folds them in order.
 #include "common.h"
+#include "exact_dev.h"
 #include "exact_math.h"
 #include "t5g_kernels.h"
 
 namespace t5g {
-
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 // ---- weight repack: E16[g][kb][lane (q, r)][t] = P16[g][kb][lane (t, r)][q] (u32 words)
 __global__ void pack_e16_kernel(const uint32_t* __restrict__ p16, uint32_t* __restrict__ e16, long n_words) {
@@ -79,20 +78,6 @@ __device__ __forceinline__ int xmm_kbc(const XmmArgs& a, int m, int n) {
     const uint16_t* tab = (a.kb_b && n >= a.nsplit_col) ? a.kb_b : a.kb_a;
     const int kbc = tab ? tab[min(max(mu, 1), a.kb_len) - 1] : a.KB;
     return kbc <= 0 ? a.KB : kbc;
-}
-
-// chunk sum of one 16 x 16 tile: E and O chains over the chunk, then E + O
-__device__ __forceinline__ f32x4_t xmm_chunk(const u32x4& w, const u32x4& x) {
-    f32x4_t e = {0.f, 0.f, 0.f, 0.f}, o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        e = __builtin_amdgcn_mfma_f32_16x16x4f32(bf_lo(w[t]), bf_lo(x[t]), e, 0, 0, 0);
-        o = __builtin_amdgcn_mfma_f32_16x16x4f32(bf_hi(w[t]), bf_hi(x[t]), o, 0, 0, 0);
-    }
-    f32x4_t c;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) c[i] = __fadd_rn(e[i], o[i]);
-    return c;
 }
 
 // fold state of one output element (the reference's part / total chain)

@@ -94,3 +94,41 @@ def test_run_inference_transcribes_reference_speech_with_whisper(tmp_path, monke
     from t5gemma_tts_amd.text import normalize_text_with_lang
     _, lang_code = normalize_text_with_lang("hi", None)
     assert seen and seen[0] == normalize_text_with_lang(text, lang_code)[0]
+
+
+@pytest.mark.timeout(900)
+def test_run_inference_accepts_reference_extremes(tmp_path):
+    """the drop-in CLI path accepts the reference's extremes -- a 100 s
+    reference clip (cut_off_sec = 100, inference_commandline_hf.py:91, 181: 5 001 codes, a
+    5 003-token prefill) and a 90 s target (4 500 frames + the extra_cutoff budget) -- on
+    the full-size 2b-2b model in parity mode (the default), through the XCodec2 encoder,
+    the engine and the 44.1 kHz decoder, with the CLI's default sizing (cli.load_codec)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import sys
+    from t5gemma_tts_amd import cli
+    from t5gemma_tts_amd.audio import write_wav
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import MAX_AUDIO, T5GemmaVoiceForConditionalGeneration
+    from t5gemma_tts_amd.weights import synthetic_weights
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "tests", "golden"))
+    from make_golden_codec_enc import test_wave
+    cfg = named_config("2b2b")
+    model = T5GemmaVoiceForConditionalGeneration(cfg, synthetic_weights(cfg, 7, device="cuda"), device="cuda:0",
+                                                 max_batch=1, max_text=512, max_audio=MAX_AUDIO)
+    codec = cli.load_codec(codec="44k", max_batch=1)
+    ref = str(tmp_path / "ref100s.wav")
+    write_wav(ref, test_wave(16000 * 100, 5), 16000)
+    out = cli.run_inference(reference_speech=ref, reference_text="a reference transcript of one hundred seconds",
+                            target_text="the target sentence that should take about ninety seconds to speak",
+                            target_duration=90.0, seed=1, dump_tokens=True, output_dir=str(tmp_path / "out"),
+                            model=model, audio_tokenizer=codec, text_tokenizer=cli.ByteTokenizer())
+    assert os.path.exists(out)
+    concat = np.load(str(tmp_path / "out" / "concat_frames.npy")).reshape(-1)
+    gen = np.load(str(tmp_path / "out" / "generated_frames.npy")).reshape(-1)
+    print(f"100 s prompt + 90 s target: concat {concat.size} frames, generated {gen.size}")
+    assert concat.size - gen.size == 16000 * 100 // 320 + 1        # the 5 001 prompt codes
+    # random weights may sample EOS before the time budget (the reference's stop rule); the
+    # budget of a 90 s target is the ceiling
+    assert 1 <= gen.size <= 4500 + 50 * cfg.extra_cutoff + 2

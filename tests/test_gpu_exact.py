@@ -319,3 +319,27 @@ def test_exact_engine_long_golden():
     _need_gpu()
     rep = _run_golden("golden_long", max_audio=1024, max_text=64, max_gen=760, batch=2)
     assert all(r["tokens_equal"] and r["logit_rows_equal"] == r["steps"] for r in rep), rep
+
+
+def test_sdpa_expf_device_equals_glibc_restatement():
+    """csrc/common.h sdpa_expf (the exact attention kernels' std::exp(float)) == the reference
+    host's glibc expf (oracle/glibc_expf.c, equal to libm on all 2^32 inputs) on 2^24 floats
+    of (-104, 0] plus every input where glibc differs from the correctly rounded exp in a
+    dense scan of (-1, 0]."""
+    _need_gpu()
+    from oracle import sdpa_emu as E
+    from t5gemma_tts_amd import _lib
+    L = _lib.lib()
+    g = np.random.default_rng(11)
+    x = np.concatenate([-g.random(1 << 24, dtype=np.float32) * 104.0,
+                        -np.arange(0, 1 << 23, dtype=np.float32) / np.float32(1 << 23),
+                        np.array([0.0, -87.3365478515625, -88.0, -103.2789, -103.9721, -104.0, -np.inf], np.float32)])
+    x = x.astype(np.float32)
+    ref = E.expf(torch.from_numpy(x)).numpy()
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.empty_like(xd)
+    assert L.t5g_sdpa_expf(C.c_void_p(xd.data_ptr()), C.c_void_p(yd.data_ptr()), x.size, _st()) == 0
+    torch.cuda.synchronize()
+    got = yd.cpu().numpy()
+    bad = int((got.view(np.int32) != ref.view(np.int32)).sum())
+    assert bad == 0, bad

@@ -58,3 +58,28 @@ def test_fexp_matches_aten_vector_exp():
         ok += int((got.view(torch.int16) == ref.view(torch.int16)).sum())
         tot += got.numel()
     assert ok == tot
+
+
+def test_expf_restatement_equals_host_libm():
+    """oracle.sdpa_emu.expf (oracle/glibc_expf.c) == this host's glibc expf -- the
+    std::exp(float) of aten's flash attention on the reference host -- on 2^22 floats of the
+    softmax's range (-104, 0] plus the edge inputs; and it is not the correctly rounded exp
+    there (the round-4 model): the test also finds inputs where the two differ. The exhaustive
+    2^32 check is tools/cpu_order/check_glibc_expf.c (profiles/r05_s2_glibc_expf_exhaustive.log)."""
+    import ctypes
+
+    import numpy as np
+
+    from oracle import sdpa_emu as E
+    libm = ctypes.CDLL("libm.so.6")
+    libm.expf.restype, libm.expf.argtypes = ctypes.c_float, [ctypes.c_float]
+    rng = np.random.default_rng(7)
+    x = np.concatenate([-rng.random(1 << 22, dtype=np.float32) * 104.0,
+                        np.array([0.0, -0.0, -87.3365478515625, -88.0, -103.2789, -103.9721, -104.0, -np.inf,
+                                  -1e-30, -0.45788383], np.float32)]).astype(np.float32)
+    got = E.expf(torch.from_numpy(x)).numpy()
+    idx = np.concatenate([np.arange(20000), np.arange(x.size - 10, x.size)])
+    ref = np.array([libm.expf(float(v)) for v in x[idx]], np.float32)
+    assert np.array_equal(got[idx].view(np.int32), ref.view(np.int32))
+    cr = np.exp(x.astype(np.float64)).astype(np.float32)
+    assert (cr != got).sum() > 0   # glibc expf is not correctly rounded on this range

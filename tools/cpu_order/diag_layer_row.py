@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--name", default="golden_longprompt4k")
     ap.add_argument("--layer", type=int, default=24)
     ap.add_argument("--row", type=int, default=2765)
+    ap.add_argument("--save", default="", help="torch.save the layer's self-attention inputs / output here")
     a = ap.parse_args()
     import make_golden as MG
     from oracle import cpu_order as CO
@@ -115,6 +116,10 @@ def main():
                         (bits(CO.linear(x[None], mod.weight.detach(), None, kb=k)[0]) != bits(y)).sum()) == 0]
             out.append(r)
             print(json.dumps(r), flush=True)
+        if a.save and "self_sdpa" in cap:
+            q, k, v, mask, is_causal, scale, gqa, o = cap["self_sdpa"]
+            torch.save({"q": q, "k": k, "v": v, "mask": mask, "is_causal": is_causal, "scale": scale, "gqa": gqa,
+                        "o": o}, a.save)
         for tag in ("self_sdpa", "cross_sdpa"):
             if tag not in cap:
                 continue
