@@ -302,26 +302,35 @@ def main():
         torch.cuda.synchronize(dev)
         dtp = time.perf_counter() - tp0
         gen_tokens[0] = saved
-        # roofline of the parity path's dominant kernel: the exact decode Linear (xmm_dec_kernel,
-        # 62 % of a parity step), the six launches of one layer timed with HIP events on the
-        # launching stream, layers rotated (every launch streams its weights from HBM)
+        # roofline of the parity path's dominant kernel, timed with HIP events on the launching
+        # stream, layers rotated (every launch streams its weights from HBM): the persistent
+        # exact layer (xlayer.hip) where it serves the batch, else the six exact decode
+        # Linears of one layer (xmm_dec_kernel)
         import ctypes as C
         from t5gemma_tts_amd import _lib
+        stream_p = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         us_x = C.c_float()
-        _lib.check(_lib.lib().t5g_time_exact_linears(eng.h, B, 26 * 8,
-                                                     C.c_void_p(torch.cuda.current_stream(dev).cuda_stream),
-                                                     C.byref(us_x)), "time_exact_linears")
-        xbytes = _lib.exact_linears_bytes(B, cfg.backbone)
-        pmc_x = os.path.join(REPO, "profiles", "r05_pmc_exact_linears.json")
+        rc_xl = _lib.lib().t5g_time_xlayer(eng.h, B, 26 * 8, stream_p, C.byref(us_x))
+        if rc_xl == 0:
+            xbytes = _lib.xlayer_bytes(B, cfg.backbone, wl_tx, cfg.backbone.num_decoder_layers)
+            pmc_x = os.path.join(REPO, "profiles", "r05_pmc_xlayer.json")
+            kname = ("xlayer_kernel: one decoder layer after its self attention as one persistent launch (o, "
+                     "norm, cross-q, PM cross attention, cross-o, norm, gate/up + GeGLU, down in the reference's "
+                     "K parts, norm, next q|k|v; f32 MFMA in the reference host's fp32 orders)")
+        else:
+            _lib.check(_lib.lib().t5g_time_exact_linears(eng.h, B, 26 * 8, stream_p, C.byref(us_x)),
+                       "time_exact_linears")
+            xbytes = _lib.exact_linears_bytes(B, cfg.backbone)
+            pmc_x = os.path.join(REPO, "profiles", "r05_pmc_exact_linears.json")
+            kname = ("xmm_dec_kernel: one layer's six exact decode Linears (q|k|v, o, cross-q, cross-o, "
+                     "gate/up + GeGLU, down in the reference's K parts; f32 MFMA in the reference host's fp32 "
+                     "orders)")
         traffic_x = None
         if os.path.exists(pmc_x) and B == 8:
-            traffic_x = json.load(open(pmc_x)).get("hbm_bytes_per_layer")
+            traffic_x = json.load(open(pmc_x)).get("hbm_bytes_per_launch")
         ach_x = xbytes / (us_x.value * 1e-6) / 1e9
         parity_roof = {"bound": "hbm", "achieved": round(ach_x, 1), "peak": 8000.0, "unit": "GB/s",
-                       "frac": round(ach_x / 8000.0, 4), "traffic": traffic_x,
-                       "kernel": "xmm_dec_kernel: one layer's six exact decode Linears (q|k|v, o, cross-q, cross-o, "
-                                 "gate/up + GeGLU, down in the reference's K parts; f32 MFMA in the reference "
-                                 "host's fp32 orders), 174.6 MB of weights",
+                       "frac": round(ach_x / 8000.0, 4), "traffic": traffic_x, "kernel": kname,
                        "algorithmic_bytes": int(xbytes), "avg_us": round(us_x.value, 2)}
         parity_line = {
             "value": round(parity_stats["tokens"] / dtp, 2), "unit": "audio tokens/s",

@@ -314,8 +314,18 @@ int t5g_engine_set_sampler_path(t5g_engine* e, int32_t single_block);
  * launch with in-launch hand-offs (fused.hip; 1-16 rows; 17-32 rows fuse the MLP half) or as
  * per-op launches; bitwise equal. Default on. Computes the reference's PMDecoderLayer
  * (hf_export/modeling_t5gemma_voice.py:256-323, [tf] modeling_t5gemma.py:81-97); no
- * reference-side equivalent switch. */
+ * reference-side equivalent switch. The switch also selects parity mode's persistent layer
+ * (xlayer.hip: the same stages in the reference's CPU order, 1-8 decode rows of <= 64 text
+ * keys each; bitwise equal to parity mode's per-op launches). */
 int t5g_engine_set_fused(t5g_engine* e, int32_t enable);
+/* Test / bench hook: parity-mode persistent layer launches issued so far (a launch captured
+ * into a graph counts once, at capture). No reference-side equivalent. */
+int t5g_engine_xlayer_launches(t5g_engine* e, int64_t* n);
+/* Bench hook: average duration (us, HIP events on `stream`) of parity mode's persistent layer
+ * launch at B decode rows, layers rotated as a step runs them, on the engine's current decode
+ * state (call after a parity-mode generate). T5G_EUNSUPPORTED when the launch does not serve
+ * B rows / this model. No reference-side equivalent. */
+int t5g_time_xlayer(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us);
 /* Host hint: the longest text (encoder length) of the batch the next t5g_encode / t5g_decode
  * calls run (0: assume max_text). The persistent decode launch reads at most 64 cross keys
  * per row, so it is chosen when the batch's texts fit, whatever the engine's max_text. */

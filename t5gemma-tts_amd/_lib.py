@@ -133,6 +133,8 @@ SIGNATURES = {
     "t5g_engine_set_exact": (C.c_int, [_P, _I, _P, _I]),
     "t5g_engine_set_sampler_path": (C.c_int, [_P, _I]),
     "t5g_engine_set_fused": (C.c_int, [_P, _I]),
+    "t5g_engine_xlayer_launches": (C.c_int, [_P, C.POINTER(C.c_int64)]),
+    "t5g_time_xlayer": (C.c_int, [_P, _I, _I, _P, C.POINTER(C.c_float)]),
     "t5g_engine_set_text_max": (C.c_int, [_P, _I]),
     "t5g_engine_set_audio_max": (C.c_int, [_P, _I]),
     "t5g_engine_poison_handoff": (C.c_int, [_P, C.c_uint32]),
@@ -257,6 +259,20 @@ def exact_linears_bytes(B: int, bb) -> int:
     io = 2 * B * (d + (qd + 2 * kvd)) + 2 * B * (qd + d) + 2 * B * (d + qd) + 2 * B * (qd + d) + 2 * B * (d + f) \
         + (2 * B * f + 4 * 2 * B * d)
     return w + io
+
+
+def xlayer_bytes(B: int, bb, text_len: int, n_layers: int) -> float:
+    """Algorithmic HBM bytes of one parity-mode persistent layer launch (csrc/xlayer.hip) at B
+    rows, averaged over a step's layers (bench.py parity roofline): the layer's o, cross-q,
+    cross-o, gate/up and down weights and the next layer's q|k|v (none on the last layer) once
+    (bf16), the rows' cross K / V (text_len keys each), the self-attention output in, h in and
+    out, and the in-launch hand-offs (each written once and read once)."""
+    d, f, qd, kvd = bb.hidden_size, bb.intermediate_size, bb.num_attention_heads * bb.head_dim, \
+        bb.num_key_value_heads * bb.head_dim
+    w = 2 * (d * qd + qd * d + d * qd + 2 * f * d + d * f) + 2 * (qd + 2 * kvd) * d * (n_layers - 1) / n_layers
+    kv = 2 * 2 * B * kvd * text_len
+    io = 2 * B * qd + 2 * 2 * B * d + 2 * (2 * B * (d + d + qd + qd + d + f) + 4 * 2 * B * d) + 2 * B * (qd + 2 * kvd)
+    return w + kv + io
 
 
 def fused_block_bytes(M: int, T_x: int, d: int = 2304, f: int = 9216, q_dim: int = 2048, kv_dim: int = 1024,

@@ -16,7 +16,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "lib", "libt5gtts.so")
-SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "fused.hip", "exact.hip", "xmm.hip", "xattn.hip", "eager.hip", "noise.hip", "xc2.hip", "xc2enc.hip", "whisper.hip", "host_sampler.cpp"]
+SOURCES = ["gemm.hip", "gemv.hip", "norm.hip", "attn.hip", "sampler.hip", "engine.hip", "fused.hip", "exact.hip", "xmm.hip", "xattn.hip", "xlayer.hip", "eager.hip", "noise.hip", "xc2.hip", "xc2enc.hip", "whisper.hip", "host_sampler.cpp"]
 HEADERS = ["common.h", "t5g_kernels.h", "xc2_common.h", "exact_math.h", "exact_dev.h", "ref_ksplit.h", "sort_emu.h"]
 ARCH = os.environ.get("T5G_ARCH", "gfx950")
 # -ffp-contract=off: HIP's default (fast-honor-pragmas) fuses a*b+c into one fma even

@@ -79,7 +79,8 @@ struct t5g_engine {
     bool fused_mlp = true;
     float* part2 = nullptr;     // the fused block's in-launch slabs: cross-q [2][B][q_dim] | cross-o [4][B][d] | down [8][B][d] | self o [4][B][d]
     bf16_t* datt2 = nullptr;    // the fused block's cross-attention output [B][q_dim]
-    unsigned* fsync = nullptr;  // timeout line + one counter set per decoder layer (zeroed at creation / after a timeout)
+    unsigned* fsync = nullptr;  // timeout line + one fused.hip counter set per decoder layer + one xlayer.hip
+                                // set per decoder layer (zeroed at creation / after a timeout)
     // decode split-K factors (measured on MI355X): qkv 2, o / cross-q /
     // cross-o 4, down 8 k-slices; gate/up on the one-block-per-CU GEMV
     static constexpr int s_qkv = 2, s_o = 4, s_down = 8;
@@ -128,7 +129,16 @@ struct t5g_engine {
     uint32_t* trig_exc = nullptr;   // parity mode: RoPE cos / sin exceptions (t5g_engine_set_rope_exc)
     int n_trig_exc = 0;
     bool xmm_ready = false;
+    int64_t xl_launches = 0;   // xlayer.hip launches issued (captured ones counted once, at capture)
 };
+
+// words of e->fsync: the timeout line, the fused.hip sets, the xlayer.hip sets
+static size_t fsync_words(const t5g_config& c) {
+    return FM_LINE + (size_t)(FM_SET_WORDS + XL_SET_WORDS) * c.n_dec_layers;
+}
+static unsigned* xlayer_set(t5g_engine* e, int l) {
+    return e->fsync + FM_LINE + (size_t)FM_SET_WORDS * e->c.n_dec_layers + (size_t)XL_SET_WORDS * l;
+}
 
 template <typename T>
 static int alloc(t5g_engine* e, T** p, int64_t n) {
@@ -261,7 +271,7 @@ extern "C" int t5g_engine_create(const t5g_config* cfg, const t5g_weights* w, t5
     rc |= alloc(e, &e->fs_slow, B);
     rc |= alloc(e, &e->part2, (int64_t)2 * B * e->q_dim + (int64_t)4 * B * d + (int64_t)8 * B * d + (int64_t)4 * B * d);
     rc |= alloc(e, &e->datt2, (int64_t)B * e->q_dim);
-    rc |= alloc(e, &e->fsync, (int64_t)FM_LINE + (int64_t)FM_SET_WORDS * c.n_dec_layers);
+    rc |= alloc(e, &e->fsync, (int64_t)fsync_words(c));
     if (rc) {
         t5g_engine_destroy(e);
         return T5G_ENOMEM;
@@ -582,6 +592,68 @@ static int encode_exact(t5g_engine* e, int ntok, const int32_t* ids, const int32
     return T5G_OK;
 }
 
+// Parity decode rows through xlayer.hip (the layer after the self attention as one launch):
+// the 2b-2b shapes, M <= 8 rows, <= 64 text keys per row (the call's hint), no softcap, and
+// the reference splitting none of the layer's M = 1 Linears but the down projection, in two
+// K parts of 144 chunks (ref_ksplit.h) -- the arithmetic the launch is built for
+static bool xlayer_usable(const t5g_engine* e, int M) {
+    const t5g_config& c = e->c;
+    if (!e->fused_mlp || M < 1 || M > 8 || c.softcap > 0.f || c.n_dec_layers < 2) return false;
+    if (c.hidden != 2304 || c.intermediate != 9216 || e->q_dim != 2048 || e->kv_dim != 1024 || c.head_dim != 256 ||
+        c.n_heads != 8 || c.n_kv_heads != 4 || e->qkv_dim != 4096)
+        return false;
+    if ((e->text_max > 0 ? e->text_max : c.max_text) > 64) return false;
+    auto whole = [](int N, int K) { return ksplit_host(N, K, 1) >= K / 32; };
+    return whole(2304, 2048) && whole(2048, 2304) && whole(9216, 2304) && whole(1024, 2304) &&
+           ksplit_host(2304, 9216, 1) == 144;
+}
+
+static XLayerArgs xlayer_args(t5g_engine* e, int M, int l) {
+    const t5g_config& c = e->c;
+    const t5g_layer_weights& L = e->dec[l];
+    const t5g_engine::XLayer& X = e->dec_x[l];
+    const bool last = l == c.n_dec_layers - 1;
+    XLayerArgs a;
+    memset(&a, 0, sizeof(a));
+    a.M = M;
+    a.Wo = X.o;
+    a.Wq = X.cross_q;
+    a.Wco = X.cross_o;
+    a.Wgu = X.gate_up;
+    a.Wd = X.down;
+    a.Wqkv = last ? nullptr : e->dec_x[l + 1].qkv;
+    a.n1_post = (const bf16_t*)L.norms[1];
+    a.n1_pre = (const bf16_t*)L.norms[2];
+    a.n2_post = (const bf16_t*)L.norms[3];
+    a.n2_pre = (const bf16_t*)L.norms[4];
+    a.n3_post = (const bf16_t*)L.norms[5];
+    a.n3_pre = (const bf16_t*)(last ? e->w.dec_final_norm : e->dec[l + 1].norms[0]);
+    a.eps = c.rms_eps;
+    a.att16_self = e->datt16;
+    a.h = e->dh;
+    a.xn = e->dxn;
+    a.xn16 = e->dxn16;
+    a.tmp = e->tmp;
+    a.q = e->dq;
+    a.att = e->datt;
+    a.att16 = e->datt16;
+    a.act16 = e->dact16;
+    a.dpart = e->dpart;
+    a.qkv = e->qkv;
+    a.qkv_dim = e->qkv_dim;
+    a.ck = e->ck[l];
+    a.cv = e->cv[l];
+    a.kv_hstride = (long)c.max_text * c.head_dim;
+    a.kv_bstride = a.kv_hstride * c.n_kv_heads;
+    a.enc_len = e->enc_len;
+    a.rope_tab = e->rope_tab;
+    a.scale = c.attn_scale;
+    a.sync = xlayer_set(e, l);
+    a.sync_next = xlayer_set(e, (l + 1) % c.n_dec_layers);
+    a.timeout = e->fsync;
+    return a;
+}
+
 // decode: M = B rows fed by the sampler buffers (the reference's M = 1 per call);
 // prefill: M packed tokens, the reference's M = the row's token count (kv_len)
 static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* tok_row, const int* tok_t,
@@ -609,6 +681,10 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
         n.normed_x16 = xn16;
         return resid_norm(n, st);
     };
+    // decode: the rest of each layer as one xlayer.hip launch, which also runs the next
+    // layer's q|k|v (bitwise equal to the per-op launches below)
+    bool xl = decode && xlayer_usable(e, M) && exact_attention_decode_supported(c.n_heads / c.n_kv_heads, D);
+    bool qkv_done = false;
     for (int l = 0; l < c.n_dec_layers; ++l) {
         const t5g_layer_weights& L = e->dec[l];
         const t5g_engine::XLayer& X = e->dec_x[l];
@@ -633,8 +709,10 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
             RC(resid_norm(n, st));
         }
         // self attention
-        RC(xlin16(e, xn16, M, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
-                  e->q_dim, e->kv_dim, e->q_dim, st));
+        if (!qkv_done)
+            RC(xlin16(e, xn16, M, X.qkv, e->qkv_dim, d, nullptr, e->qkv, e->qkv_dim, nullptr, EPI_BF16, tok_row, rl,
+                      e->q_dim, e->kv_dim, e->q_dim, st));
+        qkv_done = false;
         // decode: RoPE of q and k and the cache append happen inside the scores launch
         const bool fuse = decode && exact_attention_decode_supported(c.n_heads / c.n_kv_heads, D);
         if (fuse) {
@@ -648,6 +726,16 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
             fr.ldq = e->qkv_dim;
             RC(xattn(e, e->qkv, M, tok_row, tok_t, qlen, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1,
                      c.dec_sliding[l] ? c.sliding_window : 0, att, att16, st, fr));
+            if (xl) {
+                const int rc = xlayer_launch(xlayer_args(e, M, l), st);
+                if (rc == 0) {
+                    ++e->xl_launches;
+                    qkv_done = l + 1 < c.n_dec_layers;
+                    continue;
+                }
+                if (rc != -1 || l > 0) return rc == -1 ? T5G_EINVAL : rc;   // -1 is static: all layers or none
+                xl = false;
+            }
         } else {
             RopeArgs r = xrope_args(e, M, D, pos, e->w.inv_freq, tok_row, tok_t, e->kv_len);
             r.rope_tab = decode ? e->rope_tab : nullptr;
@@ -1513,7 +1601,7 @@ static int check_handoff(t5g_engine* e, hipStream_t st) {
     HIPCHK(hipStreamSynchronize(st));
     if (!tmo) return T5G_OK;
     fprintf(stderr, "[t5gtts] fused decode hand-off timed out (code %u)\n", tmo);
-    hipMemsetAsync(e->fsync, 0, (FM_LINE + (size_t)FM_SET_WORDS * e->c.n_dec_layers) * sizeof(unsigned), st);
+    hipMemsetAsync(e->fsync, 0, fsync_words(e->c) * sizeof(unsigned), st);
     hipStreamSynchronize(st);
     return T5G_EHANDOFF;
 }
@@ -1559,6 +1647,12 @@ extern "C" int t5g_engine_set_audio_max(t5g_engine* e, int32_t n) {
     const int after = n > 0 ? n : e->c.max_audio;
     if ((before + 63) / 64 != (after + 63) / 64 || before != after) drop_graphs(e);   // grid + stop rule in the graphs
     e->audio_max = n;
+    return T5G_OK;
+}
+
+extern "C" int t5g_engine_xlayer_launches(t5g_engine* e, int64_t* n) {
+    if (!e || !n) return T5G_EINVAL;
+    *n = e->xl_launches;
     return T5G_OK;
 }
 
@@ -1787,6 +1881,36 @@ extern "C" int t5g_time_exact_linears(t5g_engine* e, int32_t B, int32_t iters, v
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     return T5G_OK;
+}
+
+// hipEvent-timed parity-mode persistent layer launches (xlayer.hip; bench.py parity roofline):
+// whole rotations over the layers as a decode step runs them (layer l's counter set zeroed by
+// layer l - 1's launch), one untimed rotation first, on the engine's current decode state
+extern "C" int t5g_time_xlayer(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us) {
+    if (!e || iters <= 0 || !avg_us || B <= 0 || B > e->c.max_batch || !e->exact || !e->xmm_ready) return T5G_EINVAL;
+    if (!xlayer_usable(e, B)) return T5G_EUNSUPPORTED;
+    hipStream_t st = (hipStream_t)stream;
+    const int L = e->c.n_dec_layers;
+    const int n = (iters + L - 1) / L * L;
+    for (int l = 0; l < L; ++l) {
+        const int rc = xlayer_launch(xlayer_args(e, B, l), st);
+        if (rc) return rc == -1 ? T5G_EUNSUPPORTED : T5G_EHIP;
+    }
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, st));
+    int rc = 0;
+    for (int i = 0; i < n && !rc; ++i) rc = xlayer_launch(xlayer_args(e, B, i % L), st);
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    if (rc) return rc == -1 ? T5G_EUNSUPPORTED : T5G_EHIP;
+    *avg_us = ms * 1000.f / (float)n;
+    return check_handoff(e, st);
 }
 
 // hipEvent-timed fused decode-MLP launches (bench.py roofline leg): layers rotated, so every

@@ -118,6 +118,43 @@ int fused_mlp_check(const FusedMlpArgs& a);   // 0: fused_mlp would launch these
 // decoder layer after one line for the timeout word.
 constexpr int FM_LINE = 32, FM_SET_LINES = 51, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
 
+// parity mode's decode layer after the self attention as one persistent launch (xlayer.hip):
+// O1 self o-proj, N1, cross q, PM cross attention, cross o, N2, gate/up + GeGLU, down in the
+// reference's two K parts, N3, the next layer's q|k|v -- the per-op launches' arithmetic,
+// bitwise. Decode rows M <= 8, the 2b-2b shapes (hidden 2304, q_dim 2048, head_dim 256, 8 q
+// heads over 4 kv heads, intermediate 9216), <= 64 text keys per row.
+struct XLayerArgs {
+    int M;
+    // E16 weights of the layer (Wqkv: the next layer's; null on the last layer)
+    const bf16_t *Wo, *Wq, *Wco, *Wgu, *Wd, *Wqkv;
+    // RMSNorm(1 + w) weights: N1 post_self / pre_cross, N2 post_cross / pre_ff, N3 post_ff /
+    // the next layer's pre_self (or the final norm)
+    const bf16_t *n1_post, *n1_pre, *n2_post, *n2_pre, *n3_post, *n3_pre;
+    float eps;
+    const bf16_t* att16_self;   // X16 self-attention output (previous launch)
+    bf16_t* h;                  // residual rows [M][hidden] (read at N1, written at N3)
+    bf16_t* xn;                 // normed rows [M][hidden] (row-major copy)
+    bf16_t* xn16;               // normed rows, X16 (handed off in-launch)
+    bf16_t* tmp;                // o-projection outputs [M][hidden] (in-launch)
+    bf16_t* q;                  // cross q [M][q_dim] un-rotated (in-launch)
+    bf16_t* att;                // cross attention output [M][q_dim] (row-major copy)
+    bf16_t* att16;              // cross attention output, X16 (in-launch)
+    bf16_t* act16;              // GeGLU act, X16 (in-launch)
+    float* dpart;               // down projection K parts [2][M][hidden] fp32 (in-launch)
+    bf16_t* qkv;                // next layer's q|k|v [M][qkv_dim] (next launch)
+    int qkv_dim;
+    const bf16_t *ck, *cv;      // the layer's cross K / V cache [B][Hkv][kv_cap][D]
+    long kv_bstride, kv_hstride;
+    const int* enc_len;         // [B] text lengths
+    const float* rope_tab;      // [B][D] this step's PM-RoPE cos | sin
+    float scale;
+    unsigned* sync;             // this launch's XL_SET_LINES counter lines (zero when it starts)
+    unsigned* sync_next;        // the next launch's set: zeroed by this launch
+    unsigned* timeout;          // sticky timeout word (fused.hip's)
+};
+constexpr int XL_SET_LINES = 56, XL_SET_WORDS = XL_SET_LINES * FM_LINE;
+int xlayer_launch(const XLayerArgs& a, hipStream_t st);   // -1: not built for these args / this device
+
 // ---- row-wise residual / RMSNorm / embedding -------------------------------
 struct NormArgs {
     int M, d;

@@ -221,8 +221,17 @@ class T5GemmaTTSEngine:
         """Fast-path decode layer after the self attention (o-proj, norm, cross-q, cross
         attention, cross-o, norm, gate/up, down, norm, the next q|k|v) as one persistent
         launch (default; 17-32 rows: the MLP half) or as per-op launches; bitwise equal
-        (csrc/fused.hip)."""
+        (csrc/fused.hip). In parity mode the same switch selects the exact-order persistent
+        layer (csrc/xlayer.hip; 1-8 rows of <= 64 text keys), bitwise equal to the per-op
+        exact launches."""
         _lib.check(self.L.t5g_engine_set_fused(self.h, 1 if enable else 0), "set_fused")
+
+    def xlayer_launches(self) -> int:
+        """Parity-mode persistent layer launches issued so far (test / bench hook; a launch
+        captured into a graph counts once)."""
+        n = C.c_int64()
+        _lib.check(self.L.t5g_engine_xlayer_launches(self.h, C.byref(n)), "xlayer_launches")
+        return n.value
 
     def set_attn_flash(self, enable: bool) -> None:
         """Fast-path decode self attention as one split-key launch with an online-softmax
