@@ -37,6 +37,31 @@
 #include "exact_math.h"
 #include "t5g_kernels.h"
 
+// diagnostic stage timeline (T5G_DBG_TS library variant only, tools/xlayer_timeline.py):
+// thread 0 of every workgroup stores the 100 MHz clock at numbered points of the launches
+// that run a next layer's q|k|v, 32 slots per workgroup
+#ifdef T5G_DBG_TS
+__device__ unsigned long long* xl_ts_buf;
+extern "C" int t5g_dbg_set_xlayer(void* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(xl_ts_buf), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+// timing variants of the GEMV stages (never in the product): 1 no MFMA, 2 no fold, 3 no
+// weight loads
+__device__ int xl_dbg_var;
+extern "C" int t5g_dbg_set_xlayer_var(int v) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(xl_dbg_var), &v, sizeof(v)) == hipSuccess ? 0 : -1;
+}
+#define XL_DBG_VAR xl_dbg_var
+#define XL_TS(k)                                                                                   \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && xl_ts_buf && a.Wqkv)                                              \
+            xl_ts_buf[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime();                   \
+    } while (0)
+#else
+#define XL_DBG_VAR 0
+#define XL_TS(k) do { } while (0)
+#endif
+
 namespace t5g {
 
 constexpr int XL_NW = 8;                    // waves per workgroup (xmm_dec_kernel's count)
@@ -47,6 +72,7 @@ constexpr int XL_D = 2304, XL_F = 9216, XL_QD = 2048, XL_KVD = 1024, XL_HD = 256
 constexpr int XL_DOWN_KBC = 144;            // the reference's K part of the down projection at M = 1 (chunks)
 constexpr unsigned XL_SPIN_MAX = 1u << 18;
 constexpr int XL_AUX_SC1 = 16;
+constexpr int XL_XWIN = 144;                // X window chunks in LDS: the down projection's K part
 
 // counter set lines (one word per 128-byte line)
 constexpr int XC_O1 = 0, XC_N1 = 8, XC_Q = 9, XC_A = 13, XC_O = 21, XC_N2 = 29, XC_G0 = 30, XC_G1 = 38, XC_D = 46,
@@ -59,6 +85,11 @@ __device__ __forceinline__ unsigned xl_ld_rlx(unsigned* p) {
 }
 __device__ __forceinline__ void xl_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void xl_barrier() { asm volatile("s_barrier" ::: "memory"); }
+// the workgroup meets after its LDS accesses completed -- and NOT after its outstanding global
+// loads: __syncthreads() is a workgroup release fence + barrier, which waits vmcnt(0), i.e. for
+// the next pass's weights requested ahead (that wait serialised every weight stream behind the
+// MFMAs: G stage 25 us -> see DESIGN.md)
+__device__ __forceinline__ void xl_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // one wave polls the N lines a stage's arrivals are spread over (any distribution) until
 // their sum reaches `total`: one memory round trip per poll; lane 63 watches the timeout word
@@ -109,13 +140,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t xl_rsrc(const void* base, uint
 // t >> 4, col t & 15) over the chunks in order as one plain chain from 0 (the reference
 // splits none of these Linears at M = 1 but the down projection, whose two K parts are two
 // tasks, each folded from 0), then the epilogue stores sc1.
-struct XlOps {
-    u32x4 w[XL_CPW], x[XL_CPW];
-};
 // one pass of <= 72 chunks of a task; a task of more chunks (the down projection's 144-chunk
-// parts) is several passes whose fold continues one chain (first / last pass flags)
+// parts) is several passes whose fold continues one chain (first / last pass flags). xb: the
+// first chunk of the X window the pass reads (the stage's whole K, or the down part's range)
 struct XlTask {
-    int g, kb_lo, kb_hi, part;
+    int g, kb_lo, kb_hi, part, xb;
     bool first, last;
 };
 struct XlGemv {
@@ -125,8 +154,18 @@ struct XlGemv {
     int N, M;
     __amdgpu_buffer_rsrc_t y, part;      // outputs (sc1 stores): Y [M][N] bf16 or Y16 / parts
     bool y16;                            // EPI_BF16: Y is row-major [M][N]; GEGLU: Y is the X16 act (K = N / 2)
+    int xwin;                            // chunks of the X window staged in LDS (<= XL_XWIN)
 };
-__device__ __forceinline__ void xl_issue_w(XlOps& o, const XlGemv& s, const XlTask& t, int wave, int lane) {
+// the weights of one pass in registers: wave w holds chunks w, w + 8, ... (<= 9)
+struct XlW {
+    u32x4 w[XL_CPW];
+};
+__device__ __forceinline__ void xl_issue_w(XlW& o, const XlGemv& s, const XlTask& t, int wave, int lane) {
+    if (XL_DBG_VAR == 3) {
+#pragma unroll
+        for (int c = 0; c < XL_CPW; ++c) o.w[c] = u32x4{(unsigned)t.g, 0u, 0u, (unsigned)lane};
+        return;
+    }
     const u32x4* wp = (const u32x4*)(s.W + (long)t.g * s.KB * 512) + lane;
 #pragma unroll
     for (int c = 0; c < XL_CPW; ++c) {
@@ -134,23 +173,39 @@ __device__ __forceinline__ void xl_issue_w(XlOps& o, const XlGemv& s, const XlTa
         o.w[c] = wp[(long)kb * 64];
     }
 }
-__device__ __forceinline__ void xl_issue_x(XlOps& o, const XlGemv& s, const XlTask& t, int wave, int lane) {
+// the X window [xb, xb + xwin) of rows 0..7 into LDS once per stage (per down part): per chunk
+// the 32 lanes (q, j < 8) of the X16 tile, 512 bytes (R8: lanes j >= 8 read lane j - 8's)
+__device__ __forceinline__ void xl_fill_x(const XlGemv& s, int xb, u32x4* xs) {
+    const int n = s.xwin * 32;
+    u32x4 v[XL_XWIN * 32 / 512];
 #pragma unroll
-    for (int c = 0; c < XL_CPW; ++c) {
-        const int kb = min(t.kb_lo + wave + c * XL_NW, t.kb_hi - 1);
-        int off = (kb * 64 + (lane & ~8)) * 16;
+    for (int u = 0; u < XL_XWIN * 32 / 512; ++u) {
+        const int i = min((int)threadIdx.x + u * 512, n - 1), kb = xb + (i >> 5), r = i & 31;
+        int off = (kb * 64 + (r >> 3) * 16 + (r & 7)) * 16;
         asm volatile("" : "+v"(off));
-        o.x[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(s.x, off, 0, XL_AUX_SC1));
+        v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(s.x, off, 0, XL_AUX_SC1));
+    }
+#pragma unroll
+    for (int u = 0; u < XL_XWIN * 32 / 512; ++u) {
+        const int i = (int)threadIdx.x + u * 512;
+        if (i < n) xs[i] = v[u];
     }
 }
-// the chunk MFMAs of one task into LDS cs[chunk][XL_EL]
-__device__ __forceinline__ void xl_mfma(const XlOps& o, const XlTask& t, float* cs, int wave, int lane) {
+// the chunk MFMAs of one pass into LDS cs[chunk][XL_EL], X from the LDS window
+__device__ __forceinline__ void xl_mfma(const XlW& o, const XlTask& t, const u32x4* xs, float* cs, int wave,
+                                        int lane) {
     const int n = t.kb_hi - t.kb_lo, j = lane & 15, q = lane >> 4;
+    const u32x4* xl = xs + (t.kb_lo - t.xb) * 32 + q * 8 + (lane & 7);
+    if (XL_DBG_VAR == 1) {
+        if (j < 8) *(f32x4_t*)&cs[wave * XL_EL + j * 16 + 4 * q] = (f32x4_t){__uint_as_float(o.w[0][0]),
+                                                                          __uint_as_float(o.w[8][1]), 0.f, 0.f};
+        return;
+    }
 #pragma unroll
     for (int c = 0; c < XL_CPW; ++c) {
         const int cc = wave + c * XL_NW;
         if (cc < n) {
-            const f32x4_t v = xmm_chunk(o.w[c], o.x[c]);
+            const f32x4_t v = xmm_chunk(o.w[c], xl[cc * 32]);
             if (j < 8) *(f32x4_t*)&cs[cc * XL_EL + j * 16 + 4 * q] = v;
         }
     }
@@ -196,34 +251,50 @@ __device__ __forceinline__ void xl_store(const XlGemv& s, const XlTask& t, int m
     __builtin_amdgcn_raw_buffer_store_b16(f2bf(rbf(y)), s.y, (m * s.N + n) * 2, 0, XL_AUX_SC1);
 }
 
-// the workgroup's tasks [t0, t1) of one GEMV stage: the first task's weights requested
-// before the stage's hand-off (wait()), each next task's operands while the current one folds
+// LDS of a GEMV stage: the X window, two chunk-sum buffers (the fold of pass i reads one while
+// the MFMAs of pass i + 1 fill the other)
+struct XlGemvLds {
+    u32x4* xs;
+    float* cs0;
+    float* cs1;
+};
+
+// the workgroup's passes [t0, t1) of one GEMV stage. The first pass's weights are requested
+// before the stage's hand-off (wait()), then the X window is staged in LDS; each next pass's
+// weights are requested before the current pass's MFMAs (two register buffers), and the
+// folder threads fold pass i while the other waves run pass i + 1's MFMAs (one barrier per
+// pass)
 template <int EPI, bool PART, typename TaskOf, typename Wait>
-__device__ __forceinline__ void xl_gemv(const XlGemv& s, int t0, int t1, TaskOf task_of, float* cs, Wait wait) {
+__device__ __forceinline__ void xl_gemv(const XlGemv& s, int t0, int t1, TaskOf task_of, const XlGemvLds& L,
+                                        Wait wait) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (t0 >= t1) return;
     float acc = 0.f;   // folder threads: the chain across a task's passes
-    XlOps ops;
-    XlTask t = task_of(t0);
-    xl_issue_w(ops, s, t, wave, lane);
+    int xb_cur = -1;
+    XlW wa, wb;
+    xl_issue_w(wa, s, task_of(t0), wave, lane);
     wait();
-    xl_issue_x(ops, s, t, wave, lane);
-    for (int i = t0; i < t1; ++i) {
-        xl_mfma(ops, t, cs, wave, lane);
-        XlTask tn = t;
-        if (i + 1 < t1) {
-            tn = task_of(i + 1);
-            xl_issue_w(ops, s, tn, wave, lane);
-            xl_issue_x(ops, s, tn, wave, lane);
+    auto pass = [&](XlW& cur, XlW& nxt, int i, float* cs) {
+        const XlTask t = task_of(i);
+        if (t.xb != xb_cur) {   // uniform: a new X window (the stage's first pass, a down part change)
+            xl_lds_barrier();   // every earlier reader of the LDS window is done
+            xl_fill_x(s, t.xb, L.xs);
+            xl_lds_barrier();
+            xb_cur = t.xb;
         }
-        __syncthreads();
+        if (i + 1 < t1) xl_issue_w(nxt, s, task_of(i + 1), wave, lane);
+        xl_mfma(cur, t, L.xs, cs, wave, lane);
+        xl_lds_barrier();
         if (tid < XL_EL) {
-            acc = xl_fold(cs, t.kb_hi - t.kb_lo, tid, t.first ? 0.f : acc);
+            acc = XL_DBG_VAR == 2 ? cs[tid] : xl_fold(cs, t.kb_hi - t.kb_lo, tid, t.first ? 0.f : acc);
             if (t.last) xl_store<EPI, PART>(s, t, tid >> 4, tid & 15, acc);
         }
-        __syncthreads();
-        t = tn;
+    };
+    for (int i = t0; i < t1; i += 2) {
+        pass(wa, wb, i, L.cs0);
+        if (i + 1 < t1) pass(wb, wa, i + 1, L.cs1);
     }
+    xl_lds_barrier();   // the folds are done before the LDS is reused
 }
 
 // ---------------------------------------------------------------- exact norm (one row)
@@ -231,15 +302,18 @@ __device__ __forceinline__ void xl_gemv(const XlGemv& s, int t0, int t1, TaskOf 
 // first d / 8 active): v = bf16(delta) (NS = 0) or bf16((0 + p0) + p1) (NS = 2, the down
 // parts), post-norm, + h, pre-norm. The row's h stays in LDS between the launch's three
 // norms (hrow) and goes back to HBM at N3; xn goes out row-major (plain) and in X16 (sc1).
-template <int NS>
+template <int NS, typename Wait>
 __device__ __forceinline__ void xl_norm_row(const XLayerArgs& a, int m, const bf16_t* post_w, const bf16_t* pre_w,
-                                            u32x4* hrow, bool first, bool last, float* sq) {
+                                            u32x4* hrow, bool first, bool last, float* sq, Wait wait) {
     const int d = XL_D, c = threadIdx.x;
     const bool active = 8 * c < d;
     const int cc = active ? c : d / 8 - 1;
+    // the norm weights and the launch's input h row are requested before the hand-off
     const u32x4 w_post = *(const u32x4*)(post_w + 8 * cc);
     const u32x4 w_pre = *(const u32x4*)(pre_w + 8 * cc);
-    const u32x4 rw = first ? *(const u32x4*)(a.h + (long)m * d + 8 * cc) : hrow[cc];
+    u32x4 rw = first ? *(const u32x4*)(a.h + (long)m * d + 8 * cc) : u32x4{0u, 0u, 0u, 0u};
+    wait();
+    if (!first) rw = hrow[cc];
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (NS == 0) {
         const __amdgpu_buffer_rsrc_t dr = xl_rsrc(a.tmp, (uint32_t)(a.M * d * 2));
@@ -318,7 +392,8 @@ struct XlAttnLds {
     float tmp[8][XL_G][32];
     float l_s[XL_G];
 };
-__device__ __forceinline__ void xl_cross_attn(const XLayerArgs& a, int qi, int kvh, int z, XlAttnLds& S) {
+template <typename Wait>
+__device__ __forceinline__ void xl_cross_attn(const XLayerArgs& a, int qi, int kvh, int z, XlAttnLds& S, Wait wait) {
     constexpr int D = XL_HD, G = XL_G, NCB = D / 32, H2 = D / 2, DZ = 32, DP = DZ / 2, NG8 = 8, CH = 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kl = (tid & 255) >> 2, qa = tid & 3;
     const bool on = tid < 256;
@@ -338,6 +413,7 @@ __device__ __forceinline__ void xl_cross_attn(const XLayerArgs& a, int qi, int k
 #pragma unroll
     for (int j = 0; j < 8; ++j)
         vw[j] = *(const uint32_t*)(Vb + (long)min(vlane ? gl * 8 + j : 0, max(span - 1, 0)) * D + 2 * dp);
+    wait();   // K / V (written before the launch) in flight across the hand-off
     if (on) {
         const float* tab = a.rope_tab + (long)row * D;
         const __amdgpu_buffer_rsrc_t qr = xl_rsrc(a.q, (uint32_t)(a.M * XL_QD * 2));
@@ -444,18 +520,23 @@ __device__ __forceinline__ void xl_run(int n, int workers, int w, int& lo, int& 
 }
 
 // ---------------------------------------------------------------- the launch
+// LDS: the X window (aliased, outside the GEMV stages, by the norms' sum-of-squares scratch
+// and the cross attention's), the two chunk-sum buffers, the norm workgroup's h row
+constexpr size_t XL_LDS_XS = (size_t)XL_XWIN * 32 * 16;
 constexpr size_t XL_LDS_CS = (size_t)XL_SC * XL_EL * 4;
 constexpr size_t XL_LDS_SQ = (size_t)(XL_D + 64) * 4;
 constexpr size_t XL_LDS_H = (size_t)XL_D * 2;
-constexpr size_t XL_LDS = XL_LDS_CS + XL_LDS_SQ + XL_LDS_H + (sizeof(XlAttnLds) + 15) / 16 * 16;
+constexpr size_t XL_LDS = XL_LDS_XS + 2 * XL_LDS_CS + XL_LDS_H;
+static_assert(XL_LDS_SQ <= XL_LDS_XS && sizeof(XlAttnLds) <= XL_LDS_XS, "aliases of the X window");
+static_assert(XL_LDS <= 160 * 1024, "LDS of one CU");
 
 template <bool HAS_QKV>
 __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* cs = (float*)smem;
-    float* sq = (float*)(smem + XL_LDS_CS);
-    u32x4* hrow = (u32x4*)(smem + XL_LDS_CS + XL_LDS_SQ);
-    XlAttnLds& al = *(XlAttnLds*)(smem + XL_LDS_CS + XL_LDS_SQ + XL_LDS_H);
+    const XlGemvLds gl{(u32x4*)smem, (float*)(smem + XL_LDS_XS), (float*)(smem + XL_LDS_XS + XL_LDS_CS)};
+    float* sq = (float*)smem;
+    u32x4* hrow = (u32x4*)(smem + XL_LDS_XS + 2 * XL_LDS_CS);
+    XlAttnLds& al = *(XlAttnLds*)smem;
     const int bu = (int)blockIdx.x, nb = (int)gridDim.x, tid = (int)threadIdx.x;
     const int M = a.M, d = XL_D;
     unsigned* set = a.sync;
@@ -466,28 +547,37 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     const bool normwg = nrow >= 0;
     const int nw = nb - M;                      // workers of the G and D stages
     auto none = [] {};
+    XL_TS(0);
 
     // ---- O1: o-projection of the self attention (K = q_dim: 64 chunks), groups 0..143
     if (bu < d / 16) {
         const XlGemv s{a.Wo, XL_QD / 32, xl_rsrc(a.att16_self, 16u * XL_QD * 2u), d, M,
-                       xl_rsrc(a.tmp, (uint32_t)(M * d * 2)), xl_rsrc(nullptr, 0u), false};
-        xl_gemv<EPI_BF16, false>(s, bu, bu + 1, [&](int g) { return XlTask{g, 0, XL_QD / 32, 0, true, true}; }, cs, none);
+                       xl_rsrc(a.tmp, (uint32_t)(M * d * 2)), xl_rsrc(nullptr, 0u), false, XL_QD / 32};
+        xl_gemv<EPI_BF16, false>(s, bu, bu + 1, [&](int g) { return XlTask{g, 0, XL_QD / 32, 0, 0, true, true}; }, gl, none);
         xl_publish(set, XC_O1 + (bu & 7), 1u);
+        XL_TS(1);
     }
     // ---- N1 (norm workgroups)
     if (normwg) {
-        xl_wait_wg<8>(set, XC_O1, (unsigned)(d / 16), tmo, 21u);
-        xl_norm_row<0>(a, nrow, a.n1_post, a.n1_pre, hrow, true, false, sq);
+        xl_norm_row<0>(a, nrow, a.n1_post, a.n1_pre, hrow, true, false, sq, [&] {
+            xl_wait_wg<8>(set, XC_O1, (unsigned)(d / 16), tmo, 21u);
+            XL_TS(19);
+        });
         xl_publish(set, XC_N1, 1u);
+        XL_TS(2);
     }
     // ---- Q: cross-q (128 groups); published per kv head (32 groups: its two q heads)
     if (bu < XL_QD / 16) {
         static_assert(XL_DOWN_KBC % 2 == 0 && XL_DOWN_KBC / 2 <= XL_SC, "down passes");
         const XlGemv s{a.Wq, d / 32, xl_rsrc(a.xn16, 16u * d * 2u), XL_QD, M, xl_rsrc(a.q, (uint32_t)(M * XL_QD * 2)),
-                       xl_rsrc(nullptr, 0u), false};
-        xl_gemv<EPI_BF16, false>(s, bu, bu + 1, [&](int g) { return XlTask{g, 0, d / 32, 0, true, true}; }, cs,
-                                 [&] { xl_wait_wg<1>(set, XC_N1, (unsigned)M, tmo, 22u); });
+                       xl_rsrc(nullptr, 0u), false, d / 32};
+        xl_gemv<EPI_BF16, false>(s, bu, bu + 1, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
+                                 [&] {
+                                     xl_wait_wg<1>(set, XC_N1, (unsigned)M, tmo, 22u);
+                                     XL_TS(3);
+                                 });
         xl_publish(set, XC_Q + bu / 32, 1u);
+        XL_TS(4);
     }
     // ---- A: PM cross attention, task t = (row, kv head, 32-dim slice), row fastest
     {
@@ -495,26 +585,36 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
         int done = 0;
         for (int t = bu; t < ntask; t += nb) {
             const int qi = t % M, kvh = (t / M) % XL_HKV, z = t / (M * XL_HKV);
-            xl_wait_wg<1>(set, XC_Q + kvh, 32u, tmo, 23u);
-            xl_cross_attn(a, qi, kvh, z, al);
+            xl_cross_attn(a, qi, kvh, z, al, [&] {
+                xl_wait_wg<1>(set, XC_Q + kvh, 32u, tmo, 23u);
+                XL_TS(5);
+            });
             ++done;
         }
         if (done) xl_publish(set, XC_A + (bu & 7), (unsigned)done);
+        XL_TS(6);
     }
     // ---- O: cross-o (K = q_dim), groups 0..143
     if (bu < d / 16) {
         const XlGemv s{a.Wco, XL_QD / 32, xl_rsrc(a.att16, 16u * XL_QD * 2u), d, M,
-                       xl_rsrc(a.tmp, (uint32_t)(M * d * 2)), xl_rsrc(nullptr, 0u), false};
+                       xl_rsrc(a.tmp, (uint32_t)(M * d * 2)), xl_rsrc(nullptr, 0u), false, XL_QD / 32};
         const unsigned nA = (unsigned)(M * XL_HKV * (XL_HD / 32));
-        xl_gemv<EPI_BF16, false>(s, bu, bu + 1, [&](int g) { return XlTask{g, 0, XL_QD / 32, 0, true, true}; }, cs,
-                                 [&] { xl_wait_wg<8>(set, XC_A, nA, tmo, 24u); });
+        xl_gemv<EPI_BF16, false>(s, bu, bu + 1, [&](int g) { return XlTask{g, 0, XL_QD / 32, 0, 0, true, true}; }, gl,
+                                 [&] {
+                                     xl_wait_wg<8>(set, XC_A, nA, tmo, 24u);
+                                     XL_TS(7);
+                                 });
         xl_publish(set, XC_O + (bu & 7), 1u);
+        XL_TS(8);
     }
     // ---- N2
     if (normwg) {
-        xl_wait_wg<8>(set, XC_O, (unsigned)(d / 16), tmo, 25u);
-        xl_norm_row<0>(a, nrow, a.n2_post, a.n2_pre, hrow, false, false, sq);
+        xl_norm_row<0>(a, nrow, a.n2_post, a.n2_pre, hrow, false, false, sq, [&] {
+            xl_wait_wg<8>(set, XC_O, (unsigned)(d / 16), tmo, 25u);
+            XL_TS(9);
+        });
         xl_publish(set, XC_N2, 1u);
+        XL_TS(10);
     }
     // ---- G: gate/up + GeGLU, contiguous runs of the 1 152 groups over the nw workers;
     // arrivals counted per down K part (groups [0, 576) hold the act features of part 0)
@@ -523,9 +623,12 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
         int lo, hi;
         xl_run(ngu, nw, bu, lo, hi);
         const XlGemv s{a.Wgu, d / 32, xl_rsrc(a.xn16, 16u * d * 2u), 2 * XL_F, M, xl_rsrc(a.act16, 16u * XL_F * 2u),
-                       xl_rsrc(nullptr, 0u), true};
-        xl_gemv<EPI_GEGLU, false>(s, lo, hi, [&](int g) { return XlTask{g, 0, d / 32, 0, true, true}; }, cs,
-                                  [&] { xl_wait_wg<1>(set, XC_N2, (unsigned)M, tmo, 26u); });
+                       xl_rsrc(nullptr, 0u), true, d / 32};
+        xl_gemv<EPI_GEGLU, false>(s, lo, hi, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
+                                  [&] {
+                                      xl_wait_wg<1>(set, XC_N2, (unsigned)M, tmo, 26u);
+                                      XL_TS(11);
+                                  });
         const int n0 = max(0, min(hi, half) - lo), n1 = max(0, hi - max(lo, half));
         xl_drain();
         __syncthreads();
@@ -535,6 +638,7 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
             if (n1) __hip_atomic_fetch_add(xline(set, XC_G1 + (bu & 7)), (unsigned)n1, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
         }
+        XL_TS(12);
     }
     // ---- D: down in the reference's two K parts, task t = part * 144 + group
     const int ngd = d / 16, ntd = 2 * ngd;
@@ -542,38 +646,47 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
         int lo, hi;
         xl_run(ntd, nw, bu, lo, hi);   // tasks (part, group); two passes of 72 chunks each
         const XlGemv s{a.Wd, XL_F / 32, xl_rsrc(a.act16, 16u * XL_F * 2u), d, M, xl_rsrc(nullptr, 0u),
-                       xl_rsrc(a.dpart, (uint32_t)(2 * M * d * 4)), false};
+                       xl_rsrc(a.dpart, (uint32_t)(2 * M * d * 4)), false, XL_DOWN_KBC};
         const bool need0 = lo < ngd && hi > lo, need1 = hi > ngd;
         xl_gemv<EPI_F32, true>(
             s, 2 * lo, 2 * hi,
             [&](int i) {
                 const int t = i >> 1, sub = i & 1, p = t / ngd;
                 const int k0 = p * XL_DOWN_KBC + sub * (XL_DOWN_KBC / 2);
-                return XlTask{t - p * ngd, k0, k0 + XL_DOWN_KBC / 2, p, sub == 0, sub == 1};
+                return XlTask{t - p * ngd, k0, k0 + XL_DOWN_KBC / 2, p, p * XL_DOWN_KBC, sub == 0, sub == 1};
             },
-            cs, [&] {
+            gl, [&] {
                 if (threadIdx.x < 64) {
                     if (need0) (void)xl_wait<8>(set, XC_G0, (unsigned)half, tmo, 27u);
                     if (need1) (void)xl_wait<8>(set, XC_G1, (unsigned)(ngu - half), tmo, 28u);
                 }
                 xl_barrier();
+                XL_TS(13);
             });
         if (hi > lo) xl_publish(set, XC_D + (bu & 7), (unsigned)(hi - lo));
+        XL_TS(14);
     }
     // ---- N3: from the parts; h back to HBM
     if (normwg) {
-        xl_wait_wg<8>(set, XC_D, (unsigned)ntd, tmo, 29u);
-        xl_norm_row<2>(a, nrow, a.n3_post, a.n3_pre, hrow, false, true, sq);
+        xl_norm_row<2>(a, nrow, a.n3_post, a.n3_pre, hrow, false, true, sq, [&] {
+            xl_wait_wg<8>(set, XC_D, (unsigned)ntd, tmo, 29u);
+            XL_TS(15);
+        });
         xl_publish(set, XC_N3, 1u);
+        XL_TS(16);
     }
     // ---- QKV: the next layer's q|k|v, 256 groups over all workgroups (read by the next launch)
     if constexpr (HAS_QKV) {
         int lo, hi;
         xl_run(a.qkv_dim / 16, nb, bu, lo, hi);
         const XlGemv s{a.Wqkv, d / 32, xl_rsrc(a.xn16, 16u * d * 2u), a.qkv_dim, M,
-                       xl_rsrc(a.qkv, (uint32_t)(M * a.qkv_dim * 2)), xl_rsrc(nullptr, 0u), false};
-        xl_gemv<EPI_BF16, false>(s, lo, hi, [&](int g) { return XlTask{g, 0, d / 32, 0, true, true}; }, cs,
-                                 [&] { xl_wait_wg<1>(set, XC_N3, (unsigned)M, tmo, 30u); });
+                       xl_rsrc(a.qkv, (uint32_t)(M * a.qkv_dim * 2)), xl_rsrc(nullptr, 0u), false, d / 32};
+        xl_gemv<EPI_BF16, false>(s, lo, hi, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
+                                 [&] {
+                                     xl_wait_wg<1>(set, XC_N3, (unsigned)M, tmo, 30u);
+                                     XL_TS(17);
+                                 });
+        XL_TS(18);
     }
 }
 

@@ -1,0 +1,321 @@
+// Rates of the exact-order chunk arithmetic of the parity Linears at decode rows (M = 8),
+// one 512-thread workgroup per CU on every CU (the xlayer.hip GEMV shape), operands in
+// registers / LDS (no HBM traffic): cycles per "chunk" = 16 outputs x 8 rows x 32 k
+// (4 096 multiply-adds in the E / O chain order), per SIMD. Variants:
+//   0  xmm_chunk (exact_dev.h): E and O chains of v_mfma_f32_16x16x4_f32, X from LDS,
+//      chunk sums to LDS (xlayer.hip's xl_mfma)
+//   1  as 0 without the LDS store of the chunk sums
+//   2  as 0, two chunks in flight (four chains interleaved)
+//   3  v_mfma_f32_4x4x1_16b_f32: 16 blocks = 4 output quads x 2 row quads x E/O, one k step
+//      of every chain per instruction (16 instructions per chunk), f32 operands in registers
+//   4  VALU v_fma_f32: lane = output (64 per wave), 8 rows x E/O accumulators, x uniform
+//      (SGPR), weights converted from bf16 pairs (2 ops per k pair)
+//   5  as 4 with v_pk_fma_f32 (E and O of one row in one instruction)
+// Also checks 2, 3, 4, 5 bitwise against 0's chunk sums on random bf16 data.
+// Build: hipcc -O3 -ffp-contract=off --offload-arch=gfx950 tools/micro_xchunk.hip -o /tmp/mx
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bflo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bfhi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+__device__ __forceinline__ f32x4 xchunk(const u32x4& w, const u32x4& x) {
+    f32x4 e = {0.f, 0.f, 0.f, 0.f}, o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        e = __builtin_amdgcn_mfma_f32_16x16x4f32(bflo(w[t]), bflo(x[t]), e, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_16x16x4f32(bfhi(w[t]), bfhi(x[t]), o, 0, 0, 0);
+    }
+    f32x4 c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = __fadd_rn(e[i], o[i]);
+    return c;
+}
+
+__device__ uint32_t hsh(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+__device__ uint16_t rbf16(uint32_t s) {
+    const uint32_t h = hsh(s);
+    const float m = (float)((int)(h & 0xffff) - 32768) / 32768.0f;
+    const int e = (int)((h >> 16) % 16) - 8;
+    return (uint16_t)(__float_as_uint(ldexpf(m, e)) >> 16);
+}
+
+// ---- the data of one chunk: W[16 outputs][32 k], X[8 rows][32 k] bf16 (seeded by chunk id)
+__device__ uint16_t Wv(int c, int o, int k) { return rbf16(c * 4096 + o * 64 + k); }
+__device__ uint16_t Xv(int c, int m, int k) { return rbf16(0x40000000u + c * 4096 + m * 64 + k); }
+
+constexpr int NCH = 16;   // distinct chunks cycled through
+
+// reference chunk sums: ref[c][m][o] = E + O (fmaf chains from 0)
+__global__ void ref_kernel(float* ref) {
+    const int c = blockIdx.x, m = threadIdx.x / 16, o = threadIdx.x % 16;
+    float e = 0.f, od = 0.f;
+    for (int k = 0; k < 32; k += 2) {
+        e = fmaf(__uint_as_float((uint32_t)Wv(c, o, k) << 16), __uint_as_float((uint32_t)Xv(c, m, k) << 16), e);
+        od = fmaf(__uint_as_float((uint32_t)Wv(c, o, k + 1) << 16), __uint_as_float((uint32_t)Xv(c, m, k + 1) << 16), od);
+    }
+    ref[(c * 8 + m) * 16 + o] = __fadd_rn(e, od);
+}
+
+__global__ void xf_kernel(float* xg) {   // X as f32 [chunk][k][m] (variants 4-5: scalar loads)
+    const int c = blockIdx.x, k = threadIdx.x / 8, m = threadIdx.x % 8;
+    xg[(c * 32 + k) * 8 + m] = __uint_as_float((uint32_t)Xv(c, m, k) << 16);
+}
+
+template <int VAR>
+__global__ __launch_bounds__(512) void rate_kernel(int passes, float* out, unsigned long long* cyc,
+                                                   const float* __restrict__ xg) {
+    __shared__ u32x4 xs[NCH][64];          // X16 lane fragments (variants 0-2)
+    __shared__ float cs[2][24 * 8 * 64];   // chunk sums
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int j = lane & 15, q = lane >> 4;
+    // stage X
+    for (int i = tid; i < NCH * 64; i += 512) {
+        const int c = i / 64, l = i % 64, jj = l & 15, qq = l >> 4, m = jj & 7;
+        u32x4 v;
+        for (int t = 0; t < 4; ++t) {
+            const int p = 4 * t + qq;   // x16 pair index: k = 2p, 2p + 1
+            v[t] = (uint32_t)Xv(c, m, 2 * p) | ((uint32_t)Xv(c, m, 2 * p + 1) << 16);
+        }
+        xs[c][l] = v;
+    }
+    // W fragments in registers: chunk cc = wave + 8 u (u < 9) -> data chunk cc % NCH
+    u32x4 w[9];
+    for (int u = 0; u < 9; ++u) {
+        const int c = (wave + 8 * u) % NCH;
+        for (int t = 0; t < 4; ++t) {
+            const int p = 4 * t + q;
+            w[u][t] = (uint32_t)Wv(c, j, 2 * p) | ((uint32_t)Wv(c, j, 2 * p + 1) << 16);
+        }
+    }
+    __syncthreads();
+    float sink = 0.f;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    if constexpr (VAR <= 2) {
+        for (int p = 0; p < passes; ++p) {
+            float* c_s = cs[p & 1];
+            if constexpr (VAR == 2) {
+#pragma unroll
+                for (int u = 0; u < 9; u += 2) {
+                    const int cc0 = wave + 8 * u, cc1 = wave + 8 * (u + 1);
+                    const u32x4 x0 = xs[cc0 % NCH][q * 16 + (lane & 7)];
+                    const u32x4 x1 = xs[cc1 % NCH][q * 16 + (lane & 7)];
+                    f32x4 e0 = {0, 0, 0, 0}, o0 = e0, e1 = e0, o1 = e0;
+                    const u32x4 w1 = u + 1 < 9 ? w[u + 1] : w[u];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(bflo(w[u][t]), bflo(x0[t]), e0, 0, 0, 0);
+                        o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(bfhi(w[u][t]), bfhi(x0[t]), o0, 0, 0, 0);
+                        e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bflo(w1[t]), bflo(x1[t]), e1, 0, 0, 0);
+                        o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bfhi(w1[t]), bfhi(x1[t]), o1, 0, 0, 0);
+                    }
+                    f32x4 c0, c1;
+                    for (int i = 0; i < 4; ++i) {
+                        c0[i] = __fadd_rn(e0[i], o0[i]);
+                        c1[i] = __fadd_rn(e1[i], o1[i]);
+                    }
+                    if (j < 8) {
+                        *(f32x4*)&c_s[cc0 * 128 + j * 16 + 4 * q] = c0;
+                        if (u + 1 < 9) *(f32x4*)&c_s[cc1 * 128 + j * 16 + 4 * q] = c1;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 9; ++u) {
+                    const int cc = wave + 8 * u;
+                    const u32x4 x = xs[cc % NCH][q * 16 + (lane & 7)];
+                    const f32x4 c = xchunk(w[u], x);
+                    if (VAR == 0) {
+                        if (j < 8) *(f32x4*)&c_s[cc * 128 + j * 16 + 4 * q] = c;
+                    } else {
+                        sink += c[0] + c[1] + c[2] + c[3];
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    } else if constexpr (VAR == 3) {
+        // block b = lane >> 2: oq = b & 3, rq = (b >> 2) & 1, eo = b >> 3; t = lane & 3
+        const int b = lane >> 2, t = lane & 3, oq = b & 3, rq = (b >> 2) & 1, eo = b >> 3;
+        float wa[16], xa[16];
+        for (int s = 0; s < 16; ++s) {
+            const int c = wave % NCH, k = 2 * s + eo;
+            wa[s] = __uint_as_float((uint32_t)Wv(c, oq * 4 + t, k) << 16);
+            xa[s] = __uint_as_float((uint32_t)Xv(c, rq * 4 + t, k) << 16);
+        }
+        for (int p = 0; p < passes; ++p) {
+            float* c_s = cs[p & 1];
+#pragma unroll
+            for (int u = 0; u < 9; u += 3) {
+                f32x4 a0 = {0, 0, 0, 0}, a1 = a0, a2 = a0;
+#pragma unroll
+                for (int s = 0; s < 16; ++s) {
+                    a0 = __builtin_amdgcn_mfma_f32_4x4x1f32(wa[s], xa[s], a0, 0, 0, 0);
+                    a1 = __builtin_amdgcn_mfma_f32_4x4x1f32(wa[s], xa[(s + 1) & 15], a1, 0, 0, 0);
+                    a2 = __builtin_amdgcn_mfma_f32_4x4x1f32(wa[(s + 1) & 15], xa[s], a2, 0, 0, 0);
+                }
+                // E + O: lanes of block b (E) and b + 8 (O): xlane 32
+                f32x4 s0, s1, s2;
+                for (int i = 0; i < 4; ++i) {
+                    s0[i] = __fadd_rn(a0[i], __shfl_xor(a0[i], 32, 64));
+                    s1[i] = __fadd_rn(a1[i], __shfl_xor(a1[i], 32, 64));
+                    s2[i] = __fadd_rn(a2[i], __shfl_xor(a2[i], 32, 64));
+                }
+                if (eo == 0) {
+                    const int cc = wave + 8 * u;
+                    for (int i = 0; i < 4; ++i) {
+                        c_s[(cc * 8 + rq * 4 + t) * 16 + oq * 4 + i] = s0[i];
+                        c_s[((cc + 8) * 8 + rq * 4 + t) * 16 + oq * 4 + i] = s1[i];
+                        c_s[((cc + 16) * 8 + rq * 4 + t) * 16 + oq * 4 + i] = s2[i];
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        if (passes < 0) sink = wa[0] + xa[0];
+    } else {
+        // VALU: lane = output (64 outputs per wave: 4 "chunks" of 16 per instruction stream),
+        // one chunk = 16 k pairs; a wave does 9 x 16-output chunks per pass as 9/4 wave-chunks
+        // of 64 outputs -> 3 wave-chunks (12 chunk-equivalents, 9 counted: time scaled below)
+        uint32_t wr[16];
+        for (int s = 0; s < 16; ++s) {
+            const int c = wave % NCH, o = lane & 15;
+            wr[s] = (uint32_t)Wv(c, o, 2 * s) | ((uint32_t)Wv(c, o, 2 * s + 1) << 16);
+        }
+        const float* xp = xg + (__builtin_amdgcn_readfirstlane(wave) % NCH) * 256;
+        for (int p = 0; p < passes; ++p) {
+            float* c_s = cs[p & 1];
+#pragma unroll 1
+            for (int u = 0; u < 3; ++u) {
+                float e[8], od[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) e[m] = od[m] = 0.f;
+                if constexpr (VAR == 4) {
+#pragma unroll
+                    for (int s = 0; s < 16; ++s) {
+                        const float w0 = bflo(wr[s]), w1 = bfhi(wr[s]);
+#pragma unroll
+                        for (int m = 0; m < 8; ++m) {
+                            e[m] = fmaf(w0, xp[(2 * s) * 8 + m], e[m]);
+                            od[m] = fmaf(w1, xp[(2 * s + 1) * 8 + m], od[m]);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < 16; ++s) {
+                        const f32x2 wv = {bflo(wr[s]), bfhi(wr[s])};
+#pragma unroll
+                        for (int m = 0; m < 8; ++m) {
+                            const f32x2 xv = {xp[(2 * s) * 8 + m], xp[(2 * s + 1) * 8 + m]};
+                            f32x2 acc = {e[m], od[m]};
+                            acc = __builtin_elementwise_fma(wv, xv, acc);
+                            e[m] = acc[0];
+                            od[m] = acc[1];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < 8; ++m) c_s[((wave * 3 + u) * 8 + m) * 64 + lane] = __fadd_rn(e[m], od[m]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (tid == 0) cyc[blockIdx.x] = t1 - t0;
+    // results of the last pass for the bitwise check (block 0)
+    if (blockIdx.x == 0) {
+        float* c_s = cs[(passes - 1) & 1];
+        for (int i = tid; i < 72 * 128; i += 512) out[i] = c_s[i];
+        if (VAR >= 4)
+            for (int i = tid; i < 24 * 8 * 64; i += 512) out[72 * 128 + i] = c_s[i];
+    }
+    if (sink == 12345.f) out[0] = sink;
+}
+
+int main() {
+    float *ref, *out;
+    unsigned long long* cyc;
+    hipMalloc(&ref, NCH * 128 * 4);
+    hipMalloc(&out, (72 * 128 + 24 * 8 * 64) * 4);
+    hipMalloc(&cyc, 256 * 8);
+    hipLaunchKernelGGL(ref_kernel, dim3(NCH), dim3(128), 0, 0, ref);
+    float* xg;
+    hipMalloc(&xg, NCH * 256 * 4);
+    hipLaunchKernelGGL(xf_kernel, dim3(NCH), dim3(256), 0, 0, xg);
+    float href[NCH * 128];
+    hipMemcpy(href, ref, sizeof(href), hipMemcpyDeviceToHost);
+    const int passes = 200;
+    const char* names[6] = {"mfma16 E/O (xl_mfma)", "mfma16 no LDS store", "mfma16 2 chunks in flight",
+                            "mfma 4x4x1 16 blocks", "VALU fma, x in SGPR", "VALU pk_fma"};
+    for (int var = 0; var < 6; ++var) {
+        hipEvent_t e0, e1;
+        hipEventCreate(&e0);
+        hipEventCreate(&e1);
+        auto launch = [&]() {
+            switch (var) {
+                case 0: hipLaunchKernelGGL(rate_kernel<0>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 1: hipLaunchKernelGGL(rate_kernel<1>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 2: hipLaunchKernelGGL(rate_kernel<2>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 3: hipLaunchKernelGGL(rate_kernel<3>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 4: hipLaunchKernelGGL(rate_kernel<4>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 5: hipLaunchKernelGGL(rate_kernel<5>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+            }
+        };
+        launch();
+        hipDeviceSynchronize();
+        hipEventRecord(e0);
+        launch();
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        unsigned long long hc[256];
+        hipMemcpy(hc, cyc, sizeof(hc), hipMemcpyDeviceToHost);
+        unsigned long long mx = 0;
+        for (int i = 0; i < 256; ++i) mx = hc[i] > mx ? hc[i] : mx;
+        // chunk-equivalents per SIMD per pass: 0-3: 2 waves x 9 chunks; 4-5: 2 waves x 3 x 4
+        const double ch = var <= 3 ? 18.0 : 24.0;
+        const double us_pass = ms * 1000.0 / passes;
+        printf("var %d %-28s %.3f us/pass  %.1f ns per chunk per SIMD  (%llu s_memtime ticks max)\n", var, names[var],
+               us_pass, us_pass * 1000.0 / ch, mx);
+        // bitwise check of block 0's last pass
+        static float h[72 * 128 + 24 * 8 * 64];
+        hipMemcpy(h, out, sizeof(h), hipMemcpyDeviceToHost);
+        int bad = 0, n = 0;
+        if (var == 0 || var == 2) {
+            for (int cc = 0; cc < 72; ++cc)
+                for (int m = 0; m < 8; ++m)
+                    for (int o = 0; o < 16; ++o, ++n) {
+                        const float r = href[((cc % NCH) * 8 + m) * 16 + o];
+                        // variant 0 / 2 wave of cc uses data chunk (cc % 8 + 8 u) % NCH = cc % NCH
+                        bad += memcmp(&r, &h[cc * 128 + m * 16 + o], 4) != 0;
+                    }
+        } else if (var == 3) {
+            for (int w = 0; w < 8; ++w)
+                for (int m = 0; m < 8; ++m)
+                    for (int o = 0; o < 16; ++o, ++n) {
+                        const float r = href[((w % NCH) * 8 + m) * 16 + o];
+                        bad += memcmp(&r, &h[(w * 8 + m) * 16 + o], 4) != 0;   // u = 0, s0: cc = w
+                    }
+        } else if (var >= 4) {
+            for (int w = 0; w < 8; ++w)
+                for (int m = 0; m < 8; ++m)
+                    for (int l = 0; l < 64; ++l, ++n) {
+                        const float r = href[((w % NCH) * 8 + m) * 16 + (l & 15)];
+                        bad += memcmp(&r, &h[72 * 128 + ((w * 3 + 0) * 8 + m) * 64 + l], 4) != 0;
+                    }
+        }
+        if (n) printf("      bitwise vs fmaf chains: %d / %d differ\n", bad, n);
+    }
+    return 0;
+}
