@@ -11,6 +11,14 @@
 //   4  VALU v_fma_f32: lane = output (64 per wave), 8 rows x E/O accumulators, x uniform
 //      (SGPR), weights converted from bf16 pairs (2 ops per k pair)
 //   5  as 4 with v_pk_fma_f32 (E and O of one row in one instruction)
+//   6  as 4, x from a VGPR (16 values per k pair, replicated over the 4 rows of 16 lanes)
+//      moved to SGPRs with v_readlane
+//   7  as 6, x broadcast by DPP row_newbcast inside v_fmac_f32 (no extra instruction)
+//   8  as 4, x f32 from LDS through uniform-address ds_read_b128 (broadcast into VGPRs)
+//  10  as 8, the wave's 4 16-lane slots reading 4 different chunks' x (4 LDS addresses)
+//  11  as 10 with xlayer.hip's inline-asm reads one k pair ahead (xl_chunk)
+//   9  as 3 with the operands converted from bf16 in the loop: W from registers (E4 layout:
+//      16 bf16 of one output and parity per lane), X from LDS (16 bf16 per lane)
 // Also checks 2, 3, 4, 5 bitwise against 0's chunk sums on random bf16 data.
 // Build: hipcc -O3 -ffp-contract=off --offload-arch=gfx950 tools/micro_xchunk.hip -o /tmp/mx
 #include <hip/hip_runtime.h>
@@ -76,6 +84,8 @@ __global__ __launch_bounds__(512) void rate_kernel(int passes, float* out, unsig
                                                    const float* __restrict__ xg) {
     __shared__ u32x4 xs[NCH][64];          // X16 lane fragments (variants 0-2)
     __shared__ float cs[2][24 * 8 * 64];   // chunk sums
+    __shared__ float xfl[NCH][32][8];      // X f32 [k][m] (variant 8)
+    __shared__ uint32_t x4[NCH][2][8][8];  // X bf16 [eo][m][s pairs] (variant 9)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int j = lane & 15, q = lane >> 4;
     // stage X
@@ -87,6 +97,14 @@ __global__ __launch_bounds__(512) void rate_kernel(int passes, float* out, unsig
             v[t] = (uint32_t)Xv(c, m, 2 * p) | ((uint32_t)Xv(c, m, 2 * p + 1) << 16);
         }
         xs[c][l] = v;
+    }
+    for (int i = tid; i < NCH * 256; i += 512) {
+        const int c = i / 256, k = (i / 8) % 32, m = i % 8;
+        xfl[c][k][m] = __uint_as_float((uint32_t)Xv(c, m, k) << 16);
+    }
+    for (int i = tid; i < NCH * 128; i += 512) {
+        const int c = i / 128, eo = (i / 64) % 2, m = (i / 8) % 8, sp = i % 8;   // s = 2 sp, 2 sp + 1
+        x4[c][eo][m][sp] = (uint32_t)Xv(c, m, 2 * (2 * sp) + eo) | ((uint32_t)Xv(c, m, 2 * (2 * sp + 1) + eo) << 16);
     }
     // W fragments in registers: chunk cc = wave + 8 u (u < 9) -> data chunk cc % NCH
     u32x4 w[9];
@@ -103,6 +121,8 @@ __global__ __launch_bounds__(512) void rate_kernel(int passes, float* out, unsig
     if constexpr (VAR <= 2) {
         for (int p = 0; p < passes; ++p) {
             float* c_s = cs[p & 1];
+#pragma unroll
+            for (int u = 0; u < 9; ++u) asm volatile("" : "+v"(w[u]));   // no hoisting out of the pass loop
             if constexpr (VAR == 2) {
 #pragma unroll
                 for (int u = 0; u < 9; u += 2) {
@@ -155,6 +175,8 @@ __global__ __launch_bounds__(512) void rate_kernel(int passes, float* out, unsig
         for (int p = 0; p < passes; ++p) {
             float* c_s = cs[p & 1];
 #pragma unroll
+            for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(wa[s]), "+v"(xa[s]));
+#pragma unroll
             for (int u = 0; u < 9; u += 3) {
                 f32x4 a0 = {0, 0, 0, 0}, a1 = a0, a2 = a0;
 #pragma unroll
@@ -182,6 +204,203 @@ __global__ __launch_bounds__(512) void rate_kernel(int passes, float* out, unsig
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
         if (passes < 0) sink = wa[0] + xa[0];
+    } else if constexpr (VAR == 9) {
+        const int b = lane >> 2, t = lane & 3, oq = b & 3, rq = (b >> 2) & 1, eo = b >> 3;
+        uint32_t wq[3][8];
+        for (int u = 0; u < 3; ++u)
+            for (int sp = 0; sp < 8; ++sp) {
+                const int c = (wave + 8 * u) % NCH, o = oq * 4 + t;
+                wq[u][sp] = (uint32_t)Wv(c, o, 2 * (2 * sp) + eo) | ((uint32_t)Wv(c, o, 2 * (2 * sp + 1) + eo) << 16);
+            }
+        for (int p = 0; p < passes; ++p) {
+            float* c_s = cs[p & 1];
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+#pragma unroll
+                for (int sp = 0; sp < 8; ++sp) asm volatile("" : "+v"(wq[u][sp]));
+#pragma unroll
+            for (int u = 0; u < 9; u += 3) {
+                f32x4 a[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+                u32x4 xw[3][2];
+#pragma unroll
+                for (int v = 0; v < 3; ++v) {
+                    const int c = (wave + 8 * (u + v)) % NCH;
+                    xw[v][0] = *(const u32x4*)&x4[c][eo][rq * 4 + t][0];
+                    xw[v][1] = *(const u32x4*)&x4[c][eo][rq * 4 + t][4];
+                }
+#pragma unroll
+                for (int sp = 0; sp < 8; ++sp)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int v = 0; v < 3; ++v) {
+                            const uint32_t ww = wq[v][sp], xx = xw[v][sp >> 2][sp & 3];
+                            a[v] = __builtin_amdgcn_mfma_f32_4x4x1f32(h ? bfhi(ww) : bflo(ww), h ? bfhi(xx) : bflo(xx),
+                                                                      a[v], 0, 0, 0);
+                        }
+#pragma unroll
+                for (int v = 0; v < 3; ++v) {
+                    f32x4 sv;
+                    for (int i = 0; i < 4; ++i) sv[i] = __fadd_rn(a[v][i], __shfl_xor(a[v][i], 32, 64));
+                    if (eo == 0) {
+                        const int cc = wave + 8 * (u + v);
+                        for (int i = 0; i < 4; ++i) c_s[(cc * 8 + rq * 4 + t) * 16 + oq * 4 + i] = sv[i];
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    } else if constexpr (VAR == 10 || VAR == 11) {
+        uint32_t wr[16];
+        for (int s = 0; s < 16; ++s) {
+            const int c = (wave * 4 + (lane >> 4)) % NCH, o = lane & 15;
+            wr[s] = (uint32_t)Wv(c, o, 2 * s) | ((uint32_t)Wv(c, o, 2 * s + 1) << 16);
+        }
+        for (int p = 0; p < passes; ++p) {
+            float* c_s = cs[p & 1];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(wr[s]));
+            int xo = ((wave * 4 + (lane >> 4)) % NCH) * 256;
+            asm volatile("" : "+v"(xo));
+            const float* xp = &xfl[0][0][0] + xo;
+#pragma unroll 1
+            for (int u = 0; u < 3; ++u) {
+                float e[8], od[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) e[m] = od[m] = 0.f;
+                if constexpr (VAR == 10) {
+#pragma unroll
+                    for (int s = 0; s < 16; ++s) {
+                        const float w0 = bflo(wr[s]), w1 = bfhi(wr[s]);
+                        const f32x4 xa = *(const f32x4*)&xp[(2 * s) * 8], xb = *(const f32x4*)&xp[(2 * s) * 8 + 4];
+                        const f32x4 xc = *(const f32x4*)&xp[(2 * s + 1) * 8], xd = *(const f32x4*)&xp[(2 * s + 1) * 8 + 4];
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            e[m] = fmaf(w0, xa[m], e[m]);
+                            e[4 + m] = fmaf(w0, xb[m], e[4 + m]);
+                            od[m] = fmaf(w1, xc[m], od[m]);
+                            od[4 + m] = fmaf(w1, xd[m], od[4 + m]);
+                        }
+                    }
+                } else {
+                    const uint32_t a0 = (uint32_t)(uintptr_t)xp;
+                    auto rd = [&](f32x4 (&x)[4], uint32_t addr) {
+                        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\tds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48"
+                                     : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]) : "v"(addr));
+                    };
+                    auto fence = [&]() {
+                        asm volatile("" : "+v"(e[0]), "+v"(e[1]), "+v"(e[2]), "+v"(e[3]), "+v"(e[4]), "+v"(e[5]), "+v"(e[6]), "+v"(e[7]));
+                        asm volatile("" : "+v"(od[0]), "+v"(od[1]), "+v"(od[2]), "+v"(od[3]), "+v"(od[4]), "+v"(od[5]), "+v"(od[6]), "+v"(od[7]));
+                    };
+                    auto fma8 = [&](uint32_t w, const f32x4 (&x)[4]) {
+                        const float w0 = bflo(w), w1 = bfhi(w);
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            e[m] = fmaf(w0, x[0][m], e[m]);
+                            e[4 + m] = fmaf(w0, x[1][m], e[4 + m]);
+                            od[m] = fmaf(w1, x[2][m], od[m]);
+                            od[4 + m] = fmaf(w1, x[3][m], od[4 + m]);
+                        }
+                    };
+                    f32x4 xa[4], xb[4];
+                    rd(xa, a0);
+#pragma unroll
+                    for (int s = 0; s < 16; s += 2) {
+                        fence();
+                        rd(xb, a0 + (s + 1) * 64);
+                        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa[0]), "+v"(xa[1]), "+v"(xa[2]), "+v"(xa[3]));
+                        fma8(wr[s], xa);
+                        if (s + 2 < 16) {
+                            fence();
+                            rd(xa, a0 + (s + 2) * 64);
+                            asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xb[0]), "+v"(xb[1]), "+v"(xb[2]), "+v"(xb[3]));
+                        } else {
+                            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xb[0]), "+v"(xb[1]), "+v"(xb[2]), "+v"(xb[3]));
+                        }
+                        fma8(wr[s + 1], xb);
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < 8; ++m) c_s[((wave * 3 + u) * 8 + m) * 64 + lane] = __fadd_rn(e[m], od[m]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    } else if constexpr (VAR == 8) {
+        uint32_t wr[16];
+        for (int s = 0; s < 16; ++s) {
+            const int c = wave % NCH, o = lane & 15;
+            wr[s] = (uint32_t)Wv(c, o, 2 * s) | ((uint32_t)Wv(c, o, 2 * s + 1) << 16);
+        }
+        for (int p = 0; p < passes; ++p) {
+            float* c_s = cs[p & 1];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(wr[s]));
+            int xo = (wave % NCH) * 256;
+            asm volatile("" : "+v"(xo));
+            const float* xp = &xfl[0][0][0] + xo;
+#pragma unroll 1
+            for (int u = 0; u < 3; ++u) {
+                float e[8], od[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) e[m] = od[m] = 0.f;
+#pragma unroll
+                for (int s = 0; s < 16; ++s) {
+                    const float w0 = bflo(wr[s]), w1 = bfhi(wr[s]);
+                    const f32x4 xa = *(const f32x4*)&xp[(2 * s) * 8], xb = *(const f32x4*)&xp[(2 * s) * 8 + 4];
+                    const f32x4 xc = *(const f32x4*)&xp[(2 * s + 1) * 8], xd = *(const f32x4*)&xp[(2 * s + 1) * 8 + 4];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        e[m] = fmaf(w0, xa[m], e[m]);
+                        e[4 + m] = fmaf(w0, xb[m], e[4 + m]);
+                        od[m] = fmaf(w1, xc[m], od[m]);
+                        od[4 + m] = fmaf(w1, xd[m], od[4 + m]);
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < 8; ++m) c_s[((wave * 3 + u) * 8 + m) * 64 + lane] = __fadd_rn(e[m], od[m]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    } else if constexpr (VAR >= 6) {
+        uint32_t wr[16];
+        float xv[16];
+        for (int s = 0; s < 16; ++s) {
+            const int c = wave % NCH, o = lane & 15, n = lane & 15;
+            wr[s] = (uint32_t)Wv(c, o, 2 * s) | ((uint32_t)Wv(c, o, 2 * s + 1) << 16);
+            xv[s] = xg[(c * 32 + 2 * s + (n >> 3)) * 8 + (n & 7)];
+        }
+        for (int p = 0; p < passes; ++p) {
+            float* c_s = cs[p & 1];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(wr[s]), "+v"(xv[s]));
+#pragma unroll 1
+            for (int u = 0; u < 3; ++u) {
+                float e[8], od[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) e[m] = od[m] = 0.f;
+#pragma unroll
+                for (int s = 0; s < 16; ++s) {
+                    const float w0 = bflo(wr[s]), w1 = bfhi(wr[s]);
+                    if constexpr (VAR == 6) {
+#pragma unroll
+                        for (int m = 0; m < 8; ++m) {
+                            e[m] = fmaf(w0, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv[s]), m)), e[m]);
+                            od[m] = fmaf(w1, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv[s]), 8 + m)), od[m]);
+                        }
+                    } else {
+#define XC_DPP(M, M8)                                                                                          \
+    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:" #M " row_mask:0xf bank_mask:0xf" : "+v"(e[M]) : "v"(xv[s]), "v"(w0)); \
+    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:" #M8 " row_mask:0xf bank_mask:0xf" : "+v"(od[M]) : "v"(xv[s]), "v"(w1));
+                        XC_DPP(0, 8) XC_DPP(1, 9) XC_DPP(2, 10) XC_DPP(3, 11) XC_DPP(4, 12) XC_DPP(5, 13) XC_DPP(6, 14)
+                        XC_DPP(7, 15)
+#undef XC_DPP
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < 8; ++m) c_s[((wave * 3 + u) * 8 + m) * 64 + lane] = __fadd_rn(e[m], od[m]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
     } else {
         // VALU: lane = output (64 outputs per wave: 4 "chunks" of 16 per instruction stream),
         // one chunk = 16 k pairs; a wave does 9 x 16-output chunks per pass as 9/4 wave-chunks
@@ -191,9 +410,13 @@ __global__ __launch_bounds__(512) void rate_kernel(int passes, float* out, unsig
             const int c = wave % NCH, o = lane & 15;
             wr[s] = (uint32_t)Wv(c, o, 2 * s) | ((uint32_t)Wv(c, o, 2 * s + 1) << 16);
         }
-        const float* xp = xg + (__builtin_amdgcn_readfirstlane(wave) % NCH) * 256;
         for (int p = 0; p < passes; ++p) {
             float* c_s = cs[p & 1];
+            int xo = (__builtin_amdgcn_readfirstlane(wave) % NCH) * 256;
+            asm volatile("" : "+s"(xo));
+            const float* xp = xg + xo;
+#pragma unroll
+            for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(wr[s]));
 #pragma unroll 1
             for (int u = 0; u < 3; ++u) {
                 float e[8], od[8];
@@ -255,9 +478,11 @@ int main() {
     float href[NCH * 128];
     hipMemcpy(href, ref, sizeof(href), hipMemcpyDeviceToHost);
     const int passes = 200;
-    const char* names[6] = {"mfma16 E/O (xl_mfma)", "mfma16 no LDS store", "mfma16 2 chunks in flight",
-                            "mfma 4x4x1 16 blocks", "VALU fma, x in SGPR", "VALU pk_fma"};
-    for (int var = 0; var < 6; ++var) {
+    const char* names[12] = {"mfma16 E/O (xl_mfma)", "mfma16 no LDS store", "mfma16 2 chunks in flight",
+                            "mfma 4x4x1 16 blocks", "VALU fma, x in SGPR", "VALU pk_fma", "VALU fma, x readlane",
+                            "VALU fmac, x DPP newbcast", "VALU fma, x LDS broadcast", "mfma 4x4x1 bf16 in loop",
+                             "VALU fma, x LDS 4 slots", "VALU 4 slots asm pipeline"};
+    for (int var = 0; var < 12; ++var) {
         hipEvent_t e0, e1;
         hipEventCreate(&e0);
         hipEventCreate(&e1);
@@ -269,6 +494,12 @@ int main() {
                 case 3: hipLaunchKernelGGL(rate_kernel<3>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
                 case 4: hipLaunchKernelGGL(rate_kernel<4>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
                 case 5: hipLaunchKernelGGL(rate_kernel<5>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 6: hipLaunchKernelGGL(rate_kernel<6>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 7: hipLaunchKernelGGL(rate_kernel<7>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 8: hipLaunchKernelGGL(rate_kernel<8>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 9: hipLaunchKernelGGL(rate_kernel<9>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 10: hipLaunchKernelGGL(rate_kernel<10>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
+                case 11: hipLaunchKernelGGL(rate_kernel<11>, dim3(256), dim3(512), 0, 0, passes, out, cyc, xg); break;
             }
         };
         launch();
@@ -284,7 +515,7 @@ int main() {
         unsigned long long mx = 0;
         for (int i = 0; i < 256; ++i) mx = hc[i] > mx ? hc[i] : mx;
         // chunk-equivalents per SIMD per pass: 0-3: 2 waves x 9 chunks; 4-5: 2 waves x 3 x 4
-        const double ch = var <= 3 ? 18.0 : 24.0;
+        const double ch = (var <= 3 || var == 9) ? 18.0 : 24.0;
         const double us_pass = ms * 1000.0 / passes;
         printf("var %d %-28s %.3f us/pass  %.1f ns per chunk per SIMD  (%llu s_memtime ticks max)\n", var, names[var],
                us_pass, us_pass * 1000.0 / ch, mx);
@@ -300,12 +531,19 @@ int main() {
                         // variant 0 / 2 wave of cc uses data chunk (cc % 8 + 8 u) % NCH = cc % NCH
                         bad += memcmp(&r, &h[cc * 128 + m * 16 + o], 4) != 0;
                     }
-        } else if (var == 3) {
+        } else if (var == 3 || var == 9) {
             for (int w = 0; w < 8; ++w)
                 for (int m = 0; m < 8; ++m)
                     for (int o = 0; o < 16; ++o, ++n) {
                         const float r = href[((w % NCH) * 8 + m) * 16 + o];
                         bad += memcmp(&r, &h[(w * 8 + m) * 16 + o], 4) != 0;   // u = 0, s0: cc = w
+                    }
+        } else if (var >= 10) {
+            for (int w = 0; w < 8; ++w)
+                for (int m = 0; m < 8; ++m)
+                    for (int l = 0; l < 64; ++l, ++n) {
+                        const float r = href[(((w * 4 + (l >> 4)) % NCH) * 8 + m) * 16 + (l & 15)];
+                        bad += memcmp(&r, &h[72 * 128 + ((w * 3 + 0) * 8 + m) * 64 + l], 4) != 0;
                     }
         } else if (var >= 4) {
             for (int w = 0; w < 8; ++w)
