@@ -44,10 +44,11 @@ __device__ __forceinline__ float ref_sumsq(const float (&v)[8], bool active, int
         for (int j = 0; j < 8; ++j) sq[c * 8 + j] = __fmul_rn(v[j], v[j]);
     }
     __syncthreads();
+    float a0 = 0.f;
     if (c < 32) {
         const int k = c >> 3, j = c & 7;
         const int size_ilp = nvec / 4;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        float a1 = 0.f, a2 = 0.f, a3 = 0.f;
         int i = 0;
         // each level-0 row of 16 is read into registers first (one LDS round trip, not 16
         // dependent ones), then added in order
@@ -78,19 +79,23 @@ __device__ __forceinline__ float ref_sumsq(const float (&v)[8], bool active, int
         a0 = __fadd_rn(__fadd_rn(__fadd_rn(a0, a1), a2), a3);
         if (k == 0)
             for (int t = size_ilp * 4; t < nvec; ++t) a0 = __fadd_rn(a0, sq[t * 8 + j]);
-        sq[nvec * 8 + c] = a0;
+    }
+    // the 8 lanes ((acc0 + acc1) + acc2) + acc3, then their sum in lane order, in wave 0 (the
+    // cascade threads are its lanes 0..31); the total goes to every thread through one LDS word
+    if (c < 64) {
+        const int l = c & 7;
+        float a = c < 32 ? a0 : 0.f;
+        const float s1 = __shfl(a, l + 8, 64), s2 = __shfl(a, l + 16, 64), s3 = __shfl(a, l + 24, 64);
+        const float lane_sum = __fadd_rn(__fadd_rn(__fadd_rn(a, s1), s2), s3);   // valid in lanes 0..7
+        float tot = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) tot = __fadd_rn(tot, __shfl(lane_sum, jj, 64));
+        if (c == 0) sq[nvec * 8] = tot;
     }
     __syncthreads();
-    float lanes[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        lanes[j] = __fadd_rn(__fadd_rn(__fadd_rn(sq[nvec * 8 + j], sq[nvec * 8 + 8 + j]), sq[nvec * 8 + 16 + j]),
-                             sq[nvec * 8 + 24 + j]);
-    float tot = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) tot = __fadd_rn(tot, lanes[j]);
-    __syncthreads();   // sq is reused by the launch's second RMSNorm
-    return tot;
+    // no trailing barrier: the next sum of squares writes sq[< nvec 8] only, and reads it (and
+    // rewrites this word) after its own barrier
+    return sq[nvec * 8];
 }
 
 // the exact RMSNorm(1 + w) of one row held 8 values per thread (norm.hip rms8<true>)

@@ -264,9 +264,12 @@ struct XlGemvLds {
 // weights are requested before the current pass's MFMAs (two register buffers), and the
 // folder threads fold pass i while the other waves run pass i + 1's MFMAs (one barrier per
 // pass)
-template <int EPI, bool PART, typename TaskOf, typename Wait>
+struct XlNoAfter {
+    __device__ void operator()(int) const {}
+};
+template <int EPI, bool PART, typename TaskOf, typename Wait, typename After = XlNoAfter>
 __device__ __forceinline__ void xl_gemv(const XlGemv& s, int t0, int t1, TaskOf task_of, const XlGemvLds& L,
-                                        Wait wait) {
+                                        Wait wait, After after = After()) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (t0 >= t1) return;
     float acc = 0.f;   // folder threads: the chain across a task's passes
@@ -289,6 +292,7 @@ __device__ __forceinline__ void xl_gemv(const XlGemv& s, int t0, int t1, TaskOf 
             acc = XL_DBG_VAR == 2 ? cs[tid] : xl_fold(cs, t.kb_hi - t.kb_lo, tid, t.first ? 0.f : acc);
             if (t.last) xl_store<EPI, PART>(s, t, tid >> 4, tid & 15, acc);
         }
+        if (t.last) after(i);   // uniform: the task's outputs are stored (by the folder threads)
     };
     for (int i = t0; i < t1; i += 2) {
         pass(wa, wb, i, L.cs0);
@@ -297,14 +301,18 @@ __device__ __forceinline__ void xl_gemv(const XlGemv& s, int t0, int t1, TaskOf 
     xl_lds_barrier();   // the folds are done before the LDS is reused
 }
 
+struct XlNoTs {
+    __device__ void operator()(int) const {}
+};
+
 // ---------------------------------------------------------------- exact norm (one row)
 // resid_norm_kernel<NS, SRC, true> for one row with post, residual and pre (512 threads, the
 // first d / 8 active): v = bf16(delta) (NS = 0) or bf16((0 + p0) + p1) (NS = 2, the down
 // parts), post-norm, + h, pre-norm. The row's h stays in LDS between the launch's three
 // norms (hrow) and goes back to HBM at N3; xn goes out row-major (plain) and in X16 (sc1).
-template <int NS, typename Wait>
+template <int NS, typename Wait, typename Ts = XlNoTs>
 __device__ __forceinline__ void xl_norm_row(const XLayerArgs& a, int m, const bf16_t* post_w, const bf16_t* pre_w,
-                                            u32x4* hrow, bool first, bool last, float* sq, Wait wait) {
+                                            u32x4* hrow, bool first, bool last, float* sq, Wait wait, Ts ts = Ts()) {
     const int d = XL_D, c = threadIdx.x;
     const bool active = 8 * c < d;
     const int cc = active ? c : d / 8 - 1;
@@ -344,7 +352,9 @@ __device__ __forceinline__ void xl_norm_row(const XLayerArgs& a, int m, const bf
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = rbf(v[j]);
     }
+    ts(0);
     rms8_exact(v, active, d, w_post, a.eps, sq);
+    ts(1);
     {
         float r8[8];
 #pragma unroll
@@ -363,7 +373,9 @@ __device__ __forceinline__ void xl_norm_row(const XLayerArgs& a, int m, const bf
         hrow[c] = hw;
         if (last) *(u32x4*)(a.h + (long)m * d + 8 * c) = hw;   // read by the next launch
     }
+    ts(2);
     rms8_exact(v, active, d, w_pre, a.eps, sq);
+    ts(3);
     if (active) {
         u32x4 pk;
 #pragma unroll
@@ -392,8 +404,9 @@ struct XlAttnLds {
     float tmp[8][XL_G][32];
     float l_s[XL_G];
 };
-template <typename Wait>
-__device__ __forceinline__ void xl_cross_attn(const XLayerArgs& a, int qi, int kvh, int z, XlAttnLds& S, Wait wait) {
+template <typename Wait, typename Ts = XlNoTs>
+__device__ __forceinline__ void xl_cross_attn(const XLayerArgs& a, int qi, int kvh, int z, XlAttnLds& S, Wait wait,
+                                              Ts ts = Ts()) {
     constexpr int D = XL_HD, G = XL_G, NCB = D / 32, H2 = D / 2, DZ = 32, DP = DZ / 2, NG8 = 8, CH = 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kl = (tid & 255) >> 2, qa = tid & 3;
     const bool on = tid < 256;
@@ -429,6 +442,7 @@ __device__ __forceinline__ void xl_cross_attn(const XLayerArgs& a, int qi, int k
         }
     }
     __syncthreads();
+    ts(0);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -454,16 +468,17 @@ __device__ __forceinline__ void xl_cross_attn(const XLayerArgs& a, int qi, int k
         if (on && lane == 0) S.wmax[wave][g] = mx;
     }
     __syncthreads();
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
+    ts(1);
+    // exact p of the block, both q heads at once (threads g * 64 + key)
+    if (tid < G * CH) {
+        const int g = tid / CH, kk = tid % CH;
         const float mb = fmaxf(fmaxf(S.wmax[0][g], S.wmax[1][g]), fmaxf(S.wmax[2][g], S.wmax[3][g]));
-        if (tid < CH) {
-            const float p = tid < span ? sdpa_p(__fsub_rn(S.ss[g][tid], mb), tid, span) : 0.f;
-            S.pex[g][tid] = p;
-            S.pbf[g][tid] = rbf(p);
-        } else if (tid < CH + 16) {
-            S.pex[g][tid] = 0.f;
-        }
+        const float p = kk < span ? sdpa_p(__fsub_rn(S.ss[g][kk], mb), kk, span) : 0.f;
+        S.pex[g][kk] = p;
+        S.pbf[g][kk] = rbf(p);
+    } else if (tid < G * CH + G * 16) {
+        const int i = tid - G * CH;
+        S.pex[i / 16][CH + i % 16] = 0.f;
     }
     __syncthreads();
     if (wave < G) {
@@ -473,6 +488,7 @@ __device__ __forceinline__ void xl_cross_attn(const XLayerArgs& a, int qi, int k
         const float l = fmaf(sdpa_block_rescale(-INFINITY, mb), 0.f, ts);
         if (lane == 0) S.l_s[g] = l;
     }
+    ts(2);
     const int ngrp = (span + 7) / 8;
     if (vlane && gl < ngrp) {
         const int k0 = gl * 8, cn = min(8, span - k0);
@@ -510,6 +526,7 @@ __device__ __forceinline__ void xl_cross_attn(const XLayerArgs& a, int qi, int k
         __builtin_amdgcn_raw_buffer_store_b16(o, orr, (int)(x16_off(qi, col, XL_QD / 32) * 2), 0, XL_AUX_SC1);
     }
     __syncthreads();   // the LDS scratch is reused by the next task
+    ts(3);
 }
 
 // contiguous run [lo, hi) of n items over `workers` workers (worker w)
@@ -517,6 +534,35 @@ __device__ __forceinline__ void xl_run(int n, int workers, int w, int& lo, int& 
     const int base = n / workers, extra = n - base * workers;
     lo = w * base + min(w, extra);
     hi = lo + base + (w < extra ? 1 : 0);
+}
+// G and D tasks of worker w (a G task is one 72-chunk pass, a D task two), so that no worker
+// runs more than 7 passes and the workers with two D tasks are off the critical path: the
+// xd = nd - nw "light" workers run 3 G tasks of K part 0 and then 2 D tasks of part 0 (ready
+// once every part-0 G task is done, which every worker runs first); the other "heavy" workers
+// run 2-3 part-0 G tasks, then 2-3 part-1 G tasks, then one D task. Before: both runs put
+// their extra tasks on the same low workers (9 passes; D end 90.7 us against 82.6 median).
+// Requires nw <= nd <= 2 nw (checked by xlayer_launch through nb >= 144 + M).
+struct XlGdRuns {
+    int g0_lo, n0, g1_lo, n1, d_lo, nd;   // part-0 G run, part-1 G run (groups), D task run
+};
+__device__ __forceinline__ XlGdRuns xl_gd_runs(int ng, int ntd, int nw, int w) {
+    const int half = ng / 2, xd = ntd - nw, H = nw - xd;
+    XlGdRuns r;
+    if (w < xd) {
+        r = XlGdRuns{3 * w, 3, half, 0, 2 * w, 2};
+    } else {
+        const int h = w - xd;
+        const int e0 = half - 3 * xd - 2 * H;             // heavy workers with 3 part-0 tasks
+        const int b1 = half / H, e1 = half - b1 * H;      // part-1 base count, extras
+        const int e1a = min(e1, H - e0), e1b = e1 - e1a;  // extras on the 2-part-0 workers, then on the first
+        r.n0 = 2 + (h < e0 ? 1 : 0);
+        r.g0_lo = 3 * xd + 2 * h + min(h, e0);
+        r.n1 = b1 + ((h >= e0 && h - e0 < e1a) || h < e1b ? 1 : 0);
+        r.g1_lo = half + b1 * h + min(h, e1b) + max(0, min(h - e0, e1a));
+        r.d_lo = 2 * xd + h;
+        r.nd = 1;
+    }
+    return r;
 }
 
 // ---------------------------------------------------------------- the launch
@@ -559,10 +605,13 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     }
     // ---- N1 (norm workgroups)
     if (normwg) {
-        xl_norm_row<0>(a, nrow, a.n1_post, a.n1_pre, hrow, true, false, sq, [&] {
-            xl_wait_wg<8>(set, XC_O1, (unsigned)(d / 16), tmo, 21u);
-            XL_TS(19);
-        });
+        xl_norm_row<0>(
+            a, nrow, a.n1_post, a.n1_pre, hrow, true, false, sq,
+            [&] {
+                xl_wait_wg<8>(set, XC_O1, (unsigned)(d / 16), tmo, 21u);
+                XL_TS(19);
+            },
+            [&](int k) { XL_TS(20 + k); });
         xl_publish(set, XC_N1, 1u);
         XL_TS(2);
     }
@@ -585,10 +634,13 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
         int done = 0;
         for (int t = bu; t < ntask; t += nb) {
             const int qi = t % M, kvh = (t / M) % XL_HKV, z = t / (M * XL_HKV);
-            xl_cross_attn(a, qi, kvh, z, al, [&] {
-                xl_wait_wg<1>(set, XC_Q + kvh, 32u, tmo, 23u);
-                XL_TS(5);
-            });
+            xl_cross_attn(
+                a, qi, kvh, z, al,
+                [&] {
+                    xl_wait_wg<1>(set, XC_Q + kvh, 32u, tmo, 23u);
+                    XL_TS(5);
+                },
+                [&](int k) { XL_TS(24 + k); });
             ++done;
         }
         if (done) xl_publish(set, XC_A + (bu & 7), (unsigned)done);
@@ -619,17 +671,33 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     // ---- G: gate/up + GeGLU, contiguous runs of the 1 152 groups over the nw workers;
     // arrivals counted per down K part (groups [0, 576) hold the act features of part 0)
     const int ngu = 2 * XL_F / 16, half = ngu / 2;
+    const int ngd = d / 16, ntd = 2 * ngd;
+    const XlGdRuns gd = xl_gd_runs(ngu, ntd, nw, bu);
     if (!normwg) {
-        int lo, hi;
-        xl_run(ngu, nw, bu, lo, hi);
+        const int ngt = gd.n0 + gd.n1;
         const XlGemv s{a.Wgu, d / 32, xl_rsrc(a.xn16, 16u * d * 2u), 2 * XL_F, M, xl_rsrc(a.act16, 16u * XL_F * 2u),
                        xl_rsrc(nullptr, 0u), true, d / 32};
-        xl_gemv<EPI_GEGLU, false>(s, lo, hi, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
+        // part 0's arrivals are published as soon as the worker's part-0 tasks are stored (the
+        // down tasks of part 0 wait on those only), part 1's at the end
+        const bool early0 = gd.n1 > 0;
+        xl_gemv<EPI_GEGLU, false>(
+            s, 0, ngt,
+            [&](int i) { return XlTask{i < gd.n0 ? gd.g0_lo + i : gd.g1_lo + (i - gd.n0), 0, d / 32, 0, 0, true, true}; },
+            gl,
                                   [&] {
                                       xl_wait_wg<1>(set, XC_N2, (unsigned)M, tmo, 26u);
                                       XL_TS(11);
+                                  },
+                                  [&](int i) {
+                                      if (early0 && i == gd.n0 - 1) {
+                                          xl_drain();
+                                          __syncthreads();
+                                          if (tid == 0)
+                                              __hip_atomic_fetch_add(xline(set, XC_G0 + (bu & 7)), (unsigned)gd.n0,
+                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                      }
                                   });
-        const int n0 = max(0, min(hi, half) - lo), n1 = max(0, hi - max(lo, half));
+        const int n0 = early0 ? 0 : gd.n0, n1 = gd.n1;
         xl_drain();
         __syncthreads();
         if (tid == 0) {
@@ -641,10 +709,8 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
         XL_TS(12);
     }
     // ---- D: down in the reference's two K parts, task t = part * 144 + group
-    const int ngd = d / 16, ntd = 2 * ngd;
     if (!normwg) {
-        int lo, hi;
-        xl_run(ntd, nw, bu, lo, hi);   // tasks (part, group); two passes of 72 chunks each
+        const int lo = gd.d_lo, hi = gd.d_lo + gd.nd;   // tasks (part, group); two passes of 72 chunks each
         const XlGemv s{a.Wd, XL_F / 32, xl_rsrc(a.act16, 16u * XL_F * 2u), d, M, xl_rsrc(nullptr, 0u),
                        xl_rsrc(a.dpart, (uint32_t)(2 * M * d * 4)), false, XL_DOWN_KBC};
         const bool need0 = lo < ngd && hi > lo, need1 = hi > ngd;

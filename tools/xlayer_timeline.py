@@ -17,7 +17,8 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-POINTS = {0: "start", 1: "O1 end", 19: "N1 wait done", 2: "N1 end", 3: "Q wait done", 4: "Q end",
+POINTS = {20: "N1 delta in", 21: "N1 rms post", 22: "N1 resid", 23: "N1 rms pre", 24: "A q staged",
+          25: "A scores", 26: "A softmax", 27: "A pv+store",0: "start", 1: "O1 end", 19: "N1 wait done", 2: "N1 end", 3: "Q wait done", 4: "Q end",
           5: "A wait done", 6: "A end", 7: "O wait done", 8: "O end", 9: "N2 wait done", 10: "N2 end",
           11: "G wait done", 12: "G end", 13: "D wait done", 14: "D end", 15: "N3 wait done", 16: "N3 end",
           17: "QKV wait done", 18: "QKV end"}
@@ -60,7 +61,7 @@ def main():
         t0 = ts[live, 0].min()
         print(f"--- rep {rep} variant {var} ({['product', 'no MFMA', 'no fold', 'no weight loads'][var]}): "
               f"{int(live.sum())} workgroups, avg launch {us.value:.2f} us (timed rotation)")
-        for k in (0, 1, 19, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18):
+        for k in (0, 1, 19, 20, 21, 22, 23, 2, 3, 4, 5, 24, 25, 26, 27, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18):
             v = ts[live, k]
             v = v[v > 0]
             if not len(v):
