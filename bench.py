@@ -327,7 +327,7 @@ def main():
                      "orders)")
         traffic_x = None
         if os.path.exists(pmc_x) and B == 8:
-            traffic_x = json.load(open(pmc_x)).get("hbm_bytes_per_launch")
+            traffic_x = json.load(open(pmc_x)).get("hbm_bytes_per_call")
         ach_x = xbytes / (us_x.value * 1e-6) / 1e9
         parity_roof = {"bound": "hbm", "achieved": round(ach_x, 1), "peak": 8000.0, "unit": "GB/s",
                        "frac": round(ach_x / 8000.0, 4), "traffic": traffic_x, "kernel": kname,

@@ -29,6 +29,13 @@ OPS = {
                             "T_x=60, 2b-2b widths (tools/pmc_fused.py: 26 layers rotated, 4.3 GB > 256 MiB Infinity "
                             "Cache); algorithmic = weights + cross K/V + o slabs, h, norm weights, RoPE rows in + h, "
                             "q|k|v slabs out"},
+    "xlayer": {"kernels": ["xlayer_kernel"],
+               "algorithmic": None,   # _lib.xlayer_bytes(8, bb, 60, 26): the average over a step's 26 layers
+               "what": "parity mode's persistent decode layer after the self attention (o-proj -> norm -> cross-q "
+                       "-> PM cross attention -> cross-o -> norm -> gate/up GeGLU -> down in the reference's K "
+                       "parts -> norm -> next q|k|v; exact fp32 orders on the f32 MFMA), M=8, T_x=60, 2b-2b widths "
+                       "(tools/pmc_xlayer.py: 26 layers rotated, 4.5 GB > 256 MiB Infinity Cache); algorithmic = "
+                       "weights + cross K/V + self-attention output, h in and out, in-launch hand-offs"},
     "attention": {"kernels": ["attn_decode_kernel<256, 2, false>", "attn_pvc_kernel<256, 2, 32>"],
                   "algorithmic": None,
                   "what": "decode self attention (scores + P.V/combine launches), 8 rows x 8/4 heads x 256, L ~ 527 "
@@ -55,7 +62,14 @@ def per_call(path, kernels):
 def main(op, out_dir, dst):
     spec = OPS[op]
     alg = spec["algorithmic"]
-    if alg is None and op == "fused_block":
+    if alg is None and op == "xlayer":
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import t5gemma_tts_amd  # noqa: F401
+        from t5gemma_tts_amd._lib import xlayer_bytes
+        from t5gemma_tts_amd.config import config_2b2b
+        bb = config_2b2b().backbone
+        alg = xlayer_bytes(8, bb, 60, bb.num_decoder_layers)
+    elif alg is None and op == "fused_block":
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         import t5gemma_tts_amd  # noqa: F401
         from t5gemma_tts_amd._lib import fused_block_bytes
