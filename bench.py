@@ -148,6 +148,9 @@ def main():
                     help="decode MLP half as three launches instead of the persistent fused launch (A/B)")
     ap.add_argument("--no-attn-flash", action="store_true",
                     help="fast path: decode self attention as the two-launch aten-order form (A/B)")
+    ap.add_argument("--no-attn-in-block", action="store_true",
+                    help="fast path: decode self attention as its own launch instead of the persistent layer "
+                         "launch's first stage (A/B)")
     ap.add_argument("--attn", choices=("sdpa", "eager"), default="sdpa",
                     help="the checkpoint's attn_implementation: eager (the reference default, tanh softcap 50) "
                          "runs parity mode's eager.hip restatement")
@@ -203,6 +206,8 @@ def main():
         eng.set_fused(False)
     if args.no_attn_flash:
         eng.set_attn_flash(False)
+    if args.no_attn_in_block:
+        eng.set_attn_in_block(False)
     codec = None
     if args.e2e:
         from t5gemma_tts_amd.codec import XCodec2Decoder, codec_44k, synthetic_codec_weights
@@ -354,14 +359,25 @@ def main():
         d, f = cfg.backbone.hidden_size, cfg.backbone.intermediate_size
         st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         if not args.no_fused:
-            us = C.c_float()
+            us, keys = C.c_float(), C.c_float()
             # 208 launches rotated over the 26 layers' weights (3.3 GB >> 256 MiB Infinity
-            # Cache): every launch streams from HBM, as inside a decode step
-            _lib.check(L.t5g_time_decode_mlp(eng.h, B, 208, st, C.byref(us)), "time_decode_mlp")
+            # Cache): every launch streams from HBM, as inside a decode step; with the self
+            # attention inside (stage S) when the step runs it so
+            rc_s = _lib.T5G_EUNSUPPORTED if args.no_attn_in_block else \
+                L.t5g_time_decode_layer(eng.h, B, 208, st, C.byref(us), C.byref(keys))
+            if rc_s != 0:
+                if rc_s != _lib.T5G_EUNSUPPORTED:
+                    _lib.check(rc_s, "time_decode_layer")
+                keys.value = 0.0
+                _lib.check(L.t5g_time_decode_mlp(eng.h, B, 208, st, C.byref(us)), "time_decode_mlp")
             if B <= 16:   # the step runs the whole post-self-attention block in one launch
                 us_k, kname = us.value, _lib.FUSED_BLOCK_KERNEL
-                alg_bytes = _lib.fused_block_bytes(B, wl_tx, d, f)
-                pmc = os.path.join(REPO, "profiles", "r04_pmc_fused_block.json")   # this round's kernel
+                alg_bytes = _lib.fused_block_bytes(B, wl_tx, d, f, self_keys=keys.value)
+                if keys.value > 0:
+                    kname = _lib.FUSED_BLOCK_S_KERNEL
+                    pmc = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s.json")
+                else:
+                    pmc = os.path.join(REPO, "profiles", "r04_pmc_fused_block.json")
             else:
                 us_k, alg_bytes, kname = us.value, _lib.fused_mlp_bytes(B, d, f), _lib.FUSED_MLP_KERNEL
                 pmc = os.path.join(REPO, "profiles", "r03_pmc_fused_mlp.json")

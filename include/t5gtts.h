@@ -304,6 +304,18 @@ int t5g_attention_decode_flash(const t5g_attn_decode_args* args, void* stream);
  * T5GemmaSelfAttention :264-304; no reference-side equivalent switch. */
 int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable);
 
+/* Fast-path decode self attention as stage S of the persistent layer launch (default 1; needs
+ * the flash form and t5g_engine_set_fused): the flash launch's arithmetic on the launch's
+ * workgroups (three 64-key chunks each), the q|k|v slabs of the previous launch in, att_self
+ * handed to the o-projection stage in-launch -- no attention launch between the layers,
+ * bitwise equal to the flash launch followed by the launch without S. Calls whose rows x kv
+ * heads x ceil(chunks / 3) exceed the CU count keep the separate launch. Replaces the
+ * reference's per-layer self-attention call inside PMDecoderLayer
+ * (hf_export/modeling_t5gemma_voice.py:256-323, [tf] modeling_t5gemma.py:264-304).
+ * t5g_engine_attn_in_block_launches: layer launches issued with S (captured ones once). */
+int t5g_engine_set_attn_in_block(t5g_engine* e, int32_t enable);
+int t5g_engine_attn_in_block_launches(t5g_engine* e, int64_t* n);
+
 /* Sampler launch shape: 0 (default) the 16-slice multi-block kernel, falling back per row to
  * the single-block kernel when a row's top-k / survivor set exceeds it; 1 the single-block
  * kernel only. Both pick the same tokens (tests/test_gpu_sampler.py). */
@@ -345,6 +357,11 @@ int t5g_engine_poison_handoff(t5g_engine* e, uint32_t code);
 /* Average device time (us, hipEvents on `stream`) of the fused decode-MLP launch at B rows,
  * rotating over the decoder layers (bench.py roofline leg; no reference equivalent). */
 int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us);
+/* The same for the persistent layer launch WITH the self-attention stage S (the fast decode
+ * step's launch; T5G_EUNSUPPORTED when the call would not take it), at the cache lengths the
+ * last call left; *keys = keys one launch reads per kv head, summed over the rows and
+ * averaged over the layers (bench.py prices the K / V stream with it). */
+int t5g_time_decode_layer(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us, float* keys);
 /* Parity mode (after t5g_engine_set_exact(e, 1, ...) and one parity call): average device time
  * (us, hipEvents on `stream`) of one decoder layer's six exact decode Linear launches at B
  * rows (q|k|v, o, cross-q, cross-o, gate/up + GeGLU, down in the reference's K parts), layers

@@ -135,6 +135,9 @@ SIGNATURES = {
     "t5g_engine_set_fused": (C.c_int, [_P, _I]),
     "t5g_engine_xlayer_launches": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "t5g_time_xlayer": (C.c_int, [_P, _I, _I, _P, C.POINTER(C.c_float)]),
+    "t5g_engine_set_attn_in_block": (C.c_int, [_P, _I]),
+    "t5g_engine_attn_in_block_launches": (C.c_int, [_P, C.POINTER(C.c_int64)]),
+    "t5g_time_decode_layer": (C.c_int, [_P, _I, _I, _P, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "t5g_engine_set_text_max": (C.c_int, [_P, _I]),
     "t5g_engine_set_audio_max": (C.c_int, [_P, _I]),
     "t5g_engine_poison_handoff": (C.c_int, [_P, C.c_uint32]),
@@ -246,6 +249,10 @@ FUSED_MLP_KERNEL = ("fused_mlp_kernel<1> (decode MLP half in one launch: cross-a
 FUSED_BLOCK_KERNEL = ("fused_block_kernel (decode layer after the self attention in one launch: "
                       "o-proj -> norm -> cross-q -> PM cross attention -> cross-o -> norm -> gate/up GeGLU -> down -> "
                       "norm -> next layer's q|k|v, 174.6 MB of weights)")
+FUSED_BLOCK_S_KERNEL = ("fused_block_kernel with stage S (decode layer in one launch: flash self attention "
+                        "over the cached K / V + append -> o-proj -> norm -> cross-q -> PM cross attention -> cross-o "
+                        "-> norm -> gate/up GeGLU -> down -> norm -> next layer's q|k|v, 174.6 MB of weights)")
+T5G_EUNSUPPORTED = -3
 
 
 def exact_linears_bytes(B: int, bb) -> int:
@@ -276,16 +283,23 @@ def xlayer_bytes(B: int, bb, text_len: int, n_layers: int) -> float:
 
 
 def fused_block_bytes(M: int, T_x: int, d: int = 2304, f: int = 9216, q_dim: int = 2048, kv_dim: int = 1024,
-                      n_layers: int = 26) -> float:
+                      n_layers: int = 26, self_keys: float = 0.0) -> float:
     """Algorithmic HBM bytes of one fused_block_kernel launch, averaged over a step's layers (the
     last layer projects no next q|k|v): self o, cross q / o, gate/up, down and the next layer's
     q|k|v weights; the self-attention output, h, the six norm weights, the rows' cross K / V
     (T_x keys) and RoPE rows in; h and the q|k|v slabs (last layer: the final normed rows) out.
     The o slabs, xn1, the q slabs, att, the cross-o slabs, xn, act and the down slabs are
-    in-launch hand-offs."""
+    in-launch hand-offs.
+    self_keys > 0: the launch runs the self attention as its stage S (t5g_time_decode_layer's
+    keys: per kv head, summed over the rows, averaged over the layers) -- the cached K / V
+    rows read (the appended one is computed, not read), the appended key / value written, the
+    layer's q|k|v slabs in; the attention output becomes an in-launch hand-off."""
     qkv_dim = q_dim + 2 * kv_dim
     base = 3 * q_dim * d * 2 + 2 * f * d * 2 + d * f * 2   # self o, cross q, cross o, gate/up, down
-    base += M * q_dim * 2 + M * d * 2 + 6 * d * 2 + M * T_x * 2 * kv_dim * 2 + M * 256 * 4 + M * d * 2
+    att_in = M * q_dim * 2
+    if self_keys > 0:
+        att_in = (self_keys - M) * kv_dim * 2 * 2 + M * kv_dim * 2 * 2 + 2 * M * qkv_dim * 4
+    base += att_in + M * d * 2 + 6 * d * 2 + M * T_x * 2 * kv_dim * 2 + M * 256 * 4 + M * d * 2
     mid = base + qkv_dim * d * 2 + 2 * M * qkv_dim * 4
     last = base + M * d * 2
     return ((n_layers - 1) * mid + last) / n_layers

@@ -125,6 +125,32 @@ __device__ __forceinline__ float xsum(float v) {
     return v;
 }
 
+// gfx950 cross-row exchanges on the VALU (v_permlane16/32_swap, no LDS round trip): the value
+// of lane l ^ 16 / l ^ 32, as xlane<16> / xlane<32>
+__device__ __forceinline__ float xlane16_v(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xlane32_v(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(((threadIdx.x >> 5) & 1) ? r[0] : r[1]);
+}
+// xsum<HI> (16 <= HI <= 64) with the same adds in the same order and no LDS exchange: the xor-16
+// / xor-32 partners through v_permlane*_swap, the xor-4 partner as a 4-lane row rotation (after
+// the xor-8 step lanes l and l ^ 8 hold equal values, so lane l + 4 and l - 4 (mod 16) both hold
+// lane l ^ 4's value)
+template <int HI>
+__device__ __forceinline__ float xsum_v(float v) {
+    static_assert(HI == 16 || HI == 32 || HI == 64, "butterfly width");
+    if constexpr (HI >= 64) v += xlane32_v(v);
+    if constexpr (HI >= 32) v += xlane16_v(v);
+    v += xlane<8>(v);
+    v += __builtin_amdgcn_update_dpp(0.f, v, 0x124, 0xf, 0xf, false);   // row_ror:4
+    v += xlane<2>(v);
+    v += xlane<1>(v);
+    return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
     if constexpr (sizeof(T) == 4 && __is_same(T, float)) {

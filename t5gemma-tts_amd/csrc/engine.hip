@@ -89,6 +89,10 @@ struct t5g_engine {
     // flash-form decode attention (fast path, t5g_engine_set_attn_flash): chunk partials,
     // chunk (max, sum), one arrival ticket per (row, kv head) -- zeroed here, left zero
     bool attn_flash = true;
+    // the flash decode self-attention as stage S of the persistent layer launch (fast path,
+    // t5g_engine_set_attn_in_block): no attention launch of its own between the layers
+    bool attn_in_block = true;
+    int64_t s_launches = 0;   // persistent layer launches run with stage S (tests)
     float* afpart = nullptr;    // [B][Hkv][nsplit][G][D]
     float* afstat = nullptr;    // [B][Hkv][nsplit][G][2]
     unsigned* aftick = nullptr; // [B][Hkv]
@@ -1148,6 +1152,32 @@ static FusedMlpArgs fused_block_args(t5g_engine* e, int M, int l) {
     return fa;
 }
 
+// stage S in front (fast path): the layer's flash decode self-attention inside the launch,
+// with decode_attention's arguments (the cache, the call's chunk grid, the q|k|v slabs);
+// false when the launch is not built for them (the attention then runs as its own launch)
+static bool fused_block_self(t5g_engine* e, int M, int l, FusedMlpArgs& fa) {
+    const t5g_config& c = e->c;
+    if (!e->attn_in_block || !e->attn_flash || !fa.Wo1) return false;
+    fa.self_attn = 1;
+    fa.qkv_in = e->part;
+    fa.sk = e->sk[l];
+    fa.sv = e->sv[l];
+    fa.s_cap = c.max_audio;
+    fa.s_nsplit = (c.max_audio + 63) / 64;
+    if (e->audio_max > 0 && e->audio_max < c.max_audio) fa.s_nsplit = (e->audio_max + 63) / 64;
+    fa.kv_len = e->kv_len;
+    fa.window = c.dec_sliding[l] ? c.sliding_window : 0;
+    fa.fpart = e->afpart;
+    fa.fstat = e->afstat;
+    fa.fticket = e->aftick;
+    if (fused_mlp_check(fa) != 0) {
+        fa.self_attn = 0;
+        return false;
+    }
+    (void)M;
+    return true;
+}
+
 static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row, const int* tok_t, const float* pos,
                         bool decode, hipStream_t st) {
     const t5g_config& c = e->c;
@@ -1256,6 +1286,18 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
                 if (rcq != 0) RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, s_qkv, nullptr, e->part, e->qkv_dim, EPI_F32, st));
             }
             qkv_done = false;
+            // the persistent layer launch with the attention as its stage S (bitwise equal to
+            // the flash launch below followed by the same launch without S)
+            if (e->fused_mlp && M <= 16 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 && s_qkv == 2 &&
+                e->q_dim == 2048 && c.n_dec_layers >= 2) {
+                FusedMlpArgs fa = fused_block_args(e, M, l);
+                if (fused_mlp_check(fa) == 0 && fused_block_self(e, M, l, fa)) {
+                    RC(fused_mlp(fa, st));
+                    ++e->s_launches;
+                    qkv_done = l != c.n_dec_layers - 1;
+                    continue;
+                }
+            }
             RC(decode_attention(e, M, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1, win, 0, true, pos, tab, s_qkv,
                                 e->qkv_dim, st));
         } else {
@@ -1632,6 +1674,21 @@ extern "C" int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable) {
     return T5G_OK;
 }
 
+extern "C" int t5g_engine_set_attn_in_block(t5g_engine* e, int32_t enable) {
+    if (!e) return T5G_EINVAL;
+    if (e->attn_in_block != (enable != 0)) {
+        e->attn_in_block = enable != 0;
+        drop_graphs(e);   // captured launches follow the flag
+    }
+    return T5G_OK;
+}
+
+extern "C" int t5g_engine_attn_in_block_launches(t5g_engine* e, int64_t* n) {
+    if (!e || !n) return T5G_EINVAL;
+    *n = e->s_launches;
+    return T5G_OK;
+}
+
 extern "C" int t5g_engine_set_text_max(t5g_engine* e, int32_t n) {
     if (!e || n < 0 || n > e->c.max_text) return T5G_EINVAL;
     const int before = e->text_max > 0 ? e->text_max : e->c.max_text;
@@ -1943,6 +2000,52 @@ extern "C" int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void
     if (rc) return rc == -1 ? T5G_EUNSUPPORTED : T5G_EHIP;
     *avg_us = ms * 1000.f / (float)n;
     return check_handoff(e, st);   // a timed launch that gave up would report a false rate
+}
+
+// hipEvent-timed persistent layer launches WITH the self-attention stage S, as the fast
+// decode step runs them (bench.py roofline leg): whole rotations over the layers at the
+// cache lengths the last call left (each launch re-appends its rows' last key and value, the
+// values the slabs in e->part give). *keys = the keys one launch reads per kv head, summed
+// over the rows and averaged over the layers (sliding layers clipped to their window).
+extern "C" int t5g_time_decode_layer(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us,
+                                     float* keys) {
+    if (!e || iters <= 0 || !avg_us || !keys || B <= 0 || B > e->c.max_batch || e->c.n_dec_layers < 2) return T5G_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const t5g_config& c = e->c;
+    const int L = c.n_dec_layers;
+    auto args = [&](int l, FusedMlpArgs& fa) {
+        fa = fused_block_args(e, B, l);
+        return fused_mlp_check(fa) == 0 && fused_block_self(e, B, l, fa);
+    };
+    FusedMlpArgs fa;
+    if (!args(0, fa)) return T5G_EUNSUPPORTED;
+    std::vector<int> len(B);
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(len.data(), e->kv_len, sizeof(int) * B, hipMemcpyDeviceToHost));
+    double ksum = 0.0;
+    for (int l = 0; l < L; ++l)
+        for (int b = 0; b < B; ++b) {
+            const int w = c.dec_sliding[l] ? c.sliding_window : 0;
+            ksum += w > 0 ? std::min(len[b], w) : len[b];
+        }
+    *keys = (float)(ksum / L);
+    const int n = (iters + L - 1) / L * L;
+    int rc = 0;
+    for (int l = 0; l < L && !rc; ++l) rc = args(l, fa) ? fused_mlp(fa, st) : -1;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, st));
+    for (int i = 0; i < n && !rc; ++i) rc = args(i % L, fa) ? fused_mlp(fa, st) : -1;
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    if (rc) return rc == -1 ? T5G_EUNSUPPORTED : T5G_EHIP;
+    *avg_us = ms * 1000.f / (float)n;
+    return check_handoff(e, st);
 }
 
 // work = scores | chunk maxima (fp32)

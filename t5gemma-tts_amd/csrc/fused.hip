@@ -42,8 +42,9 @@ constexpr int FM_NORM_UNITS = 3;  // gate/up units of a norm workgroup (tools/di
 constexpr unsigned FM_SPIN_MAX = 1u << 18;   // ~0.3-0.5 s of polling before a wait gives up
 
 // lines of a counter set (FusedMlpArgs::sync), one word per 128-byte line
-constexpr int L_N1 = 0, L_Q0 = 1, L_A0 = 9, L_O0 = 17, L_N2 = 25, L_SL0 = 26, L_D0 = 34, L_N3 = 42, L_P0 = 43;
-static_assert(L_P0 + 8 == FM_SET_LINES, "counter set layout");
+constexpr int L_N1 = 0, L_Q0 = 1, L_A0 = 9, L_O0 = 17, L_N2 = 25, L_SL0 = 26, L_D0 = 34, L_N3 = 42, L_P0 = 43,
+              L_S0 = 51;
+static_assert(L_S0 + 8 == FM_SET_LINES, "counter set layout");
 __device__ __forceinline__ unsigned* cline(unsigned* set, int line) { return set + line * FM_LINE; }
 constexpr int FS_NORM = L_N2 * FM_LINE;
 __device__ __forceinline__ int fs_slice(int s) { return (L_SL0 + s) * FM_LINE; }
@@ -556,7 +557,408 @@ constexpr int FB_GU_KB = FB_D / 32;                           // gate/up k-steps
 constexpr size_t FB_GU_OFF = (5 * FM_NW * 1024 + sizeof(FbAttnLds) + 16 + 64 * sizeof(float) + FB_D * 2 + 1023) / 1024 * 1024;
 constexpr size_t FB_LDS = FB_GU_OFF + (size_t)FB_GU_KB * 1024;
 
-template <bool XA_DUMMY = true>
+// ---- stage S: the layer's decode self-attention (a.self_attn), attn.hip
+// attn_decode_kernel<256, 2, true, true> + attn_flash_finish restated on this launch's 12
+// waves as three 4-wave groups, each one 64-key chunk in that kernel's lane map: the same
+// loads, q / new-key PM-RoPE, cache append, sums and roundings, so the launch stays bitwise
+// equal to the flash launch + the per-op chain. Chunk c of the call (rows in order, kv heads,
+// chunks from the row start) runs on workgroup c % nb, group c / nb, so the K / V stream is
+// spread over every CU. A chunk's partial goes out write-through with one ticket add per
+// chunk; the workgroup holding the last chunk of a (row, kv head) combines them in the flash
+// kernel's order (its whole workgroup, after every group's ticket) and publishes att_self on
+// line L_S0 + kv head, which O1's k-slice of that head pair waits for. Rows of <= 64 keys take
+// the kernel's one-block (aten-order) path in their group. Nothing in S waits, so every chunk
+// finishes and every (row, kv head) publishes exactly once.
+constexpr int FS_G = 2, FS_D = 256, FS_CH = 64, FS_LPK = FS_D / 8, FS_KPW = 64 / FS_LPK, FS_KPB = FS_KPW * 4,
+              FS_NIT = FS_CH / FS_KPB, FS_GRP = FM_NW / 4, FS_MAXROWS = 32,
+              FS_CMAX = 16;   // chunks per row (1 024 keys): the combine reads its records in one batch
+static_assert(FS_LPK == 32, "the P.V lanes of a key fold in one xor-32 step");
+struct FbSelfGrp {
+    f32x4 ored[4][FS_G][FS_LPK][2];
+    float sm[FS_G][FS_CH];
+    float pl[FS_G][FS_CH + 16];
+    float qs[FS_G][FS_D];
+    float kvnew[2][FS_D];
+    float stat_l[FS_G];
+    float cstat[FS_G][2];
+    float wts[FS_G][DEC_MAX_CHUNKS];   // the combine's chunk weights and sums
+    float lsum[FS_G];
+    int last;
+};
+struct FbSelfLds {
+    FbSelfGrp g[FS_GRP];
+    int rlo[FS_MAXROWS], rspan[FS_MAXROWS], rnch[FS_MAXROWS];
+};
+static_assert(sizeof(FbSelfLds) <= 5 * FM_NW * 1024, "stage S lives in the GEMV partial-sum LDS");
+
+// diagnostic timeline of stage S and O1 (T5G_DBG_TS library variant only,
+// tools/diag_fused_s.py): thread 0 (or `tid`) of every workgroup stores the 100 MHz clock at
+// numbered points, 32 slots per workgroup
+#ifdef T5G_DBG_TS
+__device__ unsigned long long* fs_ts_buf;
+extern "C" int t5g_dbg_set_fused_s(void* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(fs_ts_buf), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+// timing variants of stage S (never in the product): 1 no K / V loads, 2 one q|k|v slab
+// address for every lane, 3 every (row, kv head) reads row 0 / kv head 0's cache (L2 hits),
+// 4 the stage run twice (the second one warm: instruction cache, TLB, L2), 5 no K / V load
+// instructions at all
+__device__ int fs_dbg_var;
+extern "C" int t5g_dbg_set_fused_s_var(int v) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(fs_dbg_var), &v, sizeof(v)) == hipSuccess ? 0 : -1;
+}
+#define FS_DBG_VAR fs_dbg_var
+#define FS_TS_BY(k, tid)                                                                           \
+    do {                                                                                           \
+        if (threadIdx.x == (tid) && fs_ts_buf) fs_ts_buf[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define FS_DBG_VAR 0
+#define FS_TS_BY(k, tid) do { } while (0)
+#endif
+#define FS_TS(k) FS_TS_BY(k, 0)
+
+// barrier that waits for this wave's LDS traffic only (no vmcnt: loads stay in flight)
+__device__ __forceinline__ void fb_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& sl) {
+    constexpr int G = FS_G, D = FS_D, LPK = FS_LPK, KPW = FS_KPW, KPB = FS_KPB, NIT = FS_NIT;
+    const int tq = (int)threadIdx.x, wave = tq >> 6, lane = tq & 63;
+    const int grp = wave >> 2, gw = wave & 3, gt = tq & 255;
+    const int kg = lane / LPK, dl = lane % LPK;
+    const int M = a.M, Hkv = a.Hkv;
+    FbSelfGrp& L = sl.g[grp];
+    // this group's chunk slot (row m, kv head, chunk sp): slot c = sp x (M Hkv) + row x Hkv +
+    // kv head on workgroup c % nb, group c / nb -- known before the row lengths, so the q|k|v
+    // slabs and the RoPE row are requested with the row length; chunk-major, so the live
+    // chunks (sp < the row's count) fill group 0 of every workgroup before any group 1
+    // (fused_mlp_launch: slots <= 3 nb)
+    const int cidx = (int)blockIdx.x + grp * (int)gridDim.x;
+    const bool has_s = cidx < M * Hkv * a.s_nsplit;
+    const int sp = has_s ? cidx / (M * Hkv) : 0, rk = has_s ? cidx - sp * (M * Hkv) : 0;
+    const int m = rk / Hkv, kvh = rk - m * Hkv;
+    const int dvar = FS_DBG_VAR;
+    const int len = a.kv_len[m];
+    int role = 0, c4 = 0, g_own = 0, col;
+    if (gt < G * D / 4) {
+        g_own = gt / (D / 4);
+        c4 = gt % (D / 4);
+        col = (kvh * G + g_own) * D + 4 * c4;
+    } else {   // the appended key / value (used by the slot holding key t)
+        const int idx = gt - G * D / 4;
+        role = 1 + idx / (D / 4);   // 1: key, 2: value
+        c4 = idx % (D / 4);
+        col = (role == 1 ? a.q_dim : a.q_dim + Hkv * D) + kvh * D + 4 * c4;
+    }
+    const long uo = dvar == 2 ? 0 : col;
+    // unconditional (slots past the grid read row 0's): a load under a branch makes the
+    // compiler wait for everything in flight at the join, the row length included
+    const f32x4 u0 = *(const f32x4*)(a.qkv_in + (long)m * a.qkv_dim + uo);
+    const f32x4 u1 = *(const f32x4*)(a.qkv_in + ((long)M + m) * a.qkv_dim + uo);
+    const float* tr = a.rope_tab + (long)m * D + (8 * dl) % (D / 2);
+    f32x4 ca = *(const f32x4*)tr, cb = *(const f32x4*)(tr + 4);
+    f32x4 sa = *(const f32x4*)(tr + D / 2), sb = *(const f32x4*)(tr + D / 2 + 4);
+    // row geometry (attn_decode_kernel's rules: causal, the sliding window); a row of <= 64
+    // keys is one chunk (the one-block path; a row with no key still publishes)
+    const int t = len - 1;
+    const int hi = min(t + 1, len), lo = a.window > 0 ? max(0, t - a.window + 1) : 0;
+    const int span = max(hi - lo, 0);
+    const bool single = span <= FS_CH;
+    const int nch = single ? 1 : (span + FS_CH - 1) / FS_CH;
+    const bool has_c = has_s && sp < nch;
+    if (has_s && sp == 0 && gt == 0 && nch > a.s_nsplit)   // past the host's key bound: give every wait up
+        __hip_atomic_store(a.timeout, 18u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int c0 = lo + sp * FS_CH, c1 = min(hi, c0 + FS_CH), n = c1 - c0;
+    const bool gv = has_c && n > 0;
+    const bool has_t = gv && t >= c0 && t < c1;
+    if (gt == 0) L.last = 0;
+    const __amdgpu_buffer_rsrc_t ors = raw_rsrc(a.att_self, (uint32_t)(M * a.q_dim * 2));
+    const long nrec = (long)M * Hkv * a.s_nsplit;
+    const __amdgpu_buffer_rsrc_t prs = frag_rsrc(a.fpart, (uint32_t)(nrec * G * D * 4));
+    const __amdgpu_buffer_rsrc_t srs = frag_rsrc(a.fstat, (uint32_t)(nrec * G * 2 * 4));
+    const long hs = (long)a.s_cap * D, bs = hs * Hkv;
+    bf16_t* Kb = a.sk + (dvar == 3 ? 0 : m * bs + kvh * hs);
+    bf16_t* Vb = a.sv + (dvar == 3 ? 0 : m * bs + kvh * hs);
+    float c8[8], s8[8];
+    const __amdgpu_buffer_rsrc_t krs = frag_rsrc(Kb, (uint32_t)a.s_cap * D * 2u);
+    const __amdgpu_buffer_rsrc_t vrs = frag_rsrc(Vb, (uint32_t)a.s_cap * D * 2u);
+    // groups without a chunk request nothing (a wave-uniform branch): their loads would queue
+    // in the CU's memory pipeline ahead of the working groups' data
+    u32x4 kr[NIT], vr[NIT];
+    if (gv && dvar != 5) {
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int j = c0 + i * KPB + gw * KPW + kg;
+            const int off = (j < c1 && dvar != 1) ? (j * D + 8 * dl) * 2 : (int)0x7ffffff0;
+            kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
+            vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
+        }
+        // q (and the appended key / value) staged in the same block as the K / V requests, so
+        // the wait for the slabs counts exactly the requests behind them
+        f32x4 acc = u0;
+        acc += u1;
+        if (role == 0) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) L.qs[g_own][4 * c4 + jj] = rbf(acc[jj]);
+        } else if (has_t) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) L.kvnew[role - 1][4 * c4 + jj] = rbf(acc[jj]);
+        }
+        // the RoPE row consumed here too (an empty asm use): past the branch join the compiler
+        // would otherwise wait for nearly every K / V request before the q rotation
+        asm volatile("" : "+v"(ca), "+v"(cb), "+v"(sa), "+v"(sb));
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            c8[jj] = ca[jj];
+            c8[4 + jj] = cb[jj];
+            s8[jj] = sa[jj];
+            s8[4 + jj] = sb[jj];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) kr[i] = vr[i] = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) c8[jj] = s8[jj] = 0.f;
+    }
+    fb_lds_barrier();
+    FS_TS(2);
+    // groups without a chunk skip the arithmetic too (wave-uniform): their waves would take
+    // VALU issue slots from the working groups on the same SIMDs
+    if (gv) {
+        float q[G][8];
+        {
+            const float sg = dl < LPK / 2 ? -1.0f : 1.0f;
+            const int pbase = (8 * dl + D / 2) % D;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) {
+                    const float x = L.qs[g][8 * dl + jj];
+                    const float pr = L.qs[g][pbase + jj];
+                    q[g][jj] = rbf(rbf(x * c8[jj]) + rbf((sg * pr) * s8[jj]));
+                }
+        }
+        FS_TS(14);
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            // (keys past c1 were requested out of the descriptor's range: already zero)
+            const int j = c0 + i * KPB + gw * KPW + kg;
+            if (has_t && j == t) {
+                // key t: PM-RoPE of the new key, then append it and its value
+                const float sg = dl < LPK / 2 ? -1.0f : 1.0f;
+                const int pbase = (8 * dl + D / 2) % D;
+                u32x4 kw, vw;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    float ko[2], vo[2];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int dd = 8 * dl + 2 * jj + e;
+                        const float c = c8[2 * jj + e], sn = s8[2 * jj + e];
+                        const float x = L.kvnew[0][dd], pr = L.kvnew[0][pbase + 2 * jj + e];
+                        ko[e] = rbf(rbf(x * c) + rbf((sg * pr) * sn));
+                        vo[e] = L.kvnew[1][dd];
+                    }
+                    kw[jj] = pack2(ko[0], ko[1]);
+                    vw[jj] = pack2(vo[0], vo[1]);
+                }
+                kr[i] = kw;
+                vr[i] = vw;
+                *(u32x4*)(Kb + (long)t * D + 8 * dl) = kw;
+                *(u32x4*)(Vb + (long)t * D + 8 * dl) = vw;
+            }
+        }
+        // the scores stay in registers until every key's reduction is done (no store between
+        // them), so the 16 butterfly reductions of a wave overlap instead of running one by one
+        float sc[NIT][G];
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            float s[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) s[g] = 0.f;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const float k0 = bf_lo(kr[i][jj]), k1 = bf_hi(kr[i][jj]);
+#pragma unroll
+                for (int g = 0; g < G; ++g) s[g] += q[g][2 * jj] * k0 + q[g][2 * jj + 1] * k1;
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) sc[i][g] = xsum_v<LPK>(s[g]);   // xsum<LPK>'s adds, VALU exchanges
+        }
+        FS_TS(16);
+        if (dl == 0) {
+#pragma unroll
+            for (int i = 0; i < NIT; ++i)
+#pragma unroll
+                for (int g = 0; g < G; ++g) L.sm[g][i * KPB + gw * KPW + kg] = fast_score(sc[i][g], a.scale, a.softcap);
+        }
+    }
+    fb_lds_barrier();
+    FS_TS(3);
+    // softmax of the chunk: one aten block (one-block row) or the flash chunk statistics
+    if (gv && gw < G) {
+        const int g = gw;
+        const float s = lane < n ? L.sm[g][lane] : -INFINITY;
+        const float mx = wave_max(s);
+        if (single) {
+            const float p = lane < n ? sdpa_p(__fsub_rn(s, mx), lane, span) : 0.f;
+            L.pl[g][lane] = p;
+            if (lane < 16) L.pl[g][FS_CH + lane] = 0.f;
+            L.sm[g][lane] = rbf(p);
+            __builtin_amdgcn_wave_barrier();
+            const float l = sdpa_block_sum_lds<FS_CH>(L.pl[g], span, lane);
+            if (lane == 0) L.stat_l[g] = l;
+        } else {
+            const float p = lane < n ? __expf(s - mx) : 0.f;
+            L.sm[g][lane] = rbf(p);
+            const float l = xsum<64>(p);
+            if (lane == 0) {
+                L.cstat[g][0] = mx;
+                L.cstat[g][1] = l;
+            }
+        }
+    }
+    fb_lds_barrier();
+    if (gv) {
+        float o[G][8];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int jl = i * KPB + gw * KPW + kg;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float p = L.sm[g][jl];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    o[g][2 * jj] += p * bf_lo(vr[i][jj]);
+                    o[g][2 * jj + 1] += p * bf_hi(vr[i][jj]);
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) o[g][jj] += xlane32_v(o[g][jj]);   // LPK = 32: the kernel's one xor-32 step
+        if (kg == 0) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                L.ored[gw][g][dl][0] = (f32x4){o[g][0], o[g][1], o[g][2], o[g][3]};
+                L.ored[gw][g][dl][1] = (f32x4){o[g][4], o[g][5], o[g][6], o[g][7]};
+            }
+        }
+    }
+    fb_lds_barrier();
+    FS_TS(4);
+    if (gv && gt < G * LPK) {
+        const int g = gt / LPK, d8 = gt % LPK;
+        const f32x4 lo4 = L.ored[0][g][d8][0] + L.ored[1][g][d8][0] + L.ored[2][g][d8][0] + L.ored[3][g][d8][0];
+        const f32x4 hi4 = L.ored[0][g][d8][1] + L.ored[1][g][d8][1] + L.ored[2][g][d8][1] + L.ored[3][g][d8][1];
+        if (single) {   // the row's output
+            const float inv = __fdiv_rn(1.0f, L.stat_l[g]);
+            u32x4 w;
+            w[0] = pack2(__fmul_rn(lo4[0], inv), __fmul_rn(lo4[1], inv));
+            w[1] = pack2(__fmul_rn(lo4[2], inv), __fmul_rn(lo4[3], inv));
+            w[2] = pack2(__fmul_rn(hi4[0], inv), __fmul_rn(hi4[1], inv));
+            w[3] = pack2(__fmul_rn(hi4[2], inv), __fmul_rn(hi4[3], inv));
+            __builtin_amdgcn_raw_buffer_store_b128(w, ors, (m * a.q_dim + (kvh * G + g) * D + 8 * d8) * 2, 0, AUX_SC1);
+        } else {        // the chunk's partial
+            const int off = (int)(((((long)m * Hkv + kvh) * a.s_nsplit + sp) * G + g) * D + 8 * d8) * 4;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo4), prs, off, 0, AUX_SC1);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi4), prs, off + 16, 0, AUX_SC1);
+        }
+    }
+    if (gv && !single && gt < G) {
+        const u32x2_t st = {__float_as_uint(L.cstat[gt][0]), __float_as_uint(L.cstat[gt][1])};
+        __builtin_amdgcn_raw_buffer_store_b64(
+            st, srs, (int)(((((long)m * Hkv + kvh) * a.s_nsplit + sp) * G + gt) * 2) * 4, 0, AUX_SC1);
+    }
+    drain_vm();
+    fb_lds_barrier();
+    FS_TS(5);
+    unsigned* tk = a.fticket + (long)m * Hkv + kvh;
+    if (has_c && !single && gt == 0)
+        L.last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nch - 1);
+    fb_lds_barrier();
+    FS_TS(6);
+    // the group holding the last chunk of its (row, kv head) combines the chunk records
+    // (attn_flash_finish's combine on the group's 4 waves: waves 0..G-1 the chunk weights
+    // exp(m_c - M) and the sum, waves G.. the output quads, their first batch of partials
+    // requested before the weights are known); every group that completed a (row, kv head)
+    // then publishes it. The groups of a workgroup combine side by side.
+    const bool comb = has_c && !single && L.last != 0;
+    const bool pub = has_c && (single || comb);
+    {
+        constexpr int FB = FS_CMAX, NOUT = G * D / 4;
+        static_assert(FS_CMAX == 16, "attn_flash_finish's combine batch");
+        const long rec = ((long)m * Hkv + kvh) * a.s_nsplit;   // chunk records of this (row, kv head)
+        const int ot = gt - 64 * G;
+        const bool outer = comb && ot >= 0 && ot < NOUT;
+        const int og = outer ? ot / (D / 4) : 0, o4 = outer ? ot % (D / 4) : 0;
+        auto pload = [&](f32x4 (&pv)[FB], int cb) {
+#pragma unroll
+            for (int k = 0; k < FB; ++k) {
+                int off = cb + k < nch ? (int)((((rec + cb + k) * G + og) * D + 4 * o4) * 4) : (int)0x7ffffff0;
+                asm volatile("" : "+v"(off));
+                pv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, off, 0, AUX_SC1));
+            }
+        };
+        if (comb && gt == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        f32x4 pv[FB];
+        if (outer) pload(pv, 0);
+        if (comb && gw < G) {
+            constexpr int CPL = 1;   // nch <= 64: the flash kernel's lanes past nch add -inf / +0 only
+            static_assert(FS_CMAX <= 64, "one chunk record per lane");
+            const int g = gw;
+            float mc[CPL], lc[CPL];
+#pragma unroll
+            for (int i = 0; i < CPL; ++i) {
+                const int c = lane + 64 * i;
+                int off = c < nch ? (int)((((rec + c) * G + g) * 2) * 4) : (int)0x7ffffff0;
+                asm volatile("" : "+v"(off));
+                const u32x2_t st = __builtin_amdgcn_raw_buffer_load_b64(srs, off, 0, AUX_SC1);
+                mc[i] = c < nch ? __uint_as_float(st[0]) : -INFINITY;
+                lc[i] = c < nch ? __uint_as_float(st[1]) : 0.f;
+            }
+            float mm = mc[0];
+#pragma unroll
+            for (int i = 1; i < CPL; ++i) mm = fmaxf(mm, mc[i]);
+            const float Mx = wave_max(mm);
+            float wl = 0.f;
+#pragma unroll
+            for (int i = 0; i < CPL; ++i) {
+                const float w = lane + 64 * i < nch ? __expf(mc[i] - Mx) : 0.f;
+                L.wts[g][lane + 64 * i] = w;
+                wl += w * lc[i];
+            }
+            const float Ls = xsum<64>(wl);
+            if (lane == 0) L.lsum[g] = Ls;
+        }
+        fb_lds_barrier();
+        if (outer) {   // nch <= FB (fused_mlp_launch): one batch, attn_flash_finish's first
+            f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < FB; ++k) {
+                const float w = k < nch ? L.wts[og][k] : 0.f;
+                acc += w * pv[k];
+            }
+            const float inv = 1.0f / L.lsum[og];
+            const u32x2_t ow = {pack2(acc[0] * inv, acc[1] * inv), pack2(acc[2] * inv, acc[3] * inv)};
+            __builtin_amdgcn_raw_buffer_store_b64(ow, ors, (m * a.q_dim + (kvh * G + og) * D + 4 * o4) * 2, 0,
+                                                  AUX_SC1);
+        }
+    }
+    drain_vm();
+    fb_lds_barrier();
+    if (pub && gt == 0) __hip_atomic_fetch_add(cline(a.sync, L_S0 + kvh), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    FS_TS(7);
+}
+
+// SELF: with the self-attention stage S in front (a.self_attn; a separate instantiation, so the
+// launch without it carries none of S's code or registers)
+template <bool SELF>
 __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     f32x4* red = (f32x4*)smem;                                   // GEMV partial sums, <= 60 KB
@@ -578,6 +980,16 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     const bool attnwg = bu < M * a.Hq;
     const int am = bu / a.Hq, ah = bu - am * a.Hq;   // attention task (row, q head)
     bool ok = true;
+    // ---- S: the layer's self-attention on every workgroup (O1 waits for its heads)
+    if constexpr (SELF) {
+        FS_TS(0);
+        fb_self_attn(a, *(FbSelfLds*)smem);
+        if (FS_DBG_VAR == 4) {   // timing variant: the stage again, warm (points overwritten)
+            FS_TS(13);
+            fb_self_attn(a, *(FbSelfLds*)smem);
+        }
+        FS_TS(8);
+    }
 
     // ---- the attention workers request their row's cross K / V chunk and RoPE row
     // (attn_decode_kernel<256, 1, true>'s VFIRST loads, waves 0-3) right after O1
@@ -630,6 +1042,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
             }
             if (tq < d / 8) hrow[tq] = pack8f(hreg);
             fb_publish(cline(a.sync, L_N1), 1u);
+            if constexpr (SELF) FS_TS(12);
         }
         {
             if (wave == 0) ok &= fm_wait_split<8>(a.sync, L_O0, (unsigned)(4 * (nw / 4)), tmo, 4u);
@@ -664,13 +1077,17 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     const int nu_o = owork ? (a.NGo - jo + oper - 1) / oper : 0;
 
     // ---- O1: the self-attention o-projection, 4 k-slices of 16 k-steps over nw / 4 workers
-    // each (<= 3 units, 8 waves); its input is the previous launch's, so no wait
+    // each (<= 3 units, 8 waves); its input is the previous launch's (no wait), or stage S's:
+    // k-slice so is the q-head pair of kv head so, complete when its M rows have published
     if (a.Wo1 && owork) {
         bf16x8_s w1[3][2];
         fb_issue<8, 2, 3>(w1, a.Wo1, a.NGo, a.q_dim / 32, so * 16, 16, jo, oper, nu_o);
+        if (SELF && wave == FM_NW - 1) ok &= fm_wait_n<1>(a.sync, L_S0 + so, (unsigned)M, tmo, 17u);
+        if constexpr (SELF) FS_TS_BY(9, (FM_NW - 1) * 64);
         fb_finish<8, EPI_F32, 2, 3, 2>(w1, jo, oper, nu_o, so * 16, 16, a.att_self, a.q_dim, M * a.q_dim * 2, M,
                                        a.o1slab + (long)so * M * d, d, M * d * 4, d, red);
         fb_publish(cline(a.sync, L_P0 + (w & 7)), 1u);
+        if constexpr (SELF) FS_TS(10);
     }
     kv_prefetch();
 
@@ -686,6 +1103,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
             fb_issue<FM_NW, 3, 2>(wq, a.Wq, a.NGq, d / 32, sq * 36, 36, jq, qper, nu_q);
             if (wave == 0) ok &= fm_wait_n<1>(a.sync, L_N1, (unsigned)M, tmo, 1u);
             T5G_TS(1);
+            if constexpr (SELF) FS_TS(11);
             fb_finish<FM_NW, EPI_F32, 3, 2, 2>(wq, jq, qper, nu_q, sq * 36, 36, a.xn1, d, M * d * 2, M,
                                                a.qslab + (long)sq * M * a.q_dim, a.q_dim, M * a.q_dim * 4, a.q_dim,
                                                red);
@@ -930,6 +1348,16 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
             return -1;
         if (!a.dslab || !a.post3_w || !a.pre3_w) return -1;
         if (a.Wo1 && (!a.att_self || !a.o1slab)) return -1;
+        // stage S: 8 q heads over 4 kv heads of 256 (O1's 4 k-slices = the 4 head pairs), the
+        // flash kernel's chunk records (rows of <= s_nsplit x 64 keys, checked by the host)
+        if (a.self_attn &&
+            (!a.Wo1 || !a.qkv_in || !a.sk || !a.sv || !a.kv_len || !a.fpart || !a.fstat || !a.fticket || a.Hq != 8 ||
+             a.Hkv != 4 || a.D != FS_D || a.M > FS_MAXROWS || a.qkv_dim != a.q_dim + 2 * a.Hkv * a.D || a.s_cap < 1 ||
+             a.s_nsplit < 1 || a.s_nsplit > DEC_MAX_CHUNKS || a.s_nsplit > (a.s_cap + FS_CH - 1) / FS_CH ||
+             a.window < 0 || (long)a.M * a.Hkv * a.s_nsplit * FS_G * FS_D * 4 > 0x7fff0000L ||
+             a.M * a.Hkv * a.s_nsplit > FS_GRP * nb ||   // <= 3 chunks per workgroup
+             a.s_nsplit > FS_CMAX))                        // one combine batch
+            return -1;
         if (a.Wqkv && (!a.qkv_out || a.NGqkv * 16 != a.qkv_dim)) return -1;
         a.norm_b0 = nb - a.M;
         static_assert(FB_GU_KB == FM_NW * 6 && FB_GU_KB % 3 == 0 && FB_LDS <= FM_LDS_MAX, "gate/up LDS unit");
@@ -938,18 +1366,18 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
         // function attributes and the occupancy check are per device (an engine per GPU in
         // one process must not skip the second device's hipFuncSetAttribute)
         if (dev < 0 || dev >= 64) return -1;
-        static bool attr_b[64] = {};
-        if (!attr_b[dev]) {
-            (void)hipFuncSetAttribute((const void*)fused_block_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)FM_LDS_MAX);
+        const int sv = a.self_attn ? 1 : 0;
+        auto* fb = sv ? fused_block_kernel<true> : fused_block_kernel<false>;
+        static bool attr_b[64][2] = {};
+        if (!attr_b[dev][sv]) {
+            (void)hipFuncSetAttribute((const void*)fb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FM_LDS_MAX);
             int occ = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fused_block_kernel<true>, FM_NW * 64, shm) !=
-                    hipSuccess || occ < 1)
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fb, FM_NW * 64, shm) != hipSuccess || occ < 1)
                 return -1;
-            attr_b[dev] = true;
+            attr_b[dev][sv] = true;
         }
         if (!launch) return 0;
-        hipLaunchKernelGGL(fused_block_kernel<true>, dim3((unsigned)nb), dim3(FM_NW * 64), shm, st, a);
+        hipLaunchKernelGGL(fb, dim3((unsigned)nb), dim3(FM_NW * 64), shm, st, a);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     const size_t shm = (size_t)5 * MT * FM_NW * 64 * 16;

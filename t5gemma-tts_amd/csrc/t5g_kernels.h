@@ -106,17 +106,32 @@ struct FusedMlpArgs {
     float* qkv_out;           // [2][M][qkv_dim]
     // ---- the self-attention o-projection in front (Wo1 non-null): O1 = att_self . Wo1^T as
     //   fp32 slabs [4][M][d] in o1slab (in-launch), the N1 norm's input instead of o_slabs
-    const bf16_t* att_self;   // [M][q_dim] self-attention output (previous launch)
+    const bf16_t* att_self;   // [M][q_dim] self-attention output (previous launch, or stage S)
     const bf16_t* Wo1;        // packed self o_proj, NGo row groups, K = q_dim
     float* o1slab;
+    // ---- the layer's decode self-attention in front of O1 (self_attn = 1, needs Wo1): stage
+    //   S = attn.hip attn_decode_kernel<256, 2, true, true>'s arithmetic (q / new-key PM-RoPE
+    //   from the q|k|v slabs, the key and value appended to the cache, flash-form 64-key chunk
+    //   partials, the last chunk of a (row, kv head) combining), writing att_self in-launch
+    int self_attn;
+    const float* qkv_in;      // [2][M][qkv_dim] this layer's q|k|v slabs (previous launch)
+    bf16_t* sk;               // self K / V cache of the layer [B][Hkv][s_cap][D]
+    bf16_t* sv;
+    int s_cap;                // cache capacity (keys)
+    int s_nsplit;             // 64-key chunk records per (row, kv head) in fpart / fstat
+    const int* kv_len;        // [B] keys of each row, the appended one included
+    int window;               // sliding window (0: none)
+    float* fpart;             // [M][Hkv][s_nsplit][G][D] chunk partials
+    float* fstat;             // [M][Hkv][s_nsplit][G][2] chunk max / sum
+    unsigned* fticket;        // [M][Hkv] arrival tickets (zero between launches)
 };
 int fused_mlp(const FusedMlpArgs& a, hipStream_t st);
 int fused_mlp_check(const FusedMlpArgs& a);   // 0: fused_mlp would launch these args; -1: not built for them
 // counter words of one fused launch, each on its own 128-byte line (arrivals on one line
 // serialise at ~12 ns each): N1, 8 cross-q heads, 8 attention heads, 8 cross-o groups,
-// N2, 8 down slices, 8 down groups, N3, 8 o-projection groups. The engine keeps one set per
-// decoder layer after one line for the timeout word.
-constexpr int FM_LINE = 32, FM_SET_LINES = 51, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
+// N2, 8 down slices, 8 down groups, N3, 8 o-projection groups, 8 self-attention kv heads.
+// The engine keeps one set per decoder layer after one line for the timeout word.
+constexpr int FM_LINE = 32, FM_SET_LINES = 59, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
 
 // parity mode's decode layer after the self attention as one persistent launch (xlayer.hip):
 // O1 self o-proj, N1, cross q, PM cross attention, cross o, N2, gate/up + GeGLU, down in the

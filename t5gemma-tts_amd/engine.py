@@ -233,6 +233,21 @@ class T5GemmaTTSEngine:
         _lib.check(self.L.t5g_engine_xlayer_launches(self.h, C.byref(n)), "xlayer_launches")
         return n.value
 
+    def set_attn_in_block(self, enable: bool) -> None:
+        """Fast-path decode self attention as the first stage of the persistent layer launch
+        (default; csrc/fused.hip stage S: no attention launch between the layers) or as its
+        own flash launch; bitwise equal. Needs the flash form and the persistent launch
+        (set_attn_flash, set_fused); rows x kv heads x ceil(chunks / 3) above the CU count
+        keep the separate launch."""
+        _lib.check(self.L.t5g_engine_set_attn_in_block(self.h, 1 if enable else 0), "set_attn_in_block")
+
+    def attn_in_block_launches(self) -> int:
+        """Fast-path persistent layer launches issued with the self attention inside (test /
+        bench hook; a launch captured into a graph counts once)."""
+        n = C.c_int64()
+        _lib.check(self.L.t5g_engine_attn_in_block_launches(self.h, C.byref(n)), "attn_in_block_launches")
+        return n.value
+
     def set_attn_flash(self, enable: bool) -> None:
         """Fast-path decode self attention as one split-key launch with an online-softmax
         combine (default) or as the two-launch aten-order form (scores, then P.V / combine);

@@ -1,0 +1,127 @@
+"""The fast path's decode self attention as stage S of the persistent layer launch
+(csrc/fused.hip fb_self_attn: the flash launch's arithmetic, one 64-key chunk per 4-wave
+group spread over every workgroup, the holder of a (row, kv head)'s last chunk combining, att_self handed to the o-projection
+in-launch) against the same step with the attention as its own flash launch
+(attn.hip attn_decode_kernel<256, 2, true, true>): tokens and every logit row bitwise equal,
+at the true 2b-2b widths (2 + 2 layers), for 1-16 rows with rows of one chunk (the aten-order
+single-block path), of several chunks and of partial chunk triples; on a sliding-window layer
+past its window; and a call whose rows need more tasks than workgroups keeps the separate
+launch (same bits). Reference: [tf] modeling_t5gemma.py:264-304 (self attention in
+PMDecoderLayer, hf_export/modeling_t5gemma_voice.py:256-323)."""
+import dataclasses
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN  # noqa: F401  (sys.path set-up)
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+
+
+def _engine(max_batch, max_audio, window=None):
+    import json
+    import os
+    from conftest import GOLDEN as G
+    from t5gemma_tts_amd.config import named_config
+    from t5gemma_tts_amd.engine import T5GemmaTTSEngine
+    from t5gemma_tts_amd.weights import synthetic_weights
+    meta = json.load(open(os.path.join(G, "golden_mid.json")))
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    if window is not None:
+        cfg = dataclasses.replace(cfg, backbone=dataclasses.replace(cfg.backbone, sliding_window=window))
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=max_batch, max_text=64, max_audio=max_audio,
+                           max_gen=40)
+    return cfg, eng
+
+
+def _utts(cfg, n, seed, tp_max):
+    from t5gemma_tts_amd.engine import Utterance
+    rng = np.random.default_rng(seed)
+    utts = []
+    for i in range(n):
+        x = rng.integers(3, 4000, size=int(rng.integers(4, 40))).tolist()
+        tp = 0 if i == 0 else int(rng.integers(0, tp_max))   # row 0: one-chunk rows throughout
+        y = rng.integers(0, 65536, size=tp).tolist() + ([cfg.y_sep_token] if tp else [])
+        utts.append(Utterance(x=x, y=y, tgt_y_len=len(y) + int(rng.integers(8, 30))))
+    return utts
+
+
+def _run(eng, utts, p, seeds, on):
+    eng.set_attn_in_block(on)
+    before = eng.attn_in_block_launches()
+    # host loop (every step's logits) and the graph-replayed on-device loop (tokens)
+    out = eng.generate(utts, p, seeds=seeds, parity=True, exact=False, record_logits=True)
+    fast = eng.generate(utts, p, seeds=seeds)
+    return out, fast, eng.attn_in_block_launches() - before
+
+
+def _assert_same(a, b, B, tag):
+    for r in range(B):
+        assert a["gen"][r].tolist() == b["gen"][r].tolist(), (tag, r)
+    if "logits" not in a:   # the graph-replayed loop: tokens only
+        return
+    assert len(a["logits"]) == len(b["logits"]), tag
+    for s, (la, lb) in enumerate(zip(a["logits"], b["logits"])):
+        assert torch.equal(la.view(torch.int16), lb.view(torch.int16)), (tag, s)
+
+
+@pytest.mark.parametrize("B,tp_max", [(1, 1), (3, 300), (8, 400), (16, 300)])
+def test_attention_in_block_bitwise_equal_to_flash_launch(B, tp_max):
+    _need_gpu()
+    from t5gemma_tts_amd.engine import SamplingParams
+    cfg, eng = _engine(16, 448)
+    utts = _utts(cfg, B, 60 + B, tp_max)
+    p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
+    seeds = list(range(900, 900 + B))
+    on0, fon0, n_on0 = _run(eng, utts, p, seeds, True)
+    off, foff, n_off = _run(eng, utts, p, seeds, False)
+    on1, fon1, n_on1 = _run(eng, utts, p, seeds, True)
+    assert n_off == 0 and n_on0 > 0 and n_on1 > 0   # stage S ran, and only when enabled
+    _assert_same(on0, off, B, "on/off")
+    _assert_same(on0, on1, B, "on/on")
+    _assert_same(fon0, foff, B, "graph on/off")
+    _assert_same(fon0, fon1, B, "graph on/on")
+    assert sum(len(g) for g in on0["gen"]) > B
+
+
+def test_attention_in_block_sliding_window():
+    """Layer 0 slides over a 100-key window: rows past it start their chunks at t - 99."""
+    _need_gpu()
+    from t5gemma_tts_amd.engine import SamplingParams
+    cfg, eng = _engine(8, 448, window=100)
+    utts = _utts(cfg, 6, 17, 350)
+    p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
+    seeds = list(range(6))
+    on, fon, n_on = _run(eng, utts, p, seeds, True)
+    off, foff, _ = _run(eng, utts, p, seeds, False)
+    assert n_on > 0
+    _assert_same(on, off, 6, "window")
+    _assert_same(fon, foff, 6, "window graph")
+
+
+def test_attention_in_block_falls_back_past_one_task_per_workgroup():
+    """16 rows of up to ~1 100 keys: 16 x 4 kv heads x 18 chunks = 1 152 chunks > 3 per
+    workgroup (and rows past the 1 024 keys one combine batch reads), so the call keeps the
+    separate flash launch -- the same bits either way."""
+    _need_gpu()
+    from t5gemma_tts_amd.engine import SamplingParams
+    cfg, eng = _engine(16, 1152)
+    from t5gemma_tts_amd.engine import Utterance
+    rng = np.random.default_rng(3)
+    utts = [Utterance(x=rng.integers(3, 4000, size=20).tolist(),
+                      y=rng.integers(0, 65536, size=1080).tolist() + [cfg.y_sep_token], tgt_y_len=1081 + 10)
+            for _ in range(16)]
+    p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
+    seeds = list(range(16))
+    on, fon, n_on = _run(eng, utts, p, seeds, True)
+    off, foff, _ = _run(eng, utts, p, seeds, False)
+    assert n_on == 0
+    _assert_same(on, off, 16, "fallback")
+    _assert_same(fon, foff, 16, "fallback graph")

@@ -15,6 +15,7 @@ from t5gemma_tts_amd import _lib  # noqa: E402
 
 
 def main():
+    self_stage = "--self" in sys.argv   # the launch with the self attention inside (stage S)
     from t5gemma_tts_amd.config import config_2b2b
     from t5gemma_tts_amd.engine import T5GemmaTTSEngine
     from t5gemma_tts_amd.weights import synthetic_weights
@@ -22,7 +23,14 @@ def main():
     cfg = config_2b2b()
     B = 8
     sd = synthetic_weights(cfg, seed=1234, device="cuda:0")
-    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=B, max_text=64, max_audio=256, max_gen=64)
+    # --self: caches filled to the C3 mean length (~527 keys), the generate on the launches
+    # without S (another kernel instantiation), so the PMC rows of fused_block_kernel<true> are
+    # the timed launches only
+    n_gen = 376 if self_stage else 8
+    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=B, max_text=64, max_audio=160 + n_gen + 64,
+                           max_gen=n_gen + 16)
+    if self_stage:
+        eng.set_attn_in_block(False)
     del sd
     # one short C3-shaped generate (T_x 60) so the engine's rows, text lengths and cross K / V
     # are those of the bench workload
@@ -30,14 +38,24 @@ def main():
     import numpy as np
     rng = np.random.default_rng(0)
     utts = [Utterance(x=rng.integers(3, 4000, size=60).tolist(),
-                      y=rng.integers(0, 65536, size=150).tolist() + [cfg.y_sep_token], tgt_y_len=151 + 8)
+                      y=rng.integers(0, 65536, size=150).tolist() + [cfg.y_sep_token], tgt_y_len=151 + n_gen)
             for _ in range(B)]
     eng.generate(utts, SamplingParams(top_k=30, top_p=0.9, temperature=0.8), seeds=list(range(B)))
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     us = C.c_float()
-    _lib.check(L.t5g_time_decode_mlp(eng.h, B, 52, st, C.byref(us)), "time_decode_mlp")
-    alg = _lib.fused_block_bytes(B, 60)
+    if self_stage:
+        eng.set_attn_in_block(True)
+        keys = C.c_float()
+        _lib.check(L.t5g_time_decode_layer(eng.h, B, 52, st, C.byref(us), C.byref(keys)), "time_decode_layer")
+        alg = _lib.fused_block_bytes(B, 60, self_keys=keys.value)
+        print(f"keys per kv head (rows summed, layer mean) {keys.value:.1f}", flush=True)
+    else:
+        _lib.check(L.t5g_time_decode_mlp(eng.h, B, 52, st, C.byref(us)), "time_decode_mlp")
+        alg = _lib.fused_block_bytes(B, 60)
     print(f"fused_block avg {us.value:.2f} us/launch, algorithmic {alg} B -> {alg / us.value / 1e3:.1f} GB/s", flush=True)
+    if len(sys.argv) > 2 and self_stage:
+        import json
+        json.dump({"algorithmic": alg, "keys": keys.value, "avg_us": us.value}, open(sys.argv[-1], "w"))
 
 
 if __name__ == "__main__":

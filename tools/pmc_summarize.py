@@ -29,6 +29,14 @@ OPS = {
                             "T_x=60, 2b-2b widths (tools/pmc_fused.py: 26 layers rotated, 4.3 GB > 256 MiB Infinity "
                             "Cache); algorithmic = weights + cross K/V + o slabs, h, norm weights, RoPE rows in + h, "
                             "q|k|v slabs out"},
+    "fused_block_s": {"kernels": ["fused_block_kernel<true>"],
+                      "algorithmic": None,   # tools/pmc_fused.py --self writes it (keys of the run)
+                      "what": "fast-path persistent decode layer WITH the self attention (stage S: flash chunks "
+                              "over the cached K / V + append -> o-proj -> norm -> cross-q -> PM cross attention -> "
+                              "cross-o -> norm -> gate/up GeGLU -> down -> norm -> next q|k|v), M=8, T_x=60, L ~ 527, "
+                              "2b-2b widths (tools/pmc_fused.py --self: 26 layers rotated); algorithmic = weights + "
+                              "self K/V read + appended K/V + q|k|v slabs + cross K/V + h, norm weights, RoPE rows in "
+                              "+ h, q|k|v slabs out"},
     "xlayer": {"kernels": ["xlayer_kernel"],
                "algorithmic": None,   # _lib.xlayer_bytes(8, bb, 60, 26): the average over a step's 26 layers
                "what": "parity mode's persistent decode layer after the self attention (o-proj -> norm -> cross-q "
@@ -69,6 +77,8 @@ def main(op, out_dir, dst):
         from t5gemma_tts_amd.config import config_2b2b
         bb = config_2b2b().backbone
         alg = xlayer_bytes(8, bb, 60, bb.num_decoder_layers)
+    elif alg is None and op == "fused_block_s":
+        alg = json.load(open(os.path.join(out_dir, "alg.json")))["algorithmic"]
     elif alg is None and op == "fused_block":
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         import t5gemma_tts_amd  # noqa: F401
