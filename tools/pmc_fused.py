@@ -23,10 +23,10 @@ def main():
     cfg = config_2b2b()
     B = 8
     sd = synthetic_weights(cfg, seed=1234, device="cuda:0")
-    # --self: caches filled to the C3 mean length (~527 keys), the generate on the launches
-    # without S (another kernel instantiation), so the PMC rows of fused_block_kernel<true> are
-    # the timed launches only
-    n_gen = 376 if self_stage else 8
+    # --self: caches filled to the C3 bench rows' final length (903 keys: the length bench.py's
+    # roofline leg times the launch at), the generate on the launches without S (another kernel
+    # instantiation), so the PMC rows of fused_block_kernel<true> are the timed launches only
+    n_gen = 751 if self_stage else 8
     eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=B, max_text=64, max_audio=160 + n_gen + 64,
                            max_gen=n_gen + 16)
     if self_stage:
