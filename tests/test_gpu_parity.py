@@ -226,6 +226,11 @@ def _oparams(c):
 # now flip at a sampling boundary -- each flip explained and asserted below (sampler on the
 # GPU's logits picks the GPU's token, on the reference's the reference's, logits within 2 %)
 MIN_EXACT = {"golden_tiny": 12, "golden_tiny_eager": 2, "golden_tiny_window": 4}
+# teacher-forced max |logit error| / max |logit| allowed per golden: 2 %, and for
+# the eager case -- where the token-flip count above was relaxed -- a bound just above its
+# measured 1.36 % (round 4-5), so a further drift of the fast kernels' softcap path fails here
+# rather than only through token flips
+TF_RTOL = {"golden_tiny": 0.02, "golden_tiny_eager": 0.016, "golden_tiny_window": 0.02}
 
 
 def _topk_agree(g, r, k, tol):
@@ -292,7 +297,7 @@ def test_tiny_engine_vs_reference_golden(name):
         # kernels (parity mode restates eager attention for the 2b-2b call shape only)
         out = eng.generate([u], _params(c), seeds=[c["seed"]], parity=True, record_logits=True,
                            exact=False if name == "golden_tiny_eager" else None)
-        w, ex = teacher_forced_check(cfg, sd, u, _oparams(c), c["seed"], out, rtol=0.02)
+        w, ex = teacher_forced_check(cfg, sd, u, _oparams(c), c["seed"], out, rtol=TF_RTOL[name])
         worst = max(worst, w)
         rows_exact += ex
         rows += len(out["gen"][0])

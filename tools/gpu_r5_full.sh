@@ -1,0 +1,9 @@
+# Round 5 closing checks: the whole GPU suite, then smoke
+mkdir -p gpurun_out
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider \
+  > gpurun_out/r5_full_gpu_tests.log 2>&1
+rc=$?; echo "gpu suite rc=$rc" >> gpurun_out/r5_full_gpu_tests.log
+tail -3 gpurun_out/r5_full_gpu_tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r5_full_smoke.log 2>&1
+rc=$?; tail -2 gpurun_out/r5_full_smoke.log; exit $rc
