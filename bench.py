@@ -149,8 +149,11 @@ def main():
     ap.add_argument("--no-attn-flash", action="store_true",
                     help="fast path: decode self attention as the two-launch aten-order form (A/B)")
     ap.add_argument("--no-attn-in-block", action="store_true",
-                    help="fast path: decode self attention as its own launch instead of the persistent layer "
-                         "launch's first stage (A/B)")
+                    help="fast path: decode self attention as its own launch instead of inside the persistent "
+                         "layer launch (A/B)")
+    ap.add_argument("--attn-in-block", type=int, choices=(1, 2), default=None,
+                    help="fast path: stage S in front of the layer's o-projection (1) or at the end of the "
+                         "previous layer's launch (2, the engine default)")
     ap.add_argument("--attn", choices=("sdpa", "eager"), default="sdpa",
                     help="the checkpoint's attn_implementation: eager (the reference default, tanh softcap 50) "
                          "runs parity mode's eager.hip restatement")
@@ -208,6 +211,8 @@ def main():
         eng.set_attn_flash(False)
     if args.no_attn_in_block:
         eng.set_attn_in_block(False)
+    elif args.attn_in_block:
+        eng.set_attn_in_block(args.attn_in_block)
     codec = None
     if args.e2e:
         from t5gemma_tts_amd.codec import XCodec2Decoder, codec_44k, synthetic_codec_weights

@@ -304,16 +304,19 @@ int t5g_attention_decode_flash(const t5g_attn_decode_args* args, void* stream);
  * T5GemmaSelfAttention :264-304; no reference-side equivalent switch. */
 int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable);
 
-/* Fast-path decode self attention as stage S of the persistent layer launch (default 1; needs
- * the flash form and t5g_engine_set_fused): the flash launch's arithmetic on the launch's
- * workgroups (three 64-key chunks each), the q|k|v slabs of the previous launch in, att_self
- * handed to the o-projection stage in-launch -- no attention launch between the layers,
- * bitwise equal to the flash launch followed by the launch without S. Calls whose rows x kv
- * heads x ceil(chunks / 3) exceed the CU count keep the separate launch. Replaces the
- * reference's per-layer self-attention call inside PMDecoderLayer
+/* Fast-path decode self attention inside the persistent layer launch (needs the flash form and
+ * t5g_engine_set_fused). mode 0: its own flash launch between the layers; 1: stage S in front of
+ * the launch's o-projection (the flash launch's arithmetic on the launch's workgroups, three
+ * 64-key chunks each, att_self handed to the o-projection in-launch); 2 (default): stage S at
+ * the END of the previous layer's launch -- after its q|k|v stage, with the K / V requested
+ * before the N3 wait -- followed by that layer's o-projection, whose slabs the next launch's
+ * norm reads (layer 0's attention and o-projection stay the step's own launches). Every mode
+ * is bitwise equal to mode 0. Calls whose rows x kv heads x chunks exceed 3 (mode 1) / 2
+ * (mode 2) chunk slots per workgroup, or rows past 1 024 keys, keep the separate launch.
+ * Replaces the reference's per-layer self-attention call inside PMDecoderLayer
  * (hf_export/modeling_t5gemma_voice.py:256-323, [tf] modeling_t5gemma.py:264-304).
  * t5g_engine_attn_in_block_launches: layer launches issued with S (captured ones once). */
-int t5g_engine_set_attn_in_block(t5g_engine* e, int32_t enable);
+int t5g_engine_set_attn_in_block(t5g_engine* e, int32_t mode);
 int t5g_engine_attn_in_block_launches(t5g_engine* e, int64_t* n);
 
 /* Sampler launch shape: 0 (default) the 16-slice multi-block kernel, falling back per row to

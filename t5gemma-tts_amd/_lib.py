@@ -249,9 +249,10 @@ FUSED_MLP_KERNEL = ("fused_mlp_kernel<1> (decode MLP half in one launch: cross-a
 FUSED_BLOCK_KERNEL = ("fused_block_kernel (decode layer after the self attention in one launch: "
                       "o-proj -> norm -> cross-q -> PM cross attention -> cross-o -> norm -> gate/up GeGLU -> down -> "
                       "norm -> next layer's q|k|v, 174.6 MB of weights)")
-FUSED_BLOCK_S_KERNEL = ("fused_block_kernel with stage S (decode layer in one launch: flash self attention "
-                        "over the cached K / V + append -> o-proj -> norm -> cross-q -> PM cross attention -> cross-o "
-                        "-> norm -> gate/up GeGLU -> down -> norm -> next layer's q|k|v, 174.6 MB of weights)")
+FUSED_BLOCK_S_KERNEL = ("fused_block_kernel<2> (decode layer in one launch with the next layer's self attention "
+                        "at its end: norm -> cross-q -> PM cross attention -> cross-o -> norm -> gate/up GeGLU -> "
+                        "down -> norm -> next q|k|v -> next layer's flash self attention over its cached K / V + "
+                        "append -> next o-proj, 174.6 MB of weights)")
 T5G_EUNSUPPORTED = -3
 
 

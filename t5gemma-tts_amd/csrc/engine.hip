@@ -91,7 +91,7 @@ struct t5g_engine {
     bool attn_flash = true;
     // the flash decode self-attention as stage S of the persistent layer launch (fast path,
     // t5g_engine_set_attn_in_block): no attention launch of its own between the layers
-    bool attn_in_block = true;
+    int attn_in_block = 2;   // 0 own launch, 1 stage S in front of O1, 2 at the end of the previous launch
     int64_t s_launches = 0;   // persistent layer launches run with stage S (tests)
     float* afpart = nullptr;    // [B][Hkv][nsplit][G][D]
     float* afstat = nullptr;    // [B][Hkv][nsplit][G][2]
@@ -1155,9 +1155,42 @@ static FusedMlpArgs fused_block_args(t5g_engine* e, int M, int l) {
 // stage S in front (fast path): the layer's flash decode self-attention inside the launch,
 // with decode_attention's arguments (the cache, the call's chunk grid, the q|k|v slabs);
 // false when the launch is not built for them (the attention then runs as its own launch)
+static void fused_s_fields(t5g_engine* e, int l, FusedMlpArgs& fa) {
+    const t5g_config& c = e->c;
+    fa.qkv_in = e->part;
+    fa.sk = e->sk[l];
+    fa.sv = e->sv[l];
+    fa.s_cap = c.max_audio;
+    fa.s_nsplit = (c.max_audio + 63) / 64;
+    if (e->audio_max > 0 && e->audio_max < c.max_audio) fa.s_nsplit = (e->audio_max + 63) / 64;
+    fa.kv_len = e->kv_len;
+    fa.window = c.dec_sliding[l] ? c.sliding_window : 0;
+    fa.fpart = e->afpart;
+    fa.fstat = e->afstat;
+    fa.fticket = e->aftick;
+}
+
+// stage S at the end (fast path, attn_in_block 2): launch l projects layer l + 1's q|k|v,
+// runs its self attention and its o-projection into the o1slab region, which the next
+// launch's N1 reads as o_slabs (layer 0's come from the step's prologue in e->part);
+// false when the launch is not built for them
+static bool fused_block_tail(t5g_engine* e, int M, int l, FusedMlpArgs& fa) {
+    const t5g_config& c = e->c;
+    fa.Wo1 = nullptr;   // the o-projection of this layer ran at the end of the previous launch
+    fa.o_slabs = l == 0 ? e->part : fa.o1slab;
+    if (l == c.n_dec_layers - 1) return fused_mlp_check(fa) == 0;
+    fused_s_fields(e, l + 1, fa);
+    fa.self_tail = 1;
+    fa.Wo1n = (const bf16_t*)e->dec[l + 1].o;
+    fa.o1n = fa.o1slab;
+    fa.att_self = e->datt;
+    (void)M;
+    return fused_mlp_check(fa) == 0;
+}
+
 static bool fused_block_self(t5g_engine* e, int M, int l, FusedMlpArgs& fa) {
     const t5g_config& c = e->c;
-    if (!e->attn_in_block || !e->attn_flash || !fa.Wo1) return false;
+    if (e->attn_in_block != 1 || !e->attn_flash || !fa.Wo1) return false;
     fa.self_attn = 1;
     fa.qkv_in = e->part;
     fa.sk = e->sk[l];
@@ -1247,6 +1280,16 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
         return r;
     };
     bool qkv_done = false;   // the previous layer's fused block projected this layer's q|k|v
+    // stage S at the end of the launches (attn_in_block 2): every layer's launch must take it
+    bool tail = false;
+    if (decode && e->attn_in_block == 2 && e->attn_flash && e->fused_mlp && M <= 16 && d == 2304 && f == 9216 &&
+        s_o == 4 && s_down == 8 && s_qkv == 2 && e->q_dim == 2048 && c.n_dec_layers >= 2) {
+        tail = true;
+        for (int l = 0; l < c.n_dec_layers && tail; ++l) {
+            FusedMlpArgs fa = fused_block_args(e, M, l);
+            tail = fused_block_tail(e, M, l, fa);
+        }
+    }
     for (int l = 0; l < c.n_dec_layers; ++l) {
         const t5g_layer_weights& L = e->dec[l];
         if (l == 0) {
@@ -1286,6 +1329,22 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
                 if (rcq != 0) RC(gemm(xn, d, M, L.qkv, e->qkv_dim, d, s_qkv, nullptr, e->part, e->qkv_dim, EPI_F32, st));
             }
             qkv_done = false;
+            if (tail) {
+                // layer 0's attention and o-projection as their own launches (the step's
+                // prologue), then every layer's launch runs the next layer's attention and
+                // o-projection at its end (bitwise equal to the launches below)
+                if (l == 0) {
+                    RC(decode_attention(e, M, e->sk[l], e->sv[l], c.max_audio, e->kv_len, 1, win, 0, true, pos, tab,
+                                        s_qkv, e->qkv_dim, st));
+                    RC(out_proj(att, L.o));
+                }
+                FusedMlpArgs fa = fused_block_args(e, M, l);
+                if (!fused_block_tail(e, M, l, fa)) return T5G_EUNSUPPORTED;   // checked for every layer above
+                RC(fused_mlp(fa, st));
+                if (l != c.n_dec_layers - 1) ++e->s_launches;
+                qkv_done = true;
+                continue;
+            }
             // the persistent layer launch with the attention as its stage S (bitwise equal to
             // the flash launch below followed by the same launch without S)
             if (e->fused_mlp && M <= 16 && d == 2304 && f == 9216 && s_o == 4 && s_down == 8 && s_qkv == 2 &&
@@ -1674,10 +1733,10 @@ extern "C" int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable) {
     return T5G_OK;
 }
 
-extern "C" int t5g_engine_set_attn_in_block(t5g_engine* e, int32_t enable) {
-    if (!e) return T5G_EINVAL;
-    if (e->attn_in_block != (enable != 0)) {
-        e->attn_in_block = enable != 0;
+extern "C" int t5g_engine_set_attn_in_block(t5g_engine* e, int32_t mode) {
+    if (!e || mode < 0 || mode > 2) return T5G_EINVAL;
+    if (e->attn_in_block != mode) {
+        e->attn_in_block = mode;
         drop_graphs(e);   // captured launches follow the flag
     }
     return T5G_OK;
@@ -2013,17 +2072,22 @@ extern "C" int t5g_time_decode_layer(t5g_engine* e, int32_t B, int32_t iters, vo
     hipStream_t st = (hipStream_t)stream;
     const t5g_config& c = e->c;
     const int L = c.n_dec_layers;
+    // attn_in_block 1: launch l runs layer l's attention in front; 2: layer l + 1's at its end
+    // (the last launch none; layer 0's is the step's own launch, not timed here)
+    const bool tail = e->attn_in_block == 2;
     auto args = [&](int l, FusedMlpArgs& fa) {
         fa = fused_block_args(e, B, l);
+        if (tail) return fused_block_tail(e, B, l, fa);
         return fused_mlp_check(fa) == 0 && fused_block_self(e, B, l, fa);
     };
     FusedMlpArgs fa;
-    if (!args(0, fa)) return T5G_EUNSUPPORTED;
+    for (int l = 0; l < L; ++l)
+        if (!args(l, fa)) return T5G_EUNSUPPORTED;
     std::vector<int> len(B);
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipMemcpy(len.data(), e->kv_len, sizeof(int) * B, hipMemcpyDeviceToHost));
     double ksum = 0.0;
-    for (int l = 0; l < L; ++l)
+    for (int l = tail ? 1 : 0; l < L; ++l)
         for (int b = 0; b < B; ++b) {
             const int w = c.dec_sliding[l] ? c.sliding_window : 0;
             ksum += w > 0 ? std::min(len[b], w) : len[b];

@@ -43,8 +43,8 @@ constexpr unsigned FM_SPIN_MAX = 1u << 18;   // ~0.3-0.5 s of polling before a w
 
 // lines of a counter set (FusedMlpArgs::sync), one word per 128-byte line
 constexpr int L_N1 = 0, L_Q0 = 1, L_A0 = 9, L_O0 = 17, L_N2 = 25, L_SL0 = 26, L_D0 = 34, L_N3 = 42, L_P0 = 43,
-              L_S0 = 51;
-static_assert(L_S0 + 8 == FM_SET_LINES, "counter set layout");
+              L_S0 = 51, L_K0 = 59;
+static_assert(L_K0 + 8 == FM_SET_LINES, "counter set layout");
 __device__ __forceinline__ unsigned* cline(unsigned* set, int line) { return set + line * FM_LINE; }
 constexpr int FS_NORM = L_N2 * FM_LINE;
 __device__ __forceinline__ int fs_slice(int s) { return (L_SL0 + s) * FM_LINE; }
@@ -621,7 +621,13 @@ extern "C" int t5g_dbg_set_fused_s_var(int v) {
 // barrier that waits for this wave's LDS traffic only (no vmcnt: loads stay in flight)
 __device__ __forceinline__ void fb_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& sl) {
+// TAIL (a.self_tail): the stage runs at the END of the previous layer's launch for this
+// layer -- the K / V requests go out before `mid` (the N3 wait, the q|k|v stage and its
+// hand-off, run by the caller), the q|k|v slabs are read (sc1) after it; slots live on the
+// first `nwg` workgroups' groups 0-1 only (group 2's waves poll), and `len_in` is the row
+// length the caller requested at launch start. Front: `mid` is empty, len_in < 0.
+template <bool TAIL, typename Mid>
+__device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& sl, Mid&& mid, int nwg, int len_in) {
     constexpr int G = FS_G, D = FS_D, LPK = FS_LPK, KPW = FS_KPW, KPB = FS_KPB, NIT = FS_NIT;
     const int tq = (int)threadIdx.x, wave = tq >> 6, lane = tq & 63;
     const int grp = wave >> 2, gw = wave & 3, gt = tq & 255;
@@ -633,12 +639,12 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
     // slabs and the RoPE row are requested with the row length; chunk-major, so the live
     // chunks (sp < the row's count) fill group 0 of every workgroup before any group 1
     // (fused_mlp_launch: slots <= 3 nb)
-    const int cidx = (int)blockIdx.x + grp * (int)gridDim.x;
-    const bool has_s = cidx < M * Hkv * a.s_nsplit;
+    const int cidx = (int)blockIdx.x + grp * nwg;
+    const bool has_s = (int)blockIdx.x < nwg && cidx < M * Hkv * a.s_nsplit;
     const int sp = has_s ? cidx / (M * Hkv) : 0, rk = has_s ? cidx - sp * (M * Hkv) : 0;
     const int m = rk / Hkv, kvh = rk - m * Hkv;
     const int dvar = FS_DBG_VAR;
-    const int len = a.kv_len[m];
+    const int len = TAIL ? len_in : a.kv_len[m];
     int role = 0, c4 = 0, g_own = 0, col;
     if (gt < G * D / 4) {
         g_own = gt / (D / 4);
@@ -652,9 +658,13 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
     }
     const long uo = dvar == 2 ? 0 : col;
     // unconditional (slots past the grid read row 0's): a load under a branch makes the
-    // compiler wait for everything in flight at the join, the row length included
-    const f32x4 u0 = *(const f32x4*)(a.qkv_in + (long)m * a.qkv_dim + uo);
-    const f32x4 u1 = *(const f32x4*)(a.qkv_in + ((long)M + m) * a.qkv_dim + uo);
+    // compiler wait for everything in flight at the join, the row length included. In the
+    // tail the slabs are this launch's (after `mid`).
+    f32x4 u0, u1;
+    if constexpr (!TAIL) {
+        u0 = *(const f32x4*)(a.qkv_in + (long)m * a.qkv_dim + uo);
+        u1 = *(const f32x4*)(a.qkv_in + ((long)M + m) * a.qkv_dim + uo);
+    }
     const float* tr = a.rope_tab + (long)m * D + (8 * dl) % (D / 2);
     f32x4 ca = *(const f32x4*)tr, cb = *(const f32x4*)(tr + 4);
     f32x4 sa = *(const f32x4*)(tr + D / 2), sb = *(const f32x4*)(tr + D / 2 + 4);
@@ -671,7 +681,7 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
     const int c0 = lo + sp * FS_CH, c1 = min(hi, c0 + FS_CH), n = c1 - c0;
     const bool gv = has_c && n > 0;
     const bool has_t = gv && t >= c0 && t < c1;
-    if (gt == 0) L.last = 0;
+    if (!TAIL && gt == 0) L.last = 0;
     const __amdgpu_buffer_rsrc_t ors = raw_rsrc(a.att_self, (uint32_t)(M * a.q_dim * 2));
     const long nrec = (long)M * Hkv * a.s_nsplit;
     const __amdgpu_buffer_rsrc_t prs = frag_rsrc(a.fpart, (uint32_t)(nrec * G * D * 4));
@@ -695,14 +705,16 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
         }
         // q (and the appended key / value) staged in the same block as the K / V requests, so
         // the wait for the slabs counts exactly the requests behind them
-        f32x4 acc = u0;
-        acc += u1;
-        if (role == 0) {
+        if constexpr (!TAIL) {
+            f32x4 acc = u0;
+            acc += u1;
+            if (role == 0) {
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) L.qs[g_own][4 * c4 + jj] = rbf(acc[jj]);
-        } else if (has_t) {
+                for (int jj = 0; jj < 4; ++jj) L.qs[g_own][4 * c4 + jj] = rbf(acc[jj]);
+            } else if (has_t) {
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) L.kvnew[role - 1][4 * c4 + jj] = rbf(acc[jj]);
+                for (int jj = 0; jj < 4; ++jj) L.kvnew[role - 1][4 * c4 + jj] = rbf(acc[jj]);
+            }
         }
         // the RoPE row consumed here too (an empty asm use): past the branch join the compiler
         // would otherwise wait for nearly every K / V request before the q rotation
@@ -719,6 +731,25 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
         for (int i = 0; i < NIT; ++i) kr[i] = vr[i] = (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) c8[jj] = s8[jj] = 0.f;
+    }
+    if constexpr (TAIL) {
+        mid();   // N3, the q|k|v stage and its hand-off (workgroup-uniform, with barriers)
+        const __amdgpu_buffer_rsrc_t qrs = raw_rsrc(a.qkv_in, (uint32_t)(2 * M * a.qkv_dim * 4));
+        u0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qrs, (int)((m * a.qkv_dim + uo) * 4), 0, AUX_SC1));
+        u1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(qrs, (int)(((M + m) * a.qkv_dim + uo) * 4), 0,
+                                                                              AUX_SC1));
+        if (gt == 0) L.last = 0;
+        if (gv) {
+            f32x4 acc = u0;
+            acc += u1;
+            if (role == 0) {
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) L.qs[g_own][4 * c4 + jj] = rbf(acc[jj]);
+            } else if (has_t) {
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) L.kvnew[role - 1][4 * c4 + jj] = rbf(acc[jj]);
+            }
+        }
     }
     fb_lds_barrier();
     FS_TS(2);
@@ -956,10 +987,13 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
     FS_TS(7);
 }
 
-// SELF: with the self-attention stage S in front (a.self_attn; a separate instantiation, so the
-// launch without it carries none of S's code or registers)
-template <bool SELF>
+// SM: the self-attention stage S -- 0 none, 1 in front of O1 (a.self_attn), 2 at the end for
+// the next layer, followed by the next layer's O1 (a.self_tail; N1 then reads the previous
+// launch's o-projection slabs). Separate instantiations, so a launch carries only its own
+// stages' code and registers.
+template <int SM>
 __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a) {
+    constexpr bool SELF = SM == 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     f32x4* red = (f32x4*)smem;                                   // GEMV partial sums, <= 60 KB
     FbAttnLds& al = *(FbAttnLds*)(smem + 5 * FM_NW * 1024);      // attention scratch
@@ -983,12 +1017,21 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     // ---- S: the layer's self-attention on every workgroup (O1 waits for its heads)
     if constexpr (SELF) {
         FS_TS(0);
-        fb_self_attn(a, *(FbSelfLds*)smem);
+        fb_self_attn<false>(a, *(FbSelfLds*)smem, [] {}, nb, -1);
         if (FS_DBG_VAR == 4) {   // timing variant: the stage again, warm (points overwritten)
             FS_TS(13);
-            fb_self_attn(a, *(FbSelfLds*)smem);
+            fb_self_attn<false>(a, *(FbSelfLds*)smem, [] {}, nb, -1);
         }
         FS_TS(8);
+    }
+    // the tail's row length, requested first (the oldest load: waiting for it later waits for
+    // nothing else); the same slot map as fb_self_attn<true> over the nb - M workers
+    int len_tail = 0;
+    if constexpr (SM == 2) {
+        if (a.Wqkv) FS_TS(0);   // (the last layer's launch has no tail: its start would overwrite)
+        const int nwk = nb - M, cidx = bu + (wave >> 2) * nwk;
+        const int rk = cidx % (M * a.Hkv);
+        len_tail = a.kv_len[bu < nwk ? rk / a.Hkv : 0];
     }
 
     // ---- the attention workers request their row's cross K / V chunk and RoPE row
@@ -1292,7 +1335,38 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     // (<= 3 units), weights requested while N3 runs
     if (a.Wqkv) {
         const int kper = nw / 2, sk = w / kper, jk = w - sk * kper;
-        if (sk < 2) {
+        if constexpr (SM == 2) {
+            // the tail: q|k|v written through and handed off in-launch, the next layer's self
+            // attention (its K / V requested before the N3 wait), then the next layer's O1
+            const int nu_k = sk < 2 ? (a.NGqkv - jk + kper - 1) / kper : 0;
+            bf16x8_s wk[3][3];
+            fb_issue<FM_NW, 3, 3>(wk, a.Wqkv, a.NGqkv, d / 32, sk * 36, 36, jk, kper, nu_k);
+            auto mid = [&]() __attribute__((always_inline)) {
+                // wave 11 (group 2: never a chunk slot in the tail, so no K / V queued ahead of
+                // its polls) waits for N3, then for every q|k|v workgroup
+                if (wave == FM_NW - 1) ok &= fm_wait_n<1>(a.sync, L_N3, (unsigned)M, tmo, 15u);
+                FS_TS_BY(17, (FM_NW - 1) * 64);
+                fb_finish<FM_NW, EPI_F32, 3, 3, 2>(wk, jk, kper, nu_k, sk * 36, 36, a.xn, d, M * d * 2, M,
+                                                   a.qkv_out + (long)sk * M * a.qkv_dim, a.qkv_dim,
+                                                   M * a.qkv_dim * 4, a.qkv_dim, red);
+                fb_publish(cline(a.sync, L_K0 + (w & 7)), 1u);   // every worker (an odd one projects nothing)
+                FS_TS(18);
+                if (wave == FM_NW - 1) ok &= fm_wait_split<8>(a.sync, L_K0, (unsigned)nw, tmo, 19u);
+                FS_TS_BY(19, (FM_NW - 1) * 64);
+                wg_barrier();
+            };
+            fb_self_attn<true>(a, *(FbSelfLds*)gul, mid, nw, len_tail);
+            // the next layer's O1: k-slice so waits for kv head so's rows
+            if (owork) {
+                bf16x8_s w1[3][2];
+                fb_issue<8, 2, 3>(w1, a.Wo1n, a.NGo, a.q_dim / 32, so * 16, 16, jo, oper, nu_o);
+                if (wave == FM_NW - 1) ok &= fm_wait_n<1>(a.sync, L_S0 + so, (unsigned)M, tmo, 20u);
+                FS_TS_BY(20, (FM_NW - 1) * 64);
+                fb_finish<8, EPI_F32, 2, 3, 2>(w1, jo, oper, nu_o, so * 16, 16, a.att_self, a.q_dim, M * a.q_dim * 2, M,
+                                               a.o1n + (long)so * M * d, d, M * d * 4, d, red);
+                FS_TS(21);
+            }
+        } else if (sk < 2) {
             const int nu_k = (a.NGqkv - jk + kper - 1) / kper;
             bf16x8_s wk[3][3];
             fb_issue<FM_NW, 3, 3>(wk, a.Wqkv, a.NGqkv, d / 32, sk * 36, 36, jk, kper, nu_k);
@@ -1366,9 +1440,19 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
         // function attributes and the occupancy check are per device (an engine per GPU in
         // one process must not skip the second device's hipFuncSetAttribute)
         if (dev < 0 || dev >= 64) return -1;
-        const int sv = a.self_attn ? 1 : 0;
-        auto* fb = sv ? fused_block_kernel<true> : fused_block_kernel<false>;
-        static bool attr_b[64][2] = {};
+        // the tail: the next layer's S after the q|k|v stage, then its O1 (front O1 off); slots
+        // on groups 0-1 of the workers only (group 2 polls), the S scratch in the gate/up unit's LDS
+        static_assert(sizeof(FbSelfLds) <= (size_t)FB_GU_KB * 1024, "tail S scratch in the gate/up unit LDS");
+        if (a.self_tail &&
+            (a.self_attn || a.Wo1 || !a.Wqkv || !a.Wo1n || !a.o1n || !a.att_self || a.qkv_in != a.qkv_out ||
+             !a.sk || !a.sv || !a.kv_len || !a.fpart || !a.fstat || !a.fticket || a.Hq != 8 || a.Hkv != 4 ||
+             a.D != FS_D || a.M > FS_MAXROWS || a.qkv_dim != a.q_dim + 2 * a.Hkv * a.D || a.s_cap < 1 ||
+             a.s_nsplit < 1 || a.s_nsplit > FS_CMAX || a.s_nsplit > (a.s_cap + FS_CH - 1) / FS_CH || a.window < 0 ||
+             a.M * a.Hkv * a.s_nsplit > 2 * (nb - a.M) || (long)a.M * a.Hkv * a.s_nsplit * FS_G * FS_D * 4 > 0x7fff0000L))
+            return -1;
+        const int sv = a.self_tail ? 2 : a.self_attn ? 1 : 0;
+        auto* fb = sv == 2 ? fused_block_kernel<2> : sv ? fused_block_kernel<1> : fused_block_kernel<0>;
+        static bool attr_b[64][3] = {};
         if (!attr_b[dev][sv]) {
             (void)hipFuncSetAttribute((const void*)fb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FM_LDS_MAX);
             int occ = 0;

@@ -124,14 +124,21 @@ struct FusedMlpArgs {
     float* fpart;             // [M][Hkv][s_nsplit][G][D] chunk partials
     float* fstat;             // [M][Hkv][s_nsplit][G][2] chunk max / sum
     unsigned* fticket;        // [M][Hkv] arrival tickets (zero between launches)
+    // ---- stage S at the END instead (self_tail = 1, needs Wqkv, no Wo1): the S fields above
+    //   describe the NEXT layer, whose q|k|v this launch projects; then that layer's O1 into
+    //   o1n ([4][M][d], the next launch's o_slabs: its N1 reads them, Wo1 null there)
+    int self_tail;
+    const bf16_t* Wo1n;       // the next layer's packed self o_proj
+    float* o1n;
 };
 int fused_mlp(const FusedMlpArgs& a, hipStream_t st);
 int fused_mlp_check(const FusedMlpArgs& a);   // 0: fused_mlp would launch these args; -1: not built for them
 // counter words of one fused launch, each on its own 128-byte line (arrivals on one line
 // serialise at ~12 ns each): N1, 8 cross-q heads, 8 attention heads, 8 cross-o groups,
-// N2, 8 down slices, 8 down groups, N3, 8 o-projection groups, 8 self-attention kv heads.
+// N2, 8 down slices, 8 down groups, N3, 8 o-projection groups, 8 self-attention kv heads, 8
+// q|k|v groups (the tail's in-launch hand-off).
 // The engine keeps one set per decoder layer after one line for the timeout word.
-constexpr int FM_LINE = 32, FM_SET_LINES = 59, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
+constexpr int FM_LINE = 32, FM_SET_LINES = 67, FM_SET_WORDS = FM_SET_LINES * FM_LINE;
 
 // parity mode's decode layer after the self attention as one persistent launch (xlayer.hip):
 // O1 self o-proj, N1, cross q, PM cross attention, cross o, N2, gate/up + GeGLU, down in the

@@ -233,13 +233,14 @@ class T5GemmaTTSEngine:
         _lib.check(self.L.t5g_engine_xlayer_launches(self.h, C.byref(n)), "xlayer_launches")
         return n.value
 
-    def set_attn_in_block(self, enable: bool) -> None:
-        """Fast-path decode self attention as the first stage of the persistent layer launch
-        (default; csrc/fused.hip stage S: no attention launch between the layers) or as its
-        own flash launch; bitwise equal. Needs the flash form and the persistent launch
-        (set_attn_flash, set_fused); rows x kv heads x ceil(chunks / 3) above the CU count
-        keep the separate launch."""
-        _lib.check(self.L.t5g_engine_set_attn_in_block(self.h, 1 if enable else 0), "set_attn_in_block")
+    def set_attn_in_block(self, mode) -> None:
+        """Fast-path decode self attention inside the persistent layer launch (csrc/fused.hip
+        stage S): 0 / False its own flash launch, 1 in front of the launch's o-projection,
+        2 / True (default) at the end of the previous layer's launch after its q|k|v stage,
+        with that layer's o-projection. Bitwise equal in every mode; calls past the stage's
+        chunk-slot or 1 024-key bound keep the separate launch."""
+        m = 2 if mode is True else 0 if mode is False else int(mode)
+        _lib.check(self.L.t5g_engine_set_attn_in_block(self.h, m), "set_attn_in_block")
 
     def attn_in_block_launches(self) -> int:
         """Fast-path persistent layer launches issued with the self attention inside (test /

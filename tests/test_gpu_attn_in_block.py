@@ -54,7 +54,7 @@ def _utts(cfg, n, seed, tp_max):
 
 
 def _run(eng, utts, p, seeds, on):
-    eng.set_attn_in_block(on)
+    eng.set_attn_in_block(on)   # 0 the separate flash launch, 1 stage S in front, 2 at the end
     before = eng.attn_in_block_launches()
     # host loop (every step's logits) and the graph-replayed on-device loop (tokens)
     out = eng.generate(utts, p, seeds=seeds, parity=True, exact=False, record_logits=True)
@@ -72,17 +72,18 @@ def _assert_same(a, b, B, tag):
         assert torch.equal(la.view(torch.int16), lb.view(torch.int16)), (tag, s)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("B,tp_max", [(1, 1), (3, 300), (8, 400), (16, 300)])
-def test_attention_in_block_bitwise_equal_to_flash_launch(B, tp_max):
+def test_attention_in_block_bitwise_equal_to_flash_launch(B, tp_max, mode):
     _need_gpu()
     from t5gemma_tts_amd.engine import SamplingParams
     cfg, eng = _engine(16, 448)
     utts = _utts(cfg, B, 60 + B, tp_max)
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
     seeds = list(range(900, 900 + B))
-    on0, fon0, n_on0 = _run(eng, utts, p, seeds, True)
-    off, foff, n_off = _run(eng, utts, p, seeds, False)
-    on1, fon1, n_on1 = _run(eng, utts, p, seeds, True)
+    on0, fon0, n_on0 = _run(eng, utts, p, seeds, mode)
+    off, foff, n_off = _run(eng, utts, p, seeds, 0)
+    on1, fon1, n_on1 = _run(eng, utts, p, seeds, mode)
     assert n_off == 0 and n_on0 > 0 and n_on1 > 0   # stage S ran, and only when enabled
     _assert_same(on0, off, B, "on/off")
     _assert_same(on0, on1, B, "on/on")
@@ -91,7 +92,8 @@ def test_attention_in_block_bitwise_equal_to_flash_launch(B, tp_max):
     assert sum(len(g) for g in on0["gen"]) > B
 
 
-def test_attention_in_block_sliding_window():
+@pytest.mark.parametrize("mode", [1, 2])
+def test_attention_in_block_sliding_window(mode):
     """Layer 0 slides over a 100-key window: rows past it start their chunks at t - 99."""
     _need_gpu()
     from t5gemma_tts_amd.engine import SamplingParams
@@ -99,8 +101,8 @@ def test_attention_in_block_sliding_window():
     utts = _utts(cfg, 6, 17, 350)
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
     seeds = list(range(6))
-    on, fon, n_on = _run(eng, utts, p, seeds, True)
-    off, foff, _ = _run(eng, utts, p, seeds, False)
+    on, fon, n_on = _run(eng, utts, p, seeds, mode)
+    off, foff, _ = _run(eng, utts, p, seeds, 0)
     assert n_on > 0
     _assert_same(on, off, 6, "window")
     _assert_same(fon, foff, 6, "window graph")
@@ -120,8 +122,10 @@ def test_attention_in_block_falls_back_past_one_task_per_workgroup():
             for _ in range(16)]
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
     seeds = list(range(16))
-    on, fon, n_on = _run(eng, utts, p, seeds, True)
-    off, foff, _ = _run(eng, utts, p, seeds, False)
-    assert n_on == 0
+    on, fon, n_on = _run(eng, utts, p, seeds, 2)
+    on1, fon1, n_on1 = _run(eng, utts, p, seeds, 1)
+    off, foff, _ = _run(eng, utts, p, seeds, 0)
+    assert n_on == 0 and n_on1 == 0
     _assert_same(on, off, 16, "fallback")
+    _assert_same(on1, off, 16, "fallback 1")
     _assert_same(fon, foff, 16, "fallback graph")

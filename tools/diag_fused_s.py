@@ -16,7 +16,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["T5G_LIB"] = os.path.join(REPO, "t5gemma-tts_amd", "lib", "libt5gtts_dbg.so")
 sys.path.insert(0, REPO)
 
-NAMES = {14: "q rotated (wave 0)", 15: "first K row scored", 16: "scores done (wave 0)", 13: "second S run starts", 1: "row geometry", 2: "q staged", 3: "K in + scores", 4: "P.V reduced", 5: "partials drained",
+NAMES = {17: "N3 seen (tail)", 18: "q|k|v published", 19: "q|k|v all seen", 20: "O1n hand-off seen",
+         21: "O1n done", 14: "q rotated (wave 0)", 15: "first K row scored", 16: "scores done (wave 0)", 13: "second S run starts", 1: "row geometry", 2: "q staged", 3: "K in + scores", 4: "P.V reduced", 5: "partials drained",
          6: "ticket seen", 7: "att_self published", 8: "S left", 9: "O1 hand-off seen", 10: "O1 published",
          11: "Q hand-off seen", 12: "N1 published"}
 
@@ -34,6 +35,8 @@ def main():
     sd = synthetic_weights(cfg, seed=1234, device=dev)
     eng = T5GemmaTTSEngine(cfg, sd, device=dev, max_batch=B, max_text=64, max_audio=160 + n_gen + 64,
                            max_gen=n_gen + 16)
+    mode = int(os.environ.get("FS_MODE", "2"))   # 1: stage S in front, 2: at the end (times of layer L-2's launch)
+    eng.set_attn_in_block(mode)
     rng = np.random.default_rng(0)
     utts = [Utterance(x=rng.integers(3, 4000, size=60).tolist(),
                       y=rng.integers(0, 65536, size=150).tolist() + [cfg.y_sep_token], tgt_y_len=151 + n_gen)
@@ -55,7 +58,7 @@ def main():
         live = ts[:, 0] > 0
         t0 = ts[live, 0].min()
         print(f"--- rep {rep} variant {var}: {int(live.sum())} workgroups, B={B}, keys ~{152 + n_gen}")
-        for k in (13, 1, 2, 14, 15, 16) + tuple(range(3, 13)):
+        for k in (17, 18, 19, 13, 1, 2, 14, 15, 16) + tuple(range(3, 13)) + (20, 21):
             v = ts[live, k]
             v = v[v > 0]
             if not len(v):

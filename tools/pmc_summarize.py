@@ -29,11 +29,12 @@ OPS = {
                             "T_x=60, 2b-2b widths (tools/pmc_fused.py: 26 layers rotated, 4.3 GB > 256 MiB Infinity "
                             "Cache); algorithmic = weights + cross K/V + o slabs, h, norm weights, RoPE rows in + h, "
                             "q|k|v slabs out"},
-    "fused_block_s": {"kernels": ["fused_block_kernel<true>"],
+    "fused_block_s": {"kernels": ["fused_block_kernel<2>"],
                       "algorithmic": None,   # tools/pmc_fused.py --self writes it (keys of the run)
-                      "what": "fast-path persistent decode layer WITH the self attention (stage S: flash chunks "
-                              "over the cached K / V + append -> o-proj -> norm -> cross-q -> PM cross attention -> "
-                              "cross-o -> norm -> gate/up GeGLU -> down -> norm -> next q|k|v), M=8, T_x=60, L = 903 (the rows' "
+                      "what": "fast-path persistent decode layer WITH the next layer's self attention at its end "
+                              "(norm -> cross-q -> PM cross attention -> cross-o -> norm -> gate/up GeGLU -> down -> "
+                              "norm -> next q|k|v -> stage S: flash chunks over the next layer's cached K / V + "
+                              "append -> next o-proj), M=8, T_x=60, L = 903 (the rows' "
                               "final length, where bench.py times it), "
                               "2b-2b widths (tools/pmc_fused.py --self: 26 layers rotated); algorithmic = weights + "
                               "self K/V read + appended K/V + q|k|v slabs + cross K/V + h, norm weights, RoPE rows in "
