@@ -378,7 +378,10 @@ def main():
             if B <= 16:   # the step runs the whole post-self-attention block in one launch
                 us_k, kname = us.value, _lib.FUSED_BLOCK_KERNEL
                 alg_bytes = _lib.fused_block_bytes(B, wl_tx, d, f, self_keys=keys.value)
-                if keys.value > 0:
+                if keys.value > 0 and args.attn_in_block == 1:
+                    kname = "fused_block_kernel<1> (the layer's self attention in front of its o-projection)"
+                    pmc = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s_front.json")
+                elif keys.value > 0:
                     kname = _lib.FUSED_BLOCK_S_KERNEL
                     pmc = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s.json")
                 else:
