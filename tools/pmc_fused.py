@@ -27,7 +27,7 @@ def main():
     # roofline leg times the launch at), the generate on the launches without S (another kernel
     # instantiation), so the PMC rows of fused_block_kernel<true> are the timed launches only
     n_gen = 751 if self_stage else 8
-    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=B, max_text=64, max_audio=152 + n_gen + 8,
+    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=B, max_text=64, max_audio=152 + n_gen + 16,
                            max_gen=n_gen + 16)
     if self_stage:
         eng.set_attn_in_block(False)
