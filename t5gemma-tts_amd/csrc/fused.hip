@@ -561,9 +561,8 @@ constexpr size_t FB_LDS = FB_GU_OFF + (size_t)FB_GU_KB * 1024;
 // attn_decode_kernel<256, 2, true, true> + attn_flash_finish restated on this launch's 12
 // waves as three 4-wave groups, each one 64-key chunk in that kernel's lane map: the same
 // loads, q / new-key PM-RoPE, cache append, sums and roundings, so the launch stays bitwise
-// equal to the flash launch + the per-op chain. Chunk c of the call (rows in order, kv heads,
-// chunks from the row start) runs on workgroup c % nb, group c / nb, so the K / V stream is
-// spread over every CU. A chunk's partial goes out write-through with one ticket add per
+// equal to the flash launch + the per-op chain. Chunk slots (chunk-major: chunk x rows x kv
+// heads) run on workgroup c % nwg, group c / nwg, so the K / V stream is spread over every CU. A chunk's partial goes out write-through with one ticket add per
 // chunk; the workgroup holding the last chunk of a (row, kv head) combines them in the flash
 // kernel's order (its whole workgroup, after every group's ticket) and publishes att_self on
 // line L_S0 + kv head, which O1's k-slice of that head pair waits for. Rows of <= 64 keys take
@@ -587,7 +586,6 @@ struct FbSelfGrp {
 };
 struct FbSelfLds {
     FbSelfGrp g[FS_GRP];
-    int rlo[FS_MAXROWS], rspan[FS_MAXROWS], rnch[FS_MAXROWS];
 };
 static_assert(sizeof(FbSelfLds) <= 5 * FM_NW * 1024, "stage S lives in the GEMV partial-sum LDS");
 
