@@ -311,8 +311,9 @@ int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable);
  * the END of the previous layer's launch -- after its q|k|v stage, with the K / V requested
  * before the N3 wait -- followed by that layer's o-projection, whose slabs the next launch's
  * norm reads (layer 0's attention and o-projection stay the step's own launches). Every mode
- * is bitwise equal to mode 0. Calls whose rows x kv heads x chunks exceed 3 (mode 1) / 2
- * (mode 2) chunk slots per workgroup, or rows past 1 024 keys, keep the separate launch.
+ * is bitwise equal to mode 0. A call whose rows x kv heads x chunks exceed 2 chunk slots per
+ * worker takes mode 1 instead of 2; past 3 per workgroup, or rows past 1 024 keys, the
+ * separate launch.
  * Replaces the reference's per-layer self-attention call inside PMDecoderLayer
  * (hf_export/modeling_t5gemma_voice.py:256-323, [tf] modeling_t5gemma.py:264-304).
  * t5g_engine_attn_in_block_launches: layer launches issued with S (captured ones once). */

@@ -1190,7 +1190,8 @@ static bool fused_block_tail(t5g_engine* e, int M, int l, FusedMlpArgs& fa) {
 
 static bool fused_block_self(t5g_engine* e, int M, int l, FusedMlpArgs& fa) {
     const t5g_config& c = e->c;
-    if (e->attn_in_block != 1 || !e->attn_flash || !fa.Wo1) return false;
+    // mode 1, or mode 2 on a call the tail does not take (2 slots per worker): S in front
+    if (e->attn_in_block < 1 || !e->attn_flash || !fa.Wo1) return false;
     fa.self_attn = 1;
     fa.qkv_in = e->part;
     fa.sk = e->sk[l];
@@ -2074,13 +2075,18 @@ extern "C" int t5g_time_decode_layer(t5g_engine* e, int32_t B, int32_t iters, vo
     const int L = c.n_dec_layers;
     // attn_in_block 1: launch l runs layer l's attention in front; 2: layer l + 1's at its end
     // (the last launch none; layer 0's is the step's own launch, not timed here)
-    const bool tail = e->attn_in_block == 2;
+    // (mode 2 on a call the tail does not take runs S in front, as decoder_pass does)
+    bool tail = e->attn_in_block == 2;
+    FusedMlpArgs fa;
+    for (int l = 0; l < L && tail; ++l) {
+        fa = fused_block_args(e, B, l);
+        tail = fused_block_tail(e, B, l, fa);
+    }
     auto args = [&](int l, FusedMlpArgs& fa) {
         fa = fused_block_args(e, B, l);
         if (tail) return fused_block_tail(e, B, l, fa);
         return fused_mlp_check(fa) == 0 && fused_block_self(e, B, l, fa);
     };
-    FusedMlpArgs fa;
     for (int l = 0; l < L; ++l)
         if (!args(l, fa)) return T5G_EUNSUPPORTED;
     std::vector<int> len(B);

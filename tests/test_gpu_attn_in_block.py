@@ -129,3 +129,23 @@ def test_attention_in_block_falls_back_past_one_task_per_workgroup():
     _assert_same(on, off, 16, "fallback")
     _assert_same(on1, off, 16, "fallback 1")
     _assert_same(fon, foff, 16, "fallback graph")
+
+
+def test_tail_mode_falls_back_to_front_past_two_slots_per_worker():
+    """16 rows of ~600 keys: 16 x 4 kv heads x 10 chunks = 640 > 2 slots per worker (480), so
+    mode 2 runs stage S in front of each layer's o-projection (<= 3 per workgroup) -- still no
+    separate attention launch, the same bits."""
+    _need_gpu()
+    from t5gemma_tts_amd.engine import SamplingParams, Utterance
+    cfg, eng = _engine(16, 640)
+    rng = np.random.default_rng(4)
+    utts = [Utterance(x=rng.integers(3, 4000, size=20).tolist(),
+                      y=rng.integers(0, 65536, size=590).tolist() + [cfg.y_sep_token], tgt_y_len=591 + 10)
+            for _ in range(16)]
+    p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
+    seeds = list(range(16))
+    on, fon, n_on = _run(eng, utts, p, seeds, 2)
+    off, foff, _ = _run(eng, utts, p, seeds, 0)
+    assert n_on > 0
+    _assert_same(on, off, 16, "front fallback")
+    _assert_same(fon, foff, 16, "front fallback graph")
