@@ -799,20 +799,23 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
         }
         // the scores stay in registers until every key's reduction is done (no store between
         // them), so the 16 butterfly reductions of a wave overlap instead of running one by one
+        // the two q heads side by side in packed fp32 (v_pk_mul / v_pk_add: the same IEEE
+        // operations per head, half the instructions)
+        static_assert(G == 2, "packed head pair");
+        f32x2 qq[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) qq[jj] = (f32x2){q[0][jj], q[1][jj]};
         float sc[NIT][G];
 #pragma unroll
         for (int i = 0; i < NIT; ++i) {
-            float s[G];
-#pragma unroll
-            for (int g = 0; g < G; ++g) s[g] = 0.f;
+            f32x2 s2 = {0.f, 0.f};
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
                 const float k0 = bf_lo(kr[i][jj]), k1 = bf_hi(kr[i][jj]);
-#pragma unroll
-                for (int g = 0; g < G; ++g) s[g] += q[g][2 * jj] * k0 + q[g][2 * jj + 1] * k1;
+                s2 += qq[2 * jj] * k0 + qq[2 * jj + 1] * k1;
             }
 #pragma unroll
-            for (int g = 0; g < G; ++g) sc[i][g] = xsum_v<LPK>(s[g]);   // xsum<LPK>'s adds, VALU exchanges
+            for (int g = 0; g < G; ++g) sc[i][g] = xsum_v<LPK>(s2[g]);   // xsum<LPK>'s adds, VALU exchanges
         }
         FS_TS(16);
         if (dl == 0) {
@@ -849,28 +852,25 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
     }
     fb_lds_barrier();
     if (gv) {
+        // both heads' accumulators packed (o2[d] = {head 0, head 1}): the same per-head chain
+        f32x2 o2[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o2[jj] = (f32x2){0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+            const int jl = i * KPB + gw * KPW + kg;
+            const f32x2 pp = {L.sm[0][jl], L.sm[1][jl]};
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                o2[2 * jj] += pp * bf_lo(vr[i][jj]);
+                o2[2 * jj + 1] += pp * bf_hi(vr[i][jj]);
+            }
+        }
         float o[G][8];
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) o[g][jj] = 0.f;
-#pragma unroll
-        for (int i = 0; i < NIT; ++i) {
-            const int jl = i * KPB + gw * KPW + kg;
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const float p = L.sm[g][jl];
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    o[g][2 * jj] += p * bf_lo(vr[i][jj]);
-                    o[g][2 * jj + 1] += p * bf_hi(vr[i][jj]);
-                }
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) o[g][jj] += xlane32_v(o[g][jj]);   // LPK = 32: the kernel's one xor-32 step
+            for (int jj = 0; jj < 8; ++jj) o[g][jj] = o2[jj][g] + xlane32_v(o2[jj][g]);   // LPK = 32: one xor-32 step
         if (kg == 0) {
 #pragma unroll
             for (int g = 0; g < G; ++g) {
