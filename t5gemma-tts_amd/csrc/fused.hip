@@ -1195,7 +1195,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
                 for (int jj = 0; jj < 4; ++jj) al.qs[4 * c4 + jj] = rbf(acc[jj]);
             }
         }
-        __syncthreads();
+        fb_lds_barrier();   // LDS only: waves 4-7 keep their O weights in flight
         if (tq < 256) {
             float q[8];
             const float sg = dl < LPK / 2 ? -1.0f : 1.0f;
@@ -1214,6 +1214,8 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
                     vr[i] = (u32x4){0u, 0u, 0u, 0u};
                 }
             }
+            // every key's reduction before any store (they overlap), exchanges on the VALU
+            float scs[NIT];
 #pragma unroll
             for (int i = 0; i < NIT; ++i) {
                 float sc = 0.f;
@@ -1222,12 +1224,14 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
                     const float k0 = bf_lo(kr[i][jj]), k1 = bf_hi(kr[i][jj]);
                     sc += q[2 * jj] * k0 + q[2 * jj + 1] * k1;
                 }
-                sc = xsum<LPK>(sc);
-                const int jl = i * KPB + wave * KPW + kg;
-                if (dl == 0) al.sm[jl] = fast_score(sc, a.scale, a.softcap);
+                scs[i] = xsum_v<LPK>(sc);   // xsum<LPK>'s adds
+            }
+            if (dl == 0) {
+#pragma unroll
+                for (int i = 0; i < NIT; ++i) al.sm[i * KPB + wave * KPW + kg] = fast_score(scs[i], a.scale, a.softcap);
             }
         }
-        __syncthreads();
+        fb_lds_barrier();   // LDS only: waves 4-7 keep their O weights in flight
         if (wave == 0) {
             const float sc = lane < n ? al.sm[lane] : -INFINITY;
             const float mx = wave_max(sc);
@@ -1239,7 +1243,7 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
             const float l = sdpa_block_sum_lds<64>(al.pl, span, lane);
             if (lane == 0) al.stat_l = l;
         }
-        __syncthreads();
+        fb_lds_barrier();   // LDS only: waves 4-7 keep their O weights in flight
         if (tq < 256) {
             float o[8];
 #pragma unroll
@@ -1255,15 +1259,13 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
                 }
             }
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj)
-#pragma unroll
-                for (int off = LPK; off < 64; off <<= 1) o[jj] += __shfl_xor(o[jj], off, 64);
+            for (int jj = 0; jj < 8; ++jj) o[jj] += xlane32_v(o[jj]);   // LPK = 32: one xor-32 step
             if (kg == 0) {
                 al.ored[wave][dl][0] = (f32x4){o[0], o[1], o[2], o[3]};
                 al.ored[wave][dl][1] = (f32x4){o[4], o[5], o[6], o[7]};
             }
         }
-        __syncthreads();
+        fb_lds_barrier();   // LDS only: waves 4-7 keep their O weights in flight
         if (tq < LPK && n > 0) {
             const int d8 = tq;
             const f32x4 lo4 = al.ored[0][d8][0] + al.ored[1][d8][0] + al.ored[2][d8][0] + al.ored[3][d8][0];
@@ -1277,7 +1279,12 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
             const __amdgpu_buffer_rsrc_t orr = raw_rsrc(a.att, (uint32_t)(M * a.q_dim * 2));
             __builtin_amdgcn_raw_buffer_store_b128(w, orr, (am * a.q_dim + ah * D + 8 * d8) * 2, 0, AUX_SC1);
         }
-        fb_publish(cline(a.sync, L_A0 + ah), 1u);
+        // only wave 0 stored: it drains and publishes (the other waves' O weight requests
+        // stay in flight)
+        if (wave == 0) {
+            drain_vm();
+            if (lane == 0) __hip_atomic_fetch_add(cline(a.sync, L_A0 + ah), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 
     // ---- O: cross-o, 4 k-slices of 16 k-steps over nw / 4 workers each (<= 3 units, 8 waves)
