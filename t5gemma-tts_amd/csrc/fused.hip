@@ -388,6 +388,11 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_mlp_kernel(FusedMlpArgs a) {
 // of a stage as early as its registers allow: Q's before N1 completes, O's during the
 // attention, gate/up's right after O (norm workgroups: after N2), down's after gate/up;
 // the cross K / V of the attention workgroups and their RoPE table at launch start.
+// Round 5 adds the layer's decode self attention as stage S (fb_self_attn, the flash launch's
+// arithmetic): fused_block_kernel<1> runs it in front of O1; fused_block_kernel<2> runs the
+// NEXT layer's at the end, after the q|k|v stage (its K / V requested before the N3 wait),
+// followed by that layer's O1 into the slabs the next launch's N1 reads
+// (tests/test_gpu_attn_in_block.py: bitwise equal to the separate flash launch).
 
 // Split form of fm_gemv: the weight requests (waves < NWG) ...
 template <int NWG, int SPU, int UMAX>
