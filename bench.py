@@ -321,6 +321,8 @@ def main():
         stream_p = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         us_x = C.c_float()
         rc_xl = _lib.lib().t5g_time_xlayer(eng.h, B, 26 * 8, stream_p, C.byref(us_x))
+        if rc_xl not in (0, _lib.T5G_EUNSUPPORTED):
+            _lib.check(rc_xl, "time_xlayer")   # a real launch failure, not a shape the launch does not serve
         if rc_xl == 0:
             xbytes = _lib.xlayer_bytes(B, cfg.backbone, wl_tx, cfg.backbone.num_decoder_layers)
             pmc_x = os.path.join(REPO, "profiles", "r05_pmc_xlayer.json")
@@ -331,17 +333,18 @@ def main():
             _lib.check(_lib.lib().t5g_time_exact_linears(eng.h, B, 26 * 8, stream_p, C.byref(us_x)),
                        "time_exact_linears")
             xbytes = _lib.exact_linears_bytes(B, cfg.backbone)
-            pmc_x = os.path.join(REPO, "profiles", "r05_pmc_exact_linears.json")
             kname = ("xmm_dec_kernel: one layer's six exact decode Linears (q|k|v, o, cross-q, cross-o, "
                      "gate/up + GeGLU, down in the reference's K parts; f32 MFMA in the reference host's fp32 "
                      "orders)")
-        traffic_x = None
-        if os.path.exists(pmc_x) and B == 8:
-            traffic_x = json.load(open(pmc_x)).get("hbm_bytes_per_call")
+        traffic_x, tinfo_x = None, {"traffic_note": "PMC passes are at 8 rows"}
+        if rc_xl != 0:
+            tinfo_x = {"traffic_note": "no PMC pass of the per-op exact Linears"}
+        elif B == 8:
+            traffic_x, tinfo_x = _lib.pmc_traffic(pmc_x, "xlayer", "xlayer_kernel")
         ach_x = xbytes / (us_x.value * 1e-6) / 1e9
         parity_roof = {"bound": "hbm", "achieved": round(ach_x, 1), "peak": 8000.0, "unit": "GB/s",
                        "frac": round(ach_x / 8000.0, 4), "traffic": traffic_x, "kernel": kname,
-                       "algorithmic_bytes": int(xbytes), "avg_us": round(us_x.value, 2)}
+                       "algorithmic_bytes": int(xbytes), "avg_us": round(us_x.value, 2), **tinfo_x}
         parity_line = {
             "value": round(parity_stats["tokens"] / dtp, 2), "unit": "audio tokens/s",
             "ms_per_step": round(dtp / args.parity_steps * 1e3, 2), "steps": args.parity_steps,
@@ -380,15 +383,15 @@ def main():
                 alg_bytes = _lib.fused_block_bytes(B, wl_tx, d, f, self_keys=keys.value)
                 if keys.value > 0 and args.attn_in_block == 1:
                     kname = "fused_block_kernel<1> (the layer's self attention in front of its o-projection)"
-                    pmc = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s_front.json")
+                    pmc, pmc_op = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s_front.json"), "fused_block_s"
                 elif keys.value > 0:
                     kname = _lib.FUSED_BLOCK_S_KERNEL
-                    pmc = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s.json")
+                    pmc, pmc_op = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s.json"), "fused_block_s"
                 else:
-                    pmc = os.path.join(REPO, "profiles", "r04_pmc_fused_block.json")
+                    pmc, pmc_op = os.path.join(REPO, "profiles", "r04_pmc_fused_block.json"), "fused_block"
             else:
                 us_k, alg_bytes, kname = us.value, _lib.fused_mlp_bytes(B, d, f), _lib.FUSED_MLP_KERNEL
-                pmc = os.path.join(REPO, "profiles", "r03_pmc_fused_mlp.json")
+                pmc, pmc_op = os.path.join(REPO, "profiles", "r03_pmc_fused_mlp.json"), "fused_mlp"
         else:
             # rotate over every decoder layer's gate/up weights (2.2 GB >> 256 MiB Infinity
             # Cache) so each launch streams its weights from HBM, as inside a decode step
@@ -397,17 +400,15 @@ def main():
             us_k = _lib.time_gate_up(X.data_ptr(), d, B, [lw.gate_up for lw in eng._dec], 2 * f, d, Y.data_ptr(),
                                      208, st)
             alg_bytes, kname = 2 * f * d * 2 + B * d * 2 + B * f * 2, _lib.GATE_UP_KERNEL
-            pmc = os.path.join(REPO, "profiles", "r02_pmc_gate_up.json")
+            pmc, pmc_op = os.path.join(REPO, "profiles", "r02_pmc_gate_up.json"), "gate_up"
         achieved = alg_bytes / (us_k * 1e-6) / 1e9
-        traffic = None
-        if os.path.exists(pmc) and B == 8:
-            pj = json.load(open(pmc))
-            # the PMC pass must be of the kernel this line prices
-            if any(kname.startswith(k) or k.startswith(kname) for k in pj.get("kernels", [])):
-                traffic = pj.get("hbm_bytes_per_call")
+        traffic, tinfo = None, {"traffic_note": "PMC passes are at 8 rows"}
+        if B == 8:
+            # the PMC pass must be of the kernel this line prices, on the sources of this tree
+            traffic, tinfo = _lib.pmc_traffic(pmc, pmc_op, kname)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(achieved / 8000.0, 4), "traffic": traffic, "kernel": kname,
-                "algorithmic_bytes": int(alg_bytes), "avg_us": round(us_k, 2)}
+                "algorithmic_bytes": int(alg_bytes), "avg_us": round(us_k, 2), **tinfo}
         step_us = C.c_float()
         _lib.check(L.t5g_time_decode_step(eng.h, 20, st, C.byref(step_us)), "time_step")
         roof["decode_step_us"] = round(step_us.value, 1)

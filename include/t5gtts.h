@@ -340,7 +340,9 @@ int t5g_engine_xlayer_launches(t5g_engine* e, int64_t* n);
 /* Bench hook: average duration (us, HIP events on `stream`) of parity mode's persistent layer
  * launch at B decode rows, layers rotated as a step runs them, on the engine's current decode
  * state (call after a parity-mode generate). T5G_EUNSUPPORTED when the launch does not serve
- * B rows / this model. No reference-side equivalent. */
+ * B rows / this model. Like every t5g_time_* hook that runs engine launches, it leaves the
+ * decode state invalid: t5g_decode returns T5G_EINVAL until the next t5g_sampler_setup.
+ * No reference-side equivalent. */
 int t5g_time_xlayer(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us);
 /* Host hint: the longest text (encoder length) of the batch the next t5g_encode / t5g_decode
  * calls run (0: assume max_text). The persistent decode launch reads at most 64 cross keys

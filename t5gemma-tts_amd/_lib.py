@@ -255,6 +255,49 @@ FUSED_BLOCK_S_KERNEL = ("fused_block_kernel<2> (decode layer in one launch with 
                         "append -> next o-proj, 174.6 MB of weights)")
 T5G_EUNSUPPORTED = -3
 
+# kernel sources each PMC-measured op is built from: a profiles/*_pmc_*.json records their
+# digest when the pass runs, and bench.py quotes that file's traffic only while the sources
+# still hash the same (a kernel change that keeps the kernel's name makes the file stale)
+PMC_SOURCES = {
+    "fused_block": ["fused.hip", "common.h", "t5g_kernels.h"],
+    "fused_block_s": ["fused.hip", "common.h", "t5g_kernels.h"],
+    "fused_mlp": ["fused.hip", "common.h", "t5g_kernels.h"],
+    "xlayer": ["xlayer.hip", "exact_dev.h", "exact_math.h", "common.h", "t5g_kernels.h"],
+    "gate_up": ["gemv.hip", "common.h", "t5g_kernels.h"],
+}
+
+
+def kernel_source_digest(op: str) -> str:
+    """sha256 (hex, 16 chars) over the csrc files PMC_SOURCES names for `op`, in order."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in PMC_SOURCES[op]:
+        with open(os.path.join(_PKG, "csrc", name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(path: str, op: str, kernel_label: str = ""):
+    """(hbm bytes per launch or None, provenance dict) from a PMC summary file: None when the
+    file is missing, names another kernel, or was measured on other kernel sources than the
+    ones in this tree (its source digest differs or is absent)."""
+    import json
+    info = {"traffic_source": os.path.relpath(path, os.path.dirname(_PKG)), "traffic_source_digest": None,
+            "kernel_source_digest": kernel_source_digest(op)}
+    if not os.path.exists(path):
+        info["traffic_note"] = "no PMC file"
+        return None, info
+    pj = json.load(open(path))
+    info["traffic_source_digest"] = pj.get("source_digest")
+    if kernel_label and not any(kernel_label.startswith(k) or k.startswith(kernel_label)
+                                for k in pj.get("kernels", [])):
+        info["traffic_note"] = "PMC file measured another kernel"
+        return None, info
+    if pj.get("source_digest") != info["kernel_source_digest"]:
+        info["traffic_note"] = "stale: PMC file measured other kernel sources"
+        return None, info
+    return pj.get("hbm_bytes_per_call"), info
+
 
 def exact_linears_bytes(B: int, bb) -> int:
     """Algorithmic HBM bytes of one decoder layer's six exact decode Linear launches at B rows

@@ -133,6 +133,10 @@ struct t5g_engine {
     uint32_t* trig_exc = nullptr;   // parity mode: RoPE cos / sin exceptions (t5g_engine_set_rope_exc)
     int n_trig_exc = 0;
     bool xmm_ready = false;
+    // the timing hooks (t5g_time_*) re-run launches on the live decode state (h, the KV slot
+    // of the last step, the attention scratch): t5g_decode refuses to continue from it until a
+    // t5g_sampler_setup (after a fresh prefill) starts a new call
+    bool decode_state_invalid = false;
     int64_t xl_launches = 0;   // xlayer.hip launches issued (captured ones counted once, at capture)
 };
 
@@ -1528,6 +1532,20 @@ extern "C" int t5g_prefill(t5g_engine* e, int32_t B, int32_t ntok, const int32_t
     const t5g_config& c = e->c;
     if (B > c.max_batch || ntok > B * c.max_audio) return T5G_ECAPACITY;
     hipStream_t st = (hipStream_t)stream;
+    if (e->audio_max > 0) {
+        // t5g_engine_set_audio_max is a host hint that sizes the decode attention grids (and
+        // the stop rule): a stale hint below a row's length would silently drop that row's
+        // keys and leave the flash tickets counting, so check it once per call
+        std::vector<int> lens(B);
+        HIPCHK(hipMemcpyAsync(lens.data(), kv_len, B * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int b = 0; b < B; ++b)
+            if (lens[b] > e->audio_max) {
+                fprintf(stderr, "[t5gtts] prefill length %d of row %d > t5g_engine_set_audio_max hint %d\n", lens[b],
+                        b, e->audio_max);
+                return T5G_EINVAL;
+            }
+    }
     e->B = B;
     HIPCHK(hipMemcpyAsync(e->kv_len, kv_len, B * sizeof(int), hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemcpyAsync(e->last_rows, last_index, B * sizeof(int), hipMemcpyDeviceToDevice, st));
@@ -1556,8 +1574,18 @@ extern "C" int t5g_sampler_setup(t5g_engine* e, int32_t B, const t5g_sampler_row
     if (n_top_k_list > 4096 || n_silence > 4096) return T5G_ECAPACITY;
     static_assert(sizeof(t5g_sampler_row) == sizeof(SamplerRow), "row layout");
     static_assert(sizeof(t5g_sampler_state) == sizeof(SamplerState), "state layout");
+    // the decode grids cover the call's key bound (t5g_engine_set_audio_max); a row already
+    // past it would append keys no launch reads
+    const int bound = e->audio_max > 0 ? e->audio_max : e->c.max_audio;
+    for (int b = 0; b < B; ++b)
+        if (init[b].current_length < 0 || init[b].current_length > bound) {
+            fprintf(stderr, "[t5gtts] row %d current_length %d outside the call's key bound %d\n", b,
+                    init[b].current_length, bound);
+            return T5G_EINVAL;
+        }
     hipStream_t st = (hipStream_t)stream;
     e->B = B;
+    e->decode_state_invalid = false;
     HIPCHK(hipMemcpyAsync(e->rows, rows, B * sizeof(SamplerRow), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(e->state, init, B * sizeof(SamplerState), hipMemcpyHostToDevice, st));
     if (n_top_k_list > 0)
@@ -1648,6 +1676,10 @@ static int decode_iter(t5g_engine* e, hipStream_t st) {
 
 extern "C" int t5g_decode(t5g_engine* e, int32_t n_steps, int32_t use_graph, void* stream) {
     if (!e || e->B <= 0) return T5G_EINVAL;
+    if (e->decode_state_invalid) {
+        fprintf(stderr, "[t5gtts] t5g_decode after a timing hook: start a new call (t5g_prefill + t5g_sampler_setup)\n");
+        return T5G_EINVAL;
+    }
     hipStream_t st = (hipStream_t)stream;
     if (!use_graph) {
         for (int i = 0; i < n_steps; ++i) {
@@ -1704,6 +1736,9 @@ static int check_handoff(t5g_engine* e, hipStream_t st) {
     if (!tmo) return T5G_OK;
     fprintf(stderr, "[t5gtts] fused decode hand-off timed out (code %u)\n", tmo);
     hipMemsetAsync(e->fsync, 0, fsync_words(e->c) * sizeof(unsigned), st);
+    // the flash / stage-S arrival tickets are zero between launches; a launch that gave up
+    // (or left chunks uncovered) can leave them counting, so they are cleared with the counters
+    hipMemsetAsync(e->aftick, 0, (size_t)e->c.max_batch * e->c.n_kv_heads * sizeof(unsigned), st);
     hipStreamSynchronize(st);
     return T5G_EHANDOFF;
 }
@@ -1939,6 +1974,7 @@ extern "C" int t5g_time_gemm(const void* X, int32_t ldx, int32_t M, const void* 
 
 extern "C" int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, float* avg_us) {
     if (!e || iters <= 0 || !avg_us || e->B <= 0) return T5G_EINVAL;
+    e->decode_state_invalid = true;
     hipStream_t st = (hipStream_t)stream;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
@@ -1965,6 +2001,7 @@ extern "C" int t5g_time_decode_step(t5g_engine* e, int32_t iters, void* stream, 
 // Average microseconds per layer (six launches) in *avg_us.
 extern "C" int t5g_time_exact_linears(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us) {
     if (!e || iters <= 0 || !avg_us || B <= 0 || B > e->c.max_batch || !e->exact || !e->xmm_ready) return T5G_EINVAL;
+    e->decode_state_invalid = true;
     const t5g_config& c = e->c;
     const int d = c.hidden, f = c.intermediate;
     hipStream_t st = (hipStream_t)stream;
@@ -2006,6 +2043,7 @@ extern "C" int t5g_time_exact_linears(t5g_engine* e, int32_t B, int32_t iters, v
 extern "C" int t5g_time_xlayer(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us) {
     if (!e || iters <= 0 || !avg_us || B <= 0 || B > e->c.max_batch || !e->exact || !e->xmm_ready) return T5G_EINVAL;
     if (!xlayer_usable(e, B)) return T5G_EUNSUPPORTED;
+    e->decode_state_invalid = true;
     hipStream_t st = (hipStream_t)stream;
     const int L = e->c.n_dec_layers;
     const int n = (iters + L - 1) / L * L;
@@ -2034,6 +2072,7 @@ extern "C" int t5g_time_xlayer(t5g_engine* e, int32_t B, int32_t iters, void* st
 // launch streams its weights from HBM (2.2 GB of gate/up + down > the 256 MiB Infinity Cache)
 extern "C" int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us) {
     if (!e || iters <= 0 || !avg_us || B <= 0 || B > e->c.max_batch || e->c.n_dec_layers < 2) return T5G_EINVAL;
+    e->decode_state_invalid = true;
     hipStream_t st = (hipStream_t)stream;
     const int L = e->c.n_dec_layers;
     // whole rotations over the layers, as a decode step runs them: layer l's launch finds
@@ -2070,6 +2109,7 @@ extern "C" int t5g_time_decode_mlp(t5g_engine* e, int32_t B, int32_t iters, void
 extern "C" int t5g_time_decode_layer(t5g_engine* e, int32_t B, int32_t iters, void* stream, float* avg_us,
                                      float* keys) {
     if (!e || iters <= 0 || !avg_us || !keys || B <= 0 || B > e->c.max_batch || e->c.n_dec_layers < 2) return T5G_EINVAL;
+    e->decode_state_invalid = true;
     hipStream_t st = (hipStream_t)stream;
     const t5g_config& c = e->c;
     const int L = c.n_dec_layers;

@@ -477,7 +477,7 @@ class T5GemmaTTSEngine:
         _lib.check(L.t5g_engine_set_text_max(self.h, max(tlen)), "set_text_max")
         # the call's key bound (every row's prompt + budget, in 512-key steps so repeated
         # calls keep the captured graphs): the decode attention grids cover it, not max_audio
-        key_bound = min(self.max_audio, -(-(max(a + b for a, b in zip(alen, budgets)) + 1) // 512) * 512)
+        key_bound = min(self.max_audio, -(-(max(a + b for a, b in zip(alen, budgets)) + 1) // 64) * 64)
         _lib.check(L.t5g_engine_set_audio_max(self.h, key_bound), "set_audio_max")
         if parity:
             # the reference's multinomial draws, one stream step per sampler call (up to the row

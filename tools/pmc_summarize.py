@@ -99,6 +99,14 @@ def main(op, out_dir, dst):
            "correction": "bytes = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (gfx950: FETCH_SIZE is half of 16B/lane reads)",
            "hbm_bytes_per_call": int(hbm), "algorithmic_bytes_per_call": int(alg),
            "traffic_over_algorithmic": round(hbm / alg, 4)}
+    # the digest of the kernel sources measured (bench.py quotes this traffic only while the
+    # tree's sources still hash the same)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import t5gemma_tts_amd  # noqa: F401
+    from t5gemma_tts_amd._lib import PMC_SOURCES, kernel_source_digest
+    if op in PMC_SOURCES:
+        res["source_digest"] = kernel_source_digest(op)
+        res["source_files"] = PMC_SOURCES[op]
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
