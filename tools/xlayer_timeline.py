@@ -11,7 +11,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["T5G_LIB"] = os.path.join(REPO, "t5gemma-tts_amd", "lib", "libt5gtts_dbg.so")
+os.environ.setdefault("T5G_LIB", os.path.join(REPO, "t5gemma-tts_amd", "lib", "libt5gtts_dbg.so"))
 sys.path.insert(0, REPO)
 
 import numpy as np  # noqa: E402
