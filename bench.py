@@ -46,6 +46,9 @@ WORKLOADS = {
     "c3": (8, 60, 151, False, 2),
     "c4": (8, 36, 0, False, 3),
     "c5": (32, 60, 151, True, 4),
+    # C3 with a 10 s voice prompt (500 codes + y_sep): rows end at ~1 253 keys, past the
+    # decode attention stage's one-pass limits of round 5
+    "c3p10": (8, 60, 501, False, 2),
 }
 T_X, T_P = 60, 151          # c3 (kept for tools that import them)
 B_PER_GPU = 8
@@ -272,6 +275,7 @@ def main():
         run_sharded(rows, costs, lambda sh: generate(sh, i), comm_dev, max_per_rank=B, max_len=n_tok_row + 8)
         return gen_tokens[0] - before
 
+    s_before = eng.attn_in_block_launches()
     for i in range(args.warmup):
         step(i)
     if dist is not None:
@@ -286,6 +290,8 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
+    s_launches = eng.attn_in_block_launches() - s_before
+    s_mode = eng.attn_in_block_mode()
     tot = torch.tensor([float(tokens), dt, float(audio_frames[0])], dtype=torch.float64, device=comm_dev)
     if dist is not None:
         t_sum = tot[[0, 2]].clone()
@@ -381,7 +387,7 @@ def main():
             if B <= 16:   # the step runs the whole post-self-attention block in one launch
                 us_k, kname = us.value, _lib.FUSED_BLOCK_KERNEL
                 alg_bytes = _lib.fused_block_bytes(B, wl_tx, d, f, self_keys=keys.value)
-                if keys.value > 0 and args.attn_in_block == 1:
+                if keys.value > 0 and s_mode == 1:
                     kname = "fused_block_kernel<1> (the layer's self attention in front of its o-projection)"
                     pmc, pmc_op = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s_front.json"), "fused_block_s"
                 elif keys.value > 0:
@@ -440,7 +446,8 @@ def main():
             }
         else:
             prompt = f"T_p {wl_tp} (voice clone)" if wl_tp else "no prompt"
-            desc = {"c2": "C2 single utterance", "c3": "C3 voice-clone", "c4": "C4 text-only"}[args.workload]
+            desc = {"c2": "C2 single utterance", "c3": "C3 voice-clone", "c4": "C4 text-only",
+                    "c3p10": "C3 voice-clone with a 10 s prompt"}[args.workload]
             mode = ("parity mode (drop-in default: exact-order kernels, reference RNG stream, host sync per "
                     "step, EOS accepted)" if args.parity else
                     "top-k 30/top-p 0.9/T 0.8" + (", EOS accepted when sampled" if args.natural_eos else ""))
@@ -460,6 +467,11 @@ def main():
                            "parallelism": f"dp{world} (utterance shards)"},
                 "rtf_audio_s_per_wall_s": round(value / 50.0, 3),
                 "roofline": roof, "cpu_baseline": cpu,
+                # persistent layer launches issued with the decode self attention inside (stage
+                # S) during warm-up + timed steps -- graph-replayed steps count once, at capture;
+                # 0: every layer's attention ran as its own launch
+                "attn_in_block_launches": int(s_launches),
+                "attn_in_block_mode": s_mode,   # 2 tail, 1 front (several passes past 3 slots / CU), 0 own launch
             }
             if parity_line is not None:
                 if cpu is not None:

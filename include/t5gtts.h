@@ -312,13 +312,16 @@ int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable);
  * before the N3 wait -- followed by that layer's o-projection, whose slabs the next launch's
  * norm reads (layer 0's attention and o-projection stay the step's own launches). Every mode
  * is bitwise equal to mode 0. A call whose rows x kv heads x chunks exceed 2 chunk slots per
- * worker takes mode 1 instead of 2; past 3 per workgroup, or rows past 1 024 keys, the
- * separate launch.
+ * worker takes mode 1 instead of 2; mode 1 runs up to 2 passes of 3 slots per workgroup (8
+ * rows: rows of up to 3 072 keys); past that the separate launch.
  * Replaces the reference's per-layer self-attention call inside PMDecoderLayer
  * (hf_export/modeling_t5gemma_voice.py:256-323, [tf] modeling_t5gemma.py:264-304).
- * t5g_engine_attn_in_block_launches: layer launches issued with S (captured ones once). */
+ * t5g_engine_attn_in_block_launches: layer launches issued with S (captured ones once).
+ * t5g_engine_attn_in_block_mode: where the last decode step ran S (2, 1, or 0 = its own
+ * launch). */
 int t5g_engine_set_attn_in_block(t5g_engine* e, int32_t mode);
 int t5g_engine_attn_in_block_launches(t5g_engine* e, int64_t* n);
+int t5g_engine_attn_in_block_mode(t5g_engine* e, int32_t* mode);
 
 /* Sampler launch shape: 0 (default) the 16-slice multi-block kernel, falling back per row to
  * the single-block kernel when a row's top-k / survivor set exceeds it; 1 the single-block

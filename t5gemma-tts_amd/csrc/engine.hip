@@ -93,6 +93,7 @@ struct t5g_engine {
     // t5g_engine_set_attn_in_block): no attention launch of its own between the layers
     int attn_in_block = 2;   // 0 own launch, 1 stage S in front of O1, 2 at the end of the previous launch
     int64_t s_launches = 0;   // persistent layer launches run with stage S (tests)
+    int s_mode_used = 0;      // the last decode pass's stage-S placement: 2 tail, 1 front, 0 none
     float* afpart = nullptr;    // [B][Hkv][nsplit][G][D]
     float* afstat = nullptr;    // [B][Hkv][nsplit][G][2]
     unsigned* aftick = nullptr; // [B][Hkv]
@@ -1295,6 +1296,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
             tail = fused_block_tail(e, M, l, fa);
         }
     }
+    if (decode) e->s_mode_used = tail ? 2 : 0;
     for (int l = 0; l < c.n_dec_layers; ++l) {
         const t5g_layer_weights& L = e->dec[l];
         if (l == 0) {
@@ -1358,6 +1360,7 @@ static int decoder_pass(t5g_engine* e, int M, const int* ids, const int* tok_row
                 if (fused_mlp_check(fa) == 0 && fused_block_self(e, M, l, fa)) {
                     RC(fused_mlp(fa, st));
                     ++e->s_launches;
+                    e->s_mode_used = 1;
                     qkv_done = l != c.n_dec_layers - 1;
                     continue;
                 }
@@ -1775,6 +1778,12 @@ extern "C" int t5g_engine_set_attn_in_block(t5g_engine* e, int32_t mode) {
         e->attn_in_block = mode;
         drop_graphs(e);   // captured launches follow the flag
     }
+    return T5G_OK;
+}
+
+extern "C" int t5g_engine_attn_in_block_mode(t5g_engine* e, int32_t* mode) {
+    if (!e || !mode) return T5G_EINVAL;
+    *mode = e->s_mode_used;
     return T5G_OK;
 }
 

@@ -575,7 +575,7 @@ constexpr size_t FB_LDS = FB_GU_OFF + (size_t)FB_GU_KB * 1024;
 // finishes and every (row, kv head) publishes exactly once.
 constexpr int FS_G = 2, FS_D = 256, FS_CH = 64, FS_LPK = FS_D / 8, FS_KPW = 64 / FS_LPK, FS_KPB = FS_KPW * 4,
               FS_NIT = FS_CH / FS_KPB, FS_GRP = FM_NW / 4, FS_MAXROWS = 32,
-              FS_CMAX = 16;   // chunks per row (1 024 keys): the combine reads its records in one batch
+              FS_MAXPASS = 2;   // front: passes of 3 chunk slots per workgroup (8 rows: <= 48 chunks)
 static_assert(FS_LPK == 32, "the P.V lanes of a key fold in one xor-32 step");
 struct FbSelfGrp {
     f32x4 ored[4][FS_G][FS_LPK][2];
@@ -630,7 +630,8 @@ __device__ __forceinline__ void fb_lds_barrier() { asm volatile("s_waitcnt lgkmc
 // first `nwg` workgroups' groups 0-1 only (group 2's waves poll), and `len_in` is the row
 // length the caller requested at launch start. Front: `mid` is empty, len_in < 0.
 template <bool TAIL, typename Mid>
-__device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& sl, Mid&& mid, int nwg, int len_in) {
+__device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& sl, Mid&& mid, int nwg, int len_in,
+                                             int pass = 0) {
     constexpr int G = FS_G, D = FS_D, LPK = FS_LPK, KPW = FS_KPW, KPB = FS_KPB, NIT = FS_NIT;
     const int tq = (int)threadIdx.x, wave = tq >> 6, lane = tq & 63;
     const int grp = wave >> 2, gw = wave & 3, gt = tq & 255;
@@ -641,8 +642,8 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
     // kv head on workgroup c % nb, group c / nb -- known before the row lengths, so the q|k|v
     // slabs and the RoPE row are requested with the row length; chunk-major, so the live
     // chunks (sp < the row's count) fill group 0 of every workgroup before any group 1
-    // (fused_mlp_launch: slots <= 3 nb)
-    const int cidx = (int)blockIdx.x + grp * nwg;
+    // (in front, a call with more slots than 3 nb runs several passes: slots 3 nb p ..)
+    const int cidx = (int)blockIdx.x + (grp + FS_GRP * pass) * nwg;
     const bool has_s = (int)blockIdx.x < nwg && cidx < M * Hkv * a.s_nsplit;
     const int sp = has_s ? cidx / (M * Hkv) : 0, rk = has_s ? cidx - sp * (M * Hkv) : 0;
     const int m = rk / Hkv, kvh = rk - m * Hkv;
@@ -925,8 +926,7 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
     const bool comb = has_c && !single && L.last != 0;
     const bool pub = has_c && (single || comb);
     {
-        constexpr int FB = FS_CMAX, NOUT = G * D / 4;
-        static_assert(FS_CMAX == 16, "attn_flash_finish's combine batch");
+        constexpr int FB = 16, NOUT = G * D / 4;   // attn_flash_finish's combine batch
         const long rec = ((long)m * Hkv + kvh) * a.s_nsplit;   // chunk records of this (row, kv head)
         const int ot = gt - 64 * G;
         const bool outer = comb && ot >= 0 && ot < NOUT;
@@ -943,8 +943,7 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
         f32x4 pv[FB];
         if (outer) pload(pv, 0);
         if (comb && gw < G) {
-            constexpr int CPL = 1;   // nch <= 64: the flash kernel's lanes past nch add -inf / +0 only
-            static_assert(FS_CMAX <= 64, "one chunk record per lane");
+            constexpr int CPL = DEC_MAX_CHUNKS / 64;   // lane owns chunks lane + 64 i (attn_flash_finish)
             const int g = gw;
             float mc[CPL], lc[CPL];
 #pragma unroll
@@ -971,12 +970,15 @@ __device__ __forceinline__ void fb_self_attn(const FusedMlpArgs& a, FbSelfLds& s
             if (lane == 0) L.lsum[g] = Ls;
         }
         fb_lds_barrier();
-        if (outer) {   // nch <= FB (fused_mlp_launch): one batch, attn_flash_finish's first
+        if (outer) {   // attn_flash_finish's batches of 16 records, in order
             f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+            for (int cb = 0; cb < nch; cb += FB) {
+                if (cb > 0) pload(pv, cb);
 #pragma unroll
-            for (int k = 0; k < FB; ++k) {
-                const float w = k < nch ? L.wts[og][k] : 0.f;
-                acc += w * pv[k];
+                for (int k = 0; k < FB; ++k) {
+                    const float w = cb + k < nch ? L.wts[og][cb + k] : 0.f;
+                    acc += w * pv[k];
+                }
             }
             const float inv = 1.0f / L.lsum[og];
             const u32x2_t ow = {pack2(acc[0] * inv, acc[1] * inv), pack2(acc[2] * inv, acc[3] * inv)};
@@ -1020,7 +1022,10 @@ __global__ __launch_bounds__(FM_NW * 64) void fused_block_kernel(FusedMlpArgs a)
     // ---- S: the layer's self-attention on every workgroup (O1 waits for its heads)
     if constexpr (SELF) {
         FS_TS(0);
-        fb_self_attn<false>(a, *(FbSelfLds*)smem, [] {}, nb, -1);
+        // a call with more chunk slots than 3 per workgroup: a second pass of 3 nb slots
+        // (uniform; two inlined copies -- a loop keeps the stage's registers live across it)
+        fb_self_attn<false>(a, *(FbSelfLds*)smem, [] {}, nb, -1, 0);
+        if (M * a.Hkv * a.s_nsplit > FS_GRP * nb) fb_self_attn<false>(a, *(FbSelfLds*)smem, [] {}, nb, -1, 1);
         if (FS_DBG_VAR == 4) {   // timing variant: the stage again, warm (points overwritten)
             FS_TS(13);
             fb_self_attn<false>(a, *(FbSelfLds*)smem, [] {}, nb, -1);
@@ -1439,8 +1444,7 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
              a.Hkv != 4 || a.D != FS_D || a.M > FS_MAXROWS || a.qkv_dim != a.q_dim + 2 * a.Hkv * a.D || a.s_cap < 1 ||
              a.s_nsplit < 1 || a.s_nsplit > DEC_MAX_CHUNKS || a.s_nsplit > (a.s_cap + FS_CH - 1) / FS_CH ||
              a.window < 0 || (long)a.M * a.Hkv * a.s_nsplit * FS_G * FS_D * 4 > 0x7fff0000L ||
-             a.M * a.Hkv * a.s_nsplit > FS_GRP * nb ||   // <= 3 chunks per workgroup
-             a.s_nsplit > FS_CMAX))                        // one combine batch
+             a.M * a.Hkv * a.s_nsplit > FS_GRP * nb * FS_MAXPASS))   // <= 3 chunks per workgroup and pass
             return -1;
         if (a.Wqkv && (!a.qkv_out || a.NGqkv * 16 != a.qkv_dim)) return -1;
         a.norm_b0 = nb - a.M;
@@ -1457,7 +1461,7 @@ static int fused_mlp_launch(const FusedMlpArgs& a_in, hipStream_t st, bool launc
             (a.self_attn || a.Wo1 || !a.Wqkv || !a.Wo1n || !a.o1n || !a.att_self || a.qkv_in != a.qkv_out ||
              !a.sk || !a.sv || !a.kv_len || !a.fpart || !a.fstat || !a.fticket || a.Hq != 8 || a.Hkv != 4 ||
              a.D != FS_D || a.M > FS_MAXROWS || a.qkv_dim != a.q_dim + 2 * a.Hkv * a.D || a.s_cap < 1 ||
-             a.s_nsplit < 1 || a.s_nsplit > FS_CMAX || a.s_nsplit > (a.s_cap + FS_CH - 1) / FS_CH || a.window < 0 ||
+             a.s_nsplit < 1 || a.s_nsplit > DEC_MAX_CHUNKS || a.s_nsplit > (a.s_cap + FS_CH - 1) / FS_CH || a.window < 0 ||
              a.M * a.Hkv * a.s_nsplit > 2 * (nb - a.M) || (long)a.M * a.Hkv * a.s_nsplit * FS_G * FS_D * 4 > 0x7fff0000L))
             return -1;
         const int sv = a.self_tail ? 2 : a.self_attn ? 1 : 0;

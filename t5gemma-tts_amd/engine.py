@@ -243,6 +243,13 @@ class T5GemmaTTSEngine:
         m = 2 if mode is True else 0 if mode is False else int(mode)
         _lib.check(self.L.t5g_engine_set_attn_in_block(self.h, m), "set_attn_in_block")
 
+    def attn_in_block_mode(self) -> int:
+        """Where the last fast-path decode step ran the self attention: 2 at the end of the
+        previous layer's launch, 1 in front of the layer's o-projection, 0 its own launch."""
+        m = C.c_int32()
+        _lib.check(self.L.t5g_engine_attn_in_block_mode(self.h, C.byref(m)), "attn_in_block_mode")
+        return m.value
+
     def attn_in_block_launches(self) -> int:
         """Fast-path persistent layer launches issued with the self attention inside (test /
         bench hook; a launch captured into a graph counts once)."""
@@ -475,8 +482,9 @@ class T5GemmaTTSEngine:
         d_alen, d_last = torch.tensor(alen, **i32), torch.tensor(last, **i32)
         L = self.L
         _lib.check(L.t5g_engine_set_text_max(self.h, max(tlen)), "set_text_max")
-        # the call's key bound (every row's prompt + budget, in 512-key steps so repeated
-        # calls keep the captured graphs): the decode attention grids cover it, not max_audio
+        # the call's key bound (every row's prompt + budget, rounded up to a 64-key flash chunk;
+        # calls with the same bound keep the captured graphs): the decode attention grids
+        # cover it, not max_audio
         key_bound = min(self.max_audio, -(-(max(a + b for a, b in zip(alen, budgets)) + 1) // 64) * 64)
         _lib.check(L.t5g_engine_set_audio_max(self.h, key_bound), "set_audio_max")
         if parity:

@@ -108,17 +108,17 @@ def test_attention_in_block_sliding_window(mode):
     _assert_same(fon, foff, 6, "window graph")
 
 
-def test_attention_in_block_falls_back_past_one_task_per_workgroup():
-    """16 rows of up to ~1 100 keys: 16 x 4 kv heads x 18 chunks = 1 152 chunks > 3 per
-    workgroup (and rows past the 1 024 keys one combine batch reads), so the call keeps the
-    separate flash launch -- the same bits either way."""
+def test_attention_in_block_falls_back_past_two_passes():
+    """16 rows of up to ~1 650 keys: 16 x 4 kv heads x 26 chunks = 1 664 chunk slots > two
+    passes of 3 per workgroup (1 536), so the call keeps the separate flash launch -- the same
+    bits either way."""
     _need_gpu()
     from t5gemma_tts_amd.engine import SamplingParams
-    cfg, eng = _engine(16, 1152)
+    cfg, eng = _engine(16, 1700)
     from t5gemma_tts_amd.engine import Utterance
     rng = np.random.default_rng(3)
     utts = [Utterance(x=rng.integers(3, 4000, size=20).tolist(),
-                      y=rng.integers(0, 65536, size=1080).tolist() + [cfg.y_sep_token], tgt_y_len=1081 + 10)
+                      y=rng.integers(0, 65536, size=1630).tolist() + [cfg.y_sep_token], tgt_y_len=1631 + 10)
             for _ in range(16)]
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
     seeds = list(range(16))
@@ -149,3 +149,27 @@ def test_tail_mode_falls_back_to_front_past_two_slots_per_worker():
     assert n_on > 0
     _assert_same(on, off, 16, "front fallback")
     _assert_same(fon, foff, 16, "front fallback graph")
+
+
+@pytest.mark.parametrize("tp,max_audio", [(1240, 1300), (2480, 2560)])
+def test_attention_in_block_long_rows(tp, max_audio):
+    """Rows past 1 024 keys in the launch (round 6): 8 rows of ~1 250 keys (20 chunks: the
+    combine reads its records in two batches of 16, as the flash launch does; one pass of 3
+    slots per workgroup, front mode) and of ~2 500 keys (40 chunks: two passes of 3 nb slots).
+    Bitwise equal to the separate flash launch, stage S in every decode launch. Reference: the
+    reference serves 100 s prompts (inference_commandline_hf.py:91, 181)."""
+    _need_gpu()
+    from t5gemma_tts_amd.engine import SamplingParams, Utterance
+    cfg, eng = _engine(8, max_audio)
+    rng = np.random.default_rng(tp)
+    utts = [Utterance(x=rng.integers(3, 4000, size=20).tolist(),
+                      y=rng.integers(0, 65536, size=tp - 8 * i).tolist() + [cfg.y_sep_token],
+                      tgt_y_len=tp - 8 * i + 1 + 12)
+            for i in range(8)]
+    p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
+    seeds = list(range(8))
+    on, fon, n_on = _run(eng, utts, p, seeds, 2)
+    off, foff, n_off = _run(eng, utts, p, seeds, 0)
+    assert n_off == 0 and n_on >= 2 * 12   # stage S ran in the decode launches
+    _assert_same(on, off, 8, "long")
+    _assert_same(fon, foff, 8, "long graph")
