@@ -240,6 +240,7 @@ def main():
     speed_lines = []
     gen_tokens = [0]
     audio_frames = [0]
+    codec_s = [0.0]   # wall time inside XCodec2Decoder.decode (C5), the rest of a step is generate()
 
     def generate(shard, i, parity=None):
         parity = args.parity if parity is None else parity
@@ -264,7 +265,11 @@ def main():
             codes = torch.zeros(len(frames), max(lens), dtype=torch.long)
             for b, f in enumerate(frames):
                 codes[b, :f.numel()] = f
+            torch.cuda.synchronize(dev)
+            t_c = time.perf_counter()
             codec.decode(codes, lens=lens)
+            torch.cuda.synchronize(dev)
+            codec_s[0] += time.perf_counter() - t_c
             audio_frames[0] += sum(lens)
         return [g.tolist() for g in out["gen"]]
 
@@ -282,6 +287,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     audio_frames[0] = 0
+    codec_s[0] = 0.0
     t0 = time.perf_counter()
     tokens = 0
     for i in range(args.steps):
@@ -420,6 +426,37 @@ def main():
         roof["decode_step_us"] = round(step_us.value, 1)
         roof["decode_step_GBps"] = round(decode_weight_bytes(cfg) / (step_us.value * 1e-6) / 1e9, 1)
 
+    # ---- C5: roofline of the codec's dominant kernel, gemm_f32_kernel (89 % of the decode's
+    # device time, profiles/r06_c5_kernel_stats.csv), every GEMM launch of whole B x 751-frame
+    # decodes between its own HIP events on the launching stream; 2 M N K flops against the
+    # f32 MFMA peak (157.3 TFLOP/s: v_mfma_f32_32x32x2_f32 runs at the f32 vector rate)
+    if rank == 0 and args.e2e:
+        import ctypes as C
+        Tc = n_tok_row
+        g = torch.Generator(device="cpu").manual_seed(7)
+        codes_c = torch.randint(0, codec.cfg.codebook_size, (B, Tc), generator=g, dtype=torch.int32).to(dev)
+        wav_c = torch.empty(B, Tc * codec.cfg.hop_length, device=dev)
+        st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        g_us, g_fl, g_n, d_us = C.c_float(), C.c_double(), C.c_int32(), C.c_float()
+        rc = codec.L.xc2_time_gemms(codec.h, C.c_void_p(codes_c.data_ptr()), B, Tc, C.c_void_p(wav_c.data_ptr()), 5,
+                                    st, C.byref(g_us), C.byref(g_fl), C.byref(g_n))
+        if rc != 0:
+            raise RuntimeError(f"xc2_time_gemms failed: {rc}")
+        rc = codec.L.xc2_time_decode(codec.h, C.c_void_p(codes_c.data_ptr()), B, Tc, C.c_void_p(wav_c.data_ptr()), 5,
+                                     st, C.byref(d_us))
+        if rc != 0:
+            raise RuntimeError(f"xc2_time_decode failed: {rc}")
+        ach = g_fl.value / (g_us.value * 1e-6) / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s",
+                "frac": round(ach / 157.3, 4), "traffic": None,
+                "traffic_note": "compute-bound kernel: MFMA busy from the SQ_VALU_MFMA_BUSY_CYCLES pass "
+                                "(profiles/r06_pmc_c5_codec.csv), HBM bytes not priced",
+                "kernel": "gemm_f32_kernel (XCodec2 decoder GEMMs: fc, conv k7 / k3 as halo GEMMs, q|k|v, o, "
+                          "fc1 + SiLU, fc2, head, iSTFT basis; 128 x 128 tiles, v_mfma_f32_32x32x2_f32)",
+                "frames": f"{B} x {Tc}", "flops_per_decode": g_fl.value, "gemm_launches_per_decode": g_n.value,
+                "gemm_us_per_decode": round(g_us.value, 1), "avg_us": round(g_us.value / max(1, g_n.value), 2),
+                "decode_us": round(d_us.value, 1), "gemm_share_of_decode": round(g_us.value / d_us.value, 4)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.e2e:
         r0 = rows[0]
@@ -443,6 +480,12 @@ def main():
                            "parallelism": f"dp{world} (utterance shards)"},
                 "audio_tokens_per_s": round(value, 2), "wall_s_per_audio_s": round(dt_max / audio_s, 5),
                 "samples_per_s": round(frames_all * hop / dt_max, 1),
+                # rank 0's split of a step: generate() vs XCodec2Decoder.decode (synchronised
+                # before and after the decode)
+                "generate_ms_per_step": round((dt - codec_s[0]) / args.steps * 1e3, 2),
+                "codec_decode_ms_per_step": round(codec_s[0] / args.steps * 1e3, 2),
+                "codec_share": round(codec_s[0] / dt, 4),
+                "roofline": roof,
             }
         else:
             prompt = f"T_p {wl_tp} (voice clone)" if wl_tp else "no prompt"

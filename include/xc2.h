@@ -98,6 +98,11 @@ int xc2_gemm(const float* X_dev, int32_t ldx, int32_t M, const float* W_dev, int
              const float* bias_dev, float* Y_dev, int32_t ldy, int32_t epi, void* stream);
 int xc2_time_decode(xc2_codec* c, const int32_t* codes_dev, int32_t B, int32_t T, float* wav_dev,
                     int32_t iters, void* stream, float* avg_us);
+/* gemm_f32_kernel alone inside `iters` (<= 64) whole decodes of B x T frames, each GEMM launch
+ * between its own event pair: *gemm_us = GEMM device time per decode, *flops = 2 M N K per
+ * decode, *launches = GEMM launches per decode (the codec's roofline leg in bench.py --e2e). */
+int xc2_time_gemms(xc2_codec* c, const int32_t* codes_dev, int32_t B, int32_t T, float* wav_dev,
+                   int32_t iters, void* stream, float* gemm_us, double* flops, int32_t* launches);
 
 
 /* ===================================================================================

@@ -43,25 +43,32 @@ BF16 = torch.bfloat16
 # ----------------------------------------------------------------------------
 # backbone primitives ([tf] modeling_t5gemma.py)
 # ----------------------------------------------------------------------------
+def _acc(dt: torch.dtype) -> torch.dtype:
+    """The type the reference's fp32 steps run in: fp32, or fp64 for the fp64 restatement."""
+    return torch.float64 if dt == torch.float64 else torch.float32
+
+
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
     """T5GemmaRMSNorm ([tf] :61-78): fp32 normalise, scale by (1 + w), cast back."""
-    xf = x.float()
+    ct = _acc(x.dtype)
+    xf = x.to(ct)
     out = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
-    out = out * (1.0 + w.float())
+    out = out * (1.0 + w.to(ct))
     return out.type_as(x)
 
 
-def inv_freq_table(head_dim: int, theta: float) -> torch.Tensor:
+def inv_freq_table(head_dim: int, theta: float, dtype=torch.float) -> torch.Tensor:
     """Default RoPE inverse frequencies ([tf] :114-137)."""
-    return 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float) / head_dim))
+    return 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=dtype) / head_dim))
 
 
 def rope_cos_sin(inv_freq: torch.Tensor, pos: torch.Tensor, dtype=BF16) -> Tuple[torch.Tensor, torch.Tensor]:
     """T5GemmaRotaryEmbedding.forward ([tf] :138-151) on float positions [B, T]."""
     B = pos.shape[0]
-    inv = inv_freq[None, :, None].float().expand(B, -1, 1)
-    p = pos[:, None, :].float()
-    freqs = (inv.float() @ p.float()).transpose(1, 2)
+    ct = _acc(dtype)
+    inv = inv_freq[None, :, None].to(ct).expand(B, -1, 1)
+    p = pos[:, None, :].to(ct)
+    freqs = (inv @ p).transpose(1, 2)
     emb = torch.cat((freqs, freqs), dim=-1)
     cos = emb.cos() * 1.0
     sin = emb.sin() * 1.0
@@ -123,7 +130,7 @@ def attention(q, k, v, *, scale: float, softcap: float, n_rep: int,
             add = torch.zeros(mask.shape, dtype=w.dtype)
             add = add.masked_fill(~mask, torch.finfo(w.dtype).min)
             w = w + add
-        w = F.softmax(w, dim=-1, dtype=torch.float32).to(q.dtype)
+        w = F.softmax(w, dim=-1, dtype=_acc(q.dtype)).to(q.dtype)
         o = torch.matmul(w, v)
     return o.transpose(1, 2).reshape(B, Tq, H * D)
 
@@ -251,17 +258,21 @@ def sample_helper(logits: torch.Tensor, p: SamplerParams, st: RowState, noise: t
 # the model
 # ----------------------------------------------------------------------------
 class T5GemmaTTSOracle:
-    """Encoder / decoder / head of T5Gemma-TTS on CPU in bf16 (reference numerics)."""
+    """Encoder / decoder / head of T5Gemma-TTS on CPU in bf16 (reference numerics).
 
-    def __init__(self, cfg, sd: Dict[str, torch.Tensor]):
+    ``dtype=torch.float64``: the same graph with every tensor and every fp32 step in fp64 --
+    the noise-floor yardstick of tests/test_gpu_noise_floor.py (not a reference run)."""
+
+    def __init__(self, cfg, sd: Dict[str, torch.Tensor], dtype: torch.dtype = BF16):
         self.cfg = cfg
         self.bb = cfg.backbone
-        self.w = {k: v.to(BF16).contiguous() for k, v in sd.items()}
-        self.inv_freq = inv_freq_table(self.bb.head_dim, self.bb.rope_theta)
+        self.dt = dtype
+        self.w = {k: v.to(dtype).contiguous() for k, v in sd.items()}
+        self.inv_freq = inv_freq_table(self.bb.head_dim, self.bb.rope_theta, _acc(dtype))
         self.n_rep = self.bb.num_attention_heads // self.bb.num_key_value_heads
         self.enc_types = self.bb.layer_types("encoder")
         self.dec_types = self.bb.layer_types("decoder")
-        self.normalizer = torch.tensor(self.bb.hidden_size ** 0.5, dtype=BF16)
+        self.normalizer = torch.tensor(self.bb.hidden_size ** 0.5, dtype=dtype)
 
     # -- helpers -----------------------------------------------------------
     def _lin(self, x, name, bias=None):
@@ -306,7 +317,7 @@ class T5GemmaTTSOracle:
         pos = self.encoder_positions(T, T)
         h = F.embedding(x_ids[None], self.w["backbone.model.encoder.embed_tokens.weight"])
         h = h * self.normalizer
-        cos, sin = rope_cos_sin(self.inv_freq, pos)
+        cos, sin = rope_cos_sin(self.inv_freq, pos, self.dt)
         eps = self.bb.rms_norm_eps
         W = self.bb.sliding_window
         for i, lt in enumerate(self.enc_types):
@@ -344,7 +355,7 @@ class T5GemmaTTSOracle:
         T = emb.shape[1]
         past = cache["len"]
         h = emb * self.normalizer
-        cos, sin = rope_cos_sin(self.inv_freq, pos)
+        cos, sin = rope_cos_sin(self.inv_freq, pos, self.dt)
         eps = self.bb.rms_norm_eps
         W = self.bb.sliding_window
         Hq, Hk = self.bb.num_attention_heads, self.bb.num_key_value_heads
@@ -387,7 +398,7 @@ class T5GemmaTTSOracle:
             if cache["ck"][i] is None:
                 ck = self._heads(self._lin(memory, f"{p}.cross_attn.k_proj.weight"), Hk)
                 if self.cfg.use_pm_rope:
-                    ec, es = rope_cos_sin(self.inv_freq, enc_pos)
+                    ec, es = rope_cos_sin(self.inv_freq, enc_pos, self.dt)
                     ck = apply_rope(ck, ec, es)
                 cv = self._heads(self._lin(memory, f"{p}.cross_attn.v_proj.weight"), Hk)
                 cache["ck"][i], cache["cv"][i] = ck, cv

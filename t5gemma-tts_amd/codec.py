@@ -177,6 +177,8 @@ XC2_SIGNATURES = {
                            C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]),
     "xc2_time_decode": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
                                   C.c_void_p, C.POINTER(C.c_float)]),
+    "xc2_time_gemms": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
+                                 C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
 }
 
 

@@ -25,6 +25,7 @@
 #include <string.h>
 
 #include "xc2.h"
+#include <vector>
 #include "xc2_common.h"
 
 namespace xc2 {
@@ -481,6 +482,38 @@ int xc2_time_decode(xc2_codec* c, const int32_t* codes, int32_t B, int32_t T, fl
     (void)hipEventDestroy(e1);
     *avg_us = ms * 1000.f / (float)iters;
     return rc;
+}
+
+// gemm_f32_kernel alone over whole decodes (the codec roofline, bench.py --e2e): each GEMM
+// launch of `iters` decodes between its own pair of events. *gemm_us = summed GEMM device
+// time per decode, *flops = 2 M N K summed over one decode's GEMMs, *launches per decode.
+int xc2_time_gemms(xc2_codec* c, const int32_t* codes, int32_t B, int32_t T, float* wav, int32_t iters,
+                   void* stream, float* gemm_us, double* flops, int32_t* launches) {
+    if (!c || !gemm_us || !flops || !launches || iters <= 0 || iters > 64) return -1;
+    hipStream_t st = (hipStream_t)stream;
+    XC2_TRY(xc2_decode(c, codes, nullptr, B, T, wav, st));   // warm
+    const int cap = 256 * iters;
+    std::vector<hipEvent_t> ev(2 * cap);
+    for (auto& e : ev)
+        if (hipEventCreate(&e) != hipSuccess) return -2;
+    GemmTimer t{ev.data(), cap, 0, 0.0};
+    g_gemm_timer = &t;
+    int rc = 0;
+    for (int i = 0; i < iters && !rc; ++i) rc = xc2_decode(c, codes, nullptr, B, T, wav, st);
+    g_gemm_timer = nullptr;
+    (void)hipStreamSynchronize(st);
+    double us = 0.0;
+    for (int i = 0; i < t.n; ++i) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]);
+        us += ms * 1000.0;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    if (rc) return rc;
+    *gemm_us = (float)(us / iters);
+    *flops = t.flops / iters;
+    *launches = t.n / iters;
+    return 0;
 }
 
 }  // extern "C"

@@ -171,11 +171,30 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
         }
 }
 
+// measurement only (xc2_time_gemms): when set, every GEMM launch is bracketed by a pair of
+// events from this pool and its 2 M N K flops are counted
+struct GemmTimer {
+    hipEvent_t* ev;   // 2 * cap events
+    int cap, n;
+    double flops;
+};
+static GemmTimer* g_gemm_timer = nullptr;
+
 static int gemm(const GemmArgs& a, hipStream_t st) {
     if (a.M <= 0 || a.N <= 0) return 0;
     if (a.K <= 0 || a.K % BK || a.lda % 4 || a.ldw % 4) return -1;
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    GemmTimer* t = g_gemm_timer;
+    if (t) {
+        if (t->n >= t->cap) return -3;
+        (void)hipEventRecord(t->ev[2 * t->n], st);
+    }
     hipLaunchKernelGGL(gemm_f32_kernel, dim3(tiles), dim3(256), 0, st, a);
+    if (t) {
+        (void)hipEventRecord(t->ev[2 * t->n + 1], st);
+        ++t->n;
+        t->flops += 2.0 * a.M * a.N * a.K;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -1,0 +1,117 @@
+"""Is the fast path's logit error at the reference's own bf16 noise floor?
+
+One C3 row (T5Gemma-TTS-2b-2b at full depth, 26 + 26 layers; T_x 60, T_p 151 voice clone)
+generated on the GPU with the FAST kernels (tolerance-parity path, the reference's RNG
+stream). The CPU oracle is then teacher-forced on that token history twice:
+
+* in fp64 (every tensor and every fp32 step of the graph in fp64: the yardstick), and
+* in bf16 (the reference's own CPU numerics: the parity path's logits are bitwise these).
+
+Per step: err = max |logits - fp64| / max |fp64| for the fast path and for the reference
+bf16 run; the report (gpurun_out/noise_floor.json) carries the max and mean over the steps
+of each, and how often the reference sampler, fed each path's logits and the same noise,
+picks the fp64 run's token. Reference: hf_export/modeling_t5gemma_voice.py:702-786 (the
+sampling step the logits feed), :565-862 (the generate loop)."""
+import copy
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+STEPS = 100
+RTOL = 0.03        # the fast path's tolerance (test_gpu_parity_full.py)
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _row(cfg, seed):
+    rng = np.random.default_rng(seed)
+    x = rng.integers(3, cfg.backbone.text_vocab_size - 1, size=60)
+    x[28] = cfg.x_sep_token
+    y = rng.integers(0, cfg.audio_vocab_size, size=150).tolist() + [cfg.y_sep_token]
+    return [int(v) for v in x], [int(v) for v in y]
+
+
+@pytest.mark.timeout(1500)
+def test_fast_path_error_vs_fp64_noise_floor():
+    _need_gpu()
+    from oracle.t5g_oracle import SamplerParams as OP
+    from oracle.t5g_oracle import T5GemmaTTSOracle, draw_noise, sample_helper
+    from t5gemma_tts_amd.config import config_2b2b
+    from t5gemma_tts_amd.engine import SamplingParams, T5GemmaTTSEngine, Utterance
+    from t5gemma_tts_amd.weights import synthetic_weights
+
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    cfg = config_2b2b()
+    sd = synthetic_weights(cfg, 1234)
+    x, y = _row(cfg, 20261018)
+    u = Utterance(x=x, y=y, tgt_y_len=len(y) + STEPS + 40)
+    p = dict(top_k=30, top_p=0.9, min_p=0.0, temperature=0.8, stop_repetition=3, silence_tokens=())
+    eng = T5GemmaTTSEngine(cfg, sd, device="cuda:0", max_batch=1, max_text=64, max_audio=len(y) + 1 + STEPS + 80,
+                           max_gen=STEPS + 80)
+    out = eng.generate([u], SamplingParams(**p), seeds=[777], parity=True, exact=False, record_logits=True)
+    toks = out["gen"][0].tolist()[:STEPS]
+    fast = [out["logits"][t][0].float().cpu() for t in range(len(toks))]
+    eng.close()
+    del eng, out
+    torch.cuda.empty_cache()
+
+    op = OP(**p)
+    o16 = T5GemmaTTSOracle(cfg, sd)
+    o64 = T5GemmaTTSOracle(cfg, sd, dtype=torch.float64)
+    del sd
+    c16 = o16.prepare(u.x, u.y, u.tgt_y_len)
+    c64 = o64.prepare(u.x, u.y, u.tgt_y_len)
+    gen = torch.Generator().manual_seed(777)
+    st = c16["state"]
+    c64["state"] = st   # one row state: positions follow the same history
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    progress = os.path.join(REPO, "gpurun_out", "noise_floor_progress.txt")
+    e_fast, e_ref, same_fast, same_ref, n = [], [], 0, 0, 0
+    for t, tok in enumerate(toks):
+        l16 = o16.step_logits(c16)
+        l64 = o64.step_logits(c64)
+        scale = l64.abs().max().item()
+        e_fast.append((fast[t].double() - l64).abs().max().item() / scale)
+        e_ref.append((l16.double() - l64).abs().max().item() / scale)
+        noise = draw_noise(gen, l16.shape[-1])
+        picks, states = [], []
+        for lg in (fast[t], l16.float(), l64.float()):
+            s = copy.deepcopy(st)
+            picks.append(sample_helper(lg.to(torch.bfloat16).clone(), op, s, noise, eos=cfg.eog_inference,
+                                       encodec_sr=cfg.encodec_sr, extra_cutoff=cfg.extra_cutoff)[0])
+            states.append(s)
+        assert picks[0] == tok, f"step {t}: reference sampler on the fast logits -> {picks[0]}, GPU {tok}"
+        same_fast += int(picks[0] == picks[2])
+        same_ref += int(picks[1] == picks[2])
+        n += 1
+        # the history is the fast path's: carry the state its pick left
+        st = states[0]
+        c16["state"] = c64["state"] = st
+        st.cur_num_gen += 1
+        st.current_length += 1
+        with open(progress, "a") as f:
+            f.write(f"step {t}: fast {e_fast[-1]:.5f} ref {e_ref[-1]:.5f}\n")
+        if tok == cfg.eog_inference:
+            break
+        o16.advance(c16, tok)
+        o64.advance(c64, tok)
+    rep = {"steps": n, "row": "C3 voice clone (T_x 60, T_p 151), 2b-2b full depth, synthetic weights seed 1234",
+           "fast_vs_fp64": {"max_rel_err": max(e_fast), "mean_rel_err": float(np.mean(e_fast))},
+           "reference_bf16_vs_fp64": {"max_rel_err": max(e_ref), "mean_rel_err": float(np.mean(e_ref))},
+           "ratio_max": max(e_fast) / max(e_ref), "ratio_mean": float(np.mean(e_fast) / np.mean(e_ref)),
+           "sampler_token_same_as_fp64": {"fast": same_fast, "reference_bf16": same_ref, "steps": n},
+           "per_step": {"fast": [round(v, 6) for v in e_fast], "reference_bf16": [round(v, 6) for v in e_ref]}}
+    with open(os.path.join(REPO, "gpurun_out", "noise_floor.json"), "w") as f:
+        json.dump(rep, f, indent=1)
+    print(json.dumps({k: v for k, v in rep.items() if k != "per_step"}))
+    assert n >= STEPS // 2
+    assert max(e_fast) <= RTOL, rep["fast_vs_fp64"]

@@ -113,3 +113,24 @@ def test_oracle_matches_reference_full_depth():
         assert shas == c["logit_sha"], ci
         top = torch.topk(out["logits"].float(), 64, dim=-1)
         assert np.array_equal(top.indices.numpy().astype(np.int32), arrs[f"top_idx_{ci}"]), ci
+
+
+def test_oracle_fp64_restatement_tracks_bf16():
+    """The fp64 restatement (noise-floor yardstick of test_gpu_noise_floor.py) runs the same
+    graph: on the tiny golden case its logits stay within bf16 rounding noise of the bf16
+    oracle's, and the bf16 oracle itself is unchanged (pinned by the goldens above)."""
+    meta, _ = _load("golden_tiny")
+    cfg = named_config(meta["config"], **meta["config_kw"])
+    sd = synthetic_weights(cfg, meta["weight_seed"])
+    c = meta["cases"][0]
+    o16, o64 = T5GemmaTTSOracle(cfg, sd), T5GemmaTTSOracle(cfg, sd, dtype=torch.float64)
+    a, b = o16.prepare(c["x"], c["y"], c["tgt"]), o64.prepare(c["x"], c["y"], c["tgt"])
+    b["state"] = a["state"]
+    for tok in c["gen"][:8]:
+        l16, l64 = o16.step_logits(a), o64.step_logits(b)
+        assert l64.dtype == torch.float64
+        err = (l16.double() - l64).abs().max().item() / l64.abs().max().item()
+        assert 0.0 < err < 0.05, err
+        a["state"].current_length += 1
+        o16.advance(a, tok)
+        o64.advance(b, tok)

@@ -24,10 +24,12 @@ def flops_per_frame(cfg, T):
 def main():
     which = os.environ.get("CODEC", "16k")
     cfg = codec_16k() if which == "16k" else codec_44k()
+    # SHAPES="32x751,8x500": the B x T decodes to time (default the round-1 set)
+    shapes = [tuple(int(v) for v in s.split("x")) for s in os.environ.get("SHAPES", "1x500,8x500,32x500").split(",")]
     out = []
-    for B, T in [(1, 500), (8, 500), (32, 500)]:
+    for B, T in shapes:
         codec = XCodec2Decoder(cfg, synthetic_codec_weights(cfg, 1), device="cuda:0", max_batch=B, max_frames=T)
-        codes = torch.randint(0, 65536, (B, T), device="cuda", dtype=torch.int32)
+        codes = torch.randint(0, cfg.codebook_size, (B, T), device="cuda", dtype=torch.int32)
         wav = torch.empty(B, T * cfg.hop_length, device="cuda")
         us = C.c_float()
         st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -39,6 +41,13 @@ def main():
         r = {"codec": which, "B": B, "T": T, "ms": round(us.value / 1e3, 3), "frames_per_s": round(B * T / sec, 1),
              "audio_s_per_wall_s": round(B * T / 50.0 / sec, 1), "tflops": round(fl / sec / 1e12, 2),
              "frac_f32_mfma_peak": round(fl / sec / 157.3e12, 3)}
+        g_us, g_fl, g_n = C.c_float(), C.c_double(), C.c_int32()
+        rc = codec.L.xc2_time_gemms(codec.h, C.c_void_p(codes.data_ptr()), B, T, C.c_void_p(wav.data_ptr()), 5,
+                                    st, C.byref(g_us), C.byref(g_fl), C.byref(g_n))
+        assert rc == 0, rc
+        r.update({"gemm_us": round(g_us.value, 1), "gemm_launches": g_n.value, "gemm_flops": g_fl.value,
+                  "gemm_tflops": round(g_fl.value / (g_us.value * 1e-6) / 1e12, 2),
+                  "gemm_frac_f32_mfma_peak": round(g_fl.value / (g_us.value * 1e-6) / 157.3e12, 3)})
         print(json.dumps(r), flush=True)
         out.append(r)
         codec.close()
