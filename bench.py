@@ -516,6 +516,12 @@ def main():
                 "attn_in_block_launches": int(s_launches),
                 "attn_in_block_mode": s_mode,   # 2 tail, 1 front (several passes past 3 slots / CU), 0 own launch
             }
+            if not args.parity:
+                # teacher-forced: the reference sampler on the reference CPU run's logits picks
+                # the fast path's token (full-depth report of this tree's fast-path sources)
+                from t5gemma_tts_amd import _lib
+                line["fast_token_agreement"] = _lib.fast_token_agreement(
+                    os.path.join(REPO, "profiles", "r06_parity_full.json"))
             if parity_line is not None:
                 if cpu is not None:
                     parity_line["vs_cpu_baseline"] = round(parity_line["value"] / cpu["value"], 1)

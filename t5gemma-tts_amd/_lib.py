@@ -265,6 +265,9 @@ PMC_SOURCES = {
     "fused_mlp": ["fused.hip", "common.h", "t5g_kernels.h"],
     "xlayer": ["xlayer.hip", "exact_dev.h", "exact_math.h", "common.h", "t5g_kernels.h"],
     "gate_up": ["gemv.hip", "common.h", "t5g_kernels.h"],
+    # every source the fast decode step's logits and tokens depend on (fast_token_agreement)
+    "fast_path": ["fused.hip", "attn.hip", "gemm.hip", "gemv.hip", "norm.hip", "sampler.hip", "noise.hip",
+                  "engine.hip", "common.h", "t5g_kernels.h"],
 }
 
 
@@ -367,3 +370,29 @@ def time_gate_up(X_ptr: int, ldx: int, M: int, W_ptrs, N: int, K: int, Y_ptr: in
     us = C.c_float()
     check(lib().t5g_time_gemv(C.byref(a), arr, len(W_ptrs), iters, stream, C.byref(us)), "time_gemv")
     return us.value
+
+
+def fast_token_agreement(path: str):
+    """The fast path's teacher-forced token agreement from a committed full-depth parity
+    report (tests/test_gpu_parity_full.py -> gpurun_out/parity_full.json, copied under
+    profiles/): over the rows it teacher-forces, the steps on which the reference sampler,
+    fed the reference CPU run's logits and the same noise, picks the token the fast path
+    picked. None (with a note) when the file is missing or was made on other fast-path
+    sources than this tree's."""
+    import json
+    info = {"source": os.path.relpath(path, os.path.dirname(_PKG)), "kernel_source_digest":
+            kernel_source_digest("fast_path")}
+    if not os.path.exists(path):
+        return dict(info, note="no report")
+    rep = json.load(open(path))
+    info["source_digest"] = rep.get("source_digest")
+    if info["source_digest"] != info["kernel_source_digest"]:
+        return dict(info, note="stale: report made on other fast-path sources")
+    agree = steps = 0
+    for row in rep.get("rows", {}).values():
+        if "ref_sampler_same_token" in row:
+            agree += int(row["ref_sampler_same_token"])
+            steps += int(row["steps"])
+    if steps == 0:
+        return dict(info, note="no teacher-forced rows")
+    return dict(info, agree=agree, steps=steps, rate=round(agree / steps, 4))

@@ -47,6 +47,7 @@ def test_fast_path_error_vs_fp64_noise_floor():
     from oracle.t5g_oracle import T5GemmaTTSOracle, draw_noise, sample_helper
     from t5gemma_tts_amd.config import config_2b2b
     from t5gemma_tts_amd.engine import SamplingParams, T5GemmaTTSEngine, Utterance
+    from t5gemma_tts_amd import _lib
     from t5gemma_tts_amd.weights import synthetic_weights
 
     torch.set_num_threads(min(16, os.cpu_count() or 1))
@@ -75,7 +76,7 @@ def test_fast_path_error_vs_fp64_noise_floor():
     c64["state"] = st   # one row state: positions follow the same history
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     progress = os.path.join(REPO, "gpurun_out", "noise_floor_progress.txt")
-    e_fast, e_ref, same_fast, same_ref, n = [], [], 0, 0, 0
+    e_fast, e_ref, same_fast, same_ref, fast_ref, n = [], [], 0, 0, 0, 0
     for t, tok in enumerate(toks):
         l16 = o16.step_logits(c16)
         l64 = o64.step_logits(c64)
@@ -92,6 +93,7 @@ def test_fast_path_error_vs_fp64_noise_floor():
         assert picks[0] == tok, f"step {t}: reference sampler on the fast logits -> {picks[0]}, GPU {tok}"
         same_fast += int(picks[0] == picks[2])
         same_ref += int(picks[1] == picks[2])
+        fast_ref += int(picks[0] == picks[1])
         n += 1
         # the history is the fast path's: carry the state its pick left
         st = states[0]
@@ -109,6 +111,8 @@ def test_fast_path_error_vs_fp64_noise_floor():
            "reference_bf16_vs_fp64": {"max_rel_err": max(e_ref), "mean_rel_err": float(np.mean(e_ref))},
            "ratio_max": max(e_fast) / max(e_ref), "ratio_mean": float(np.mean(e_fast) / np.mean(e_ref)),
            "sampler_token_same_as_fp64": {"fast": same_fast, "reference_bf16": same_ref, "steps": n},
+           "sampler_token_fast_same_as_reference_bf16": fast_ref,
+           "source_digest": _lib.kernel_source_digest("fast_path"),
            "per_step": {"fast": [round(v, 6) for v in e_fast], "reference_bf16": [round(v, 6) for v in e_ref]}}
     with open(os.path.join(REPO, "gpurun_out", "noise_floor.json"), "w") as f:
         json.dump(rep, f, indent=1)

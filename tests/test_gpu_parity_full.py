@@ -103,7 +103,8 @@ def test_c3_full_depth_batch8_vs_reference():
                            max_gen=520)
     out = eng.generate(utts, SamplingParams(**p), seeds=seeds, parity=True, exact=False, record_logits=True)
     logits = out["logits"]                 # per step: [8, V] on device
-    report = {"rtol": RTOL, "rows": {}}
+    from t5gemma_tts_amd import _lib
+    report = {"rtol": RTOL, "rows": {}, "source_digest": _lib.kernel_source_digest("fast_path")}
     orc = T5GemmaTTSOracle(cfg, sd)
     op = OP(**p)
 
