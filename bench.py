@@ -450,7 +450,7 @@ def main():
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s",
                 "frac": round(ach / 157.3, 4), "traffic": None,
                 "traffic_note": "compute-bound kernel: MFMA busy from the SQ_VALU_MFMA_BUSY_CYCLES pass "
-                                "(profiles/r06_pmc_c5_codec.csv), HBM bytes not priced",
+                                "(profiles/r06_pmc_c5_codec.json: 0.72 of the SIMDs), HBM bytes not priced",
                 "kernel": "gemm_f32_kernel (XCodec2 decoder GEMMs: fc, conv k7 / k3 as halo GEMMs, q|k|v, o, "
                           "fc1 + SiLU, fc2, head, iSTFT basis; 128 x 128 tiles, v_mfma_f32_32x32x2_f32)",
                 "frames": f"{B} x {Tc}", "flops_per_decode": g_fl.value, "gemm_launches_per_decode": g_n.value,
