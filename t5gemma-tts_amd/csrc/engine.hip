@@ -2065,9 +2065,9 @@ extern "C" int t5g_time_xlayer(t5g_engine* e, int32_t B, int32_t iters, void* st
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, st));
     int rc = 0;
-    const char* one_s = getenv("T5G_TIME_ONE_LAYER");   // diagnostic, as t5g_time_decode_layer
-    const int one = one_s ? std::min(std::max(atoi(one_s), 0), L - 1) : -1;
-    for (int i = 0; i < n && !rc; ++i) rc = xlayer_launch(xlayer_args(e, B, one >= 0 ? one : i % L), st);
+    const char* rot_s = getenv("T5G_TIME_ROT");   // diagnostic, as t5g_time_decode_layer
+    const int rot = rot_s ? std::min(std::max(atoi(rot_s), 1), L - 2) : 0;
+    for (int i = 0; i < n && !rc; ++i) rc = xlayer_launch(xlayer_args(e, B, rot > 0 ? 1 + i % rot : i % L), st);
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;
@@ -2151,10 +2151,11 @@ extern "C" int t5g_time_decode_layer(t5g_engine* e, int32_t B, int32_t iters, vo
         }
     *keys = (float)(ksum / L);
     const int n = (iters + L - 1) / L * L;
-    // diagnostic (tools/probe_mall_layer.py): T5G_TIME_ONE_LAYER=l launches layer l every
-    // time, its weights then served from the Infinity Cache instead of HBM
-    const char* one_s = getenv("T5G_TIME_ONE_LAYER");
-    const int one = one_s ? std::min(std::max(atoi(one_s), 0), L - 1) : -1;
+    // diagnostic (tools/probe_mall_layer.py): T5G_TIME_ROT=n rotates over layers 1..n only
+    // (n = 1: one layer's ~175 MB of weights stay in the 256 MiB Infinity Cache; n = 2: its
+    // activations and caches stay, its weights do not)
+    const char* rot_s = getenv("T5G_TIME_ROT");
+    const int rot = rot_s ? std::min(std::max(atoi(rot_s), 1), L - 2) : 0;
     int rc = 0;
     for (int l = 0; l < L && !rc; ++l) rc = args(l, fa) ? fused_mlp(fa, st) : -1;
     hipEvent_t e0, e1;
@@ -2162,7 +2163,7 @@ extern "C" int t5g_time_decode_layer(t5g_engine* e, int32_t B, int32_t iters, vo
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, st));
     for (int i = 0; i < n && !rc; ++i) {
-        const int l = one >= 0 ? one : i % L;
+        const int l = rot > 0 ? 1 + i % rot : i % L;
         rc = args(l, fa) ? fused_mlp(fa, st) : -1;
     }
     HIPCHK(hipEventRecord(e1, st));

@@ -238,8 +238,8 @@ class T5GemmaTTSEngine:
         stage S): 0 / False its own flash launch, 1 in front of the launch's o-projection,
         2 / True (default) at the end of the previous layer's launch after its q|k|v stage,
         with that layer's o-projection. Bitwise equal in every mode; a call past the tail's
-        chunk-slot bound takes mode 1, past mode 1's (or rows past 1 024 keys) the separate
-        launch."""
+        chunk-slot bound takes mode 1 (two passes of slots, rows up to 3 072 keys at 8 rows),
+        past that the separate launch."""
         m = 2 if mode is True else 0 if mode is False else int(mode)
         _lib.check(self.L.t5g_engine_set_attn_in_block(self.h, m), "set_attn_in_block")
 

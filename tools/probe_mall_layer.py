@@ -2,7 +2,8 @@
 fast path's fused_block_kernel (t5g_time_decode_layer) and the parity path's xlayer_kernel
 (t5g_time_xlayer) at C3 (8 rows), timed with HIP events rotated over the 26 decoder layers
 (every launch streams its ~175 MB from HBM, as in a decode step) and with one layer repeated
-(T5G_TIME_ONE_LAYER: its weights then come from the 256 MiB Infinity Cache). GPU only."""
+(T5G_TIME_ROT=1: its weights then come from the 256 MiB Infinity Cache) and two or three layers
+repeated (their weights do not fit; their activations and caches do). GPU only."""
 import ctypes as C
 import json
 import os
@@ -35,21 +36,21 @@ def main():
     for parity in (False, True):
         eng.generate(utts, p, seeds=list(range(B)), chunk=64, parity=parity)
         torch.cuda.synchronize()
-        for one in (None, 12):
-            if one is None:
-                os.environ.pop("T5G_TIME_ONE_LAYER", None)
+        for rot in (None, 1, 2, 3):
+            if rot is None:
+                os.environ.pop("T5G_TIME_ROT", None)
             else:
-                os.environ["T5G_TIME_ONE_LAYER"] = str(one)
+                os.environ["T5G_TIME_ROT"] = str(rot)
             us, keys = C.c_float(), C.c_float()
             if parity:
                 _lib.check(L.t5g_time_xlayer(eng.h, B, 208, st, C.byref(us)), "time_xlayer")
             else:
                 _lib.check(L.t5g_time_decode_layer(eng.h, B, 208, st, C.byref(us), C.byref(keys)), "time_layer")
-            name = ("xlayer" if parity else "fused_block") + ("_hbm" if one is None else "_mall")
+            name = ("xlayer" if parity else "fused_block") + ("_rot26" if rot is None else f"_rot{rot}")
             out[name] = round(us.value, 2)
             print(name, out[name], "us", flush=True)
         eng.set_exact(False)
-    os.environ.pop("T5G_TIME_ONE_LAYER", None)
+    os.environ.pop("T5G_TIME_ROT", None)
     print(json.dumps(out))
 
 
