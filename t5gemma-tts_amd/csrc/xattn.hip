@@ -141,13 +141,21 @@ __global__ __launch_bounds__(256) void xattn_scores_kernel(ExactAttnArgs a, floa
             fmaxf(fmaxf(wmax[0][tid], wmax[1][tid]), fmaxf(wmax[2][tid], wmax[3][tid]));
 }
 
+// Round 6 schedule (the same operations in the same order as round 5's, bitwise): every
+// global read the workgroup needs for the first two 512-key blocks -- the chunk maxima, the
+// V rows of its 32-dimension slice, its scores -- is issued at once, right after the row
+// length, so one memory round trip precedes the arithmetic instead of three in sequence
+// (chunk maxima -> V -> scores, the scores waiting behind V in issue order). V comes in as
+// 16-byte words: lane (group gl = tid / 4 of the block, 8-dimension slice tid % 4) holds
+// the 8 keys of its group, 4x fewer load instructions than 4-byte words. Blocks past the
+// second load at the top of their own iteration.
 template <int G, int XD_D>
 __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const float* sbuf, const float* mbuf,
                                                        int cap, int nsplit) {
     constexpr int BLK = SDPA_KV_BLOCK;           // 512
-    constexpr int NGRP = BLK / 8;                // 8-key groups per block
-    constexpr int DP = XD_DZ / 2;                // dimension pairs per workgroup
-    constexpr int GL = 256 / DP;                 // group lanes (16)
+    constexpr int NGRP = BLK / 8;                // 8-key groups per block (64: one per lane quad)
+    constexpr int PPT = BLK / 256;               // block positions per thread (2)
+    static_assert(NGRP * 4 == 256 && XD_DZ == 32, "lane map: 64 groups x 4 eight-dimension slices");
     __shared__ float pex[G][BLK + 16];           // exact p (block sums)
     __shared__ float pbf[G][BLK];                // bf16-rounded p (P.V)
     __shared__ float tmp[NGRP][G][XD_DZ];        // group chain sums of the block
@@ -164,40 +172,82 @@ __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const fl
     const int nblk = (span + BLK - 1) / BLK;
     const float* sb = sbuf + ((long)qi * a.Hq + kvh * G) * cap;
     const bf16_t* Vb = a.V + row * a.kv_bstride + kvh * a.kv_hstride + (long)lo * XD_D + z * XD_DZ;
+    const int d8 = tid & 3, gl = tid >> 2;       // P.V role: 8-key group gl, dims 8 d8 .. 8 d8 + 7
+    const float* mb_row = mbuf + ((long)qi * a.Hkv + kvh) * nsplit * G;
+    // ---- every read up front (unconditional: clamped addresses, so the waits stay exact)
+    const int gm = wave < G ? wave : G - 1;
+    float cmx[(SDPA_MAX_BLOCKS * (BLK / XD_CH) + 63) / 64];
+    constexpr int NCM = (SDPA_MAX_BLOCKS * (BLK / XD_CH) + 63) / 64;
+#pragma unroll
+    for (int i = 0; i < NCM; ++i) cmx[i] = mb_row[min(lane + 64 * i, nch - 1) * G + gm];
+    auto vload = [&](u32x4 (&v)[8], int b) {
+        const int bs = b * BLK, blen = min(BLK, span - bs);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = *(const u32x4*)(Vb + (long)(bs + min(gl * 8 + j, blen - 1)) * XD_D + 8 * d8);
+    };
+    auto sload = [&](float (&sv)[G][PPT], int b) {
+        const int bs = b * BLK, blen = min(BLK, span - bs);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < PPT; ++i) sv[g][i] = sb[(long)g * cap + bs + min(tid + 256 * i, blen - 1)];
+    };
+    u32x4 v0[8], v1[8];
+    float s0[G][PPT], s1[G][PPT];
+    const int b1 = min(1, nblk - 1);
+    vload(v0, 0);
+    sload(s0, 0);
+    vload(v1, b1);
+    sload(s1, b1);
     if (wave < G) {   // running max through each block, from the chunk maxima
         const int g = wave;
         float run = -INFINITY;
         for (int b = 0; b < nblk; ++b) {
             float cm = -INFINITY;
-            for (int c = b * (BLK / XD_CH) + lane; c < min(nch, (b + 1) * (BLK / XD_CH)); c += 64)
-                cm = fmaxf(cm, mbuf[(((long)qi * a.Hkv + kvh) * nsplit + c) * G + g]);
+#pragma unroll
+            for (int i = 0; i < NCM; ++i) {
+                const int c = lane + 64 * i;
+                if (c >= b * (BLK / XD_CH) && c < min(nch, (b + 1) * (BLK / XD_CH))) cm = fmaxf(cm, cmx[i]);
+            }
             run = fmaxf(run, wave_max(cm));
             if (lane == 0) mrun[g][b] = run;
         }
         if (lane < 16) pex[g][BLK + lane] = 0.f;
     }
-    const int dp = tid % DP, gl = tid / DP;      // P.V role: dimension pair, group lane
     float l = 0.f, m_old = -INFINITY;            // wave g < G: head g's running sum
     float dst = 0.f;                             // folder (g, dim) = tid < G * XD_DZ
     const int fg = tid / XD_DZ, fd = tid % XD_DZ;
     __syncthreads();
-    constexpr int GPL = NGRP / GL;               // 8-key groups per lane and block (4)
     for (int b = 0; b < nblk; ++b) {
         const int bs = b * BLK, blen = min(BLK, span - bs);
-        // V words of this lane's groups gl + GL t, issued first: they fly during the exact
-        // p and the block sums (keys past the block re-read its last key, unused)
-        uint32_t vw[GPL][8];
+        u32x4 vb[8];
+        float sv[G][PPT];
+        if (b == 0) {
 #pragma unroll
-        for (int t = 0; t < GPL; ++t)
+            for (int j = 0; j < 8; ++j) vb[j] = v0[j];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                vw[t][j] = *(const uint32_t*)(Vb + (long)(bs + min((gl + GL * t) * 8 + j, blen - 1)) * XD_D + 2 * dp);
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int i = 0; i < PPT; ++i) sv[g][i] = s0[g][i];
+        } else if (b == 1) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) vb[j] = v1[j];
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int i = 0; i < PPT; ++i) sv[g][i] = s1[g][i];
+        } else {
+            vload(vb, b);
+            sload(sv, b);
+        }
         // exact p of the block's keys
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const float mb = mrun[g][b];
-            for (int pos = tid; pos < BLK; pos += 256) {
-                const float p = pos < blen ? sdpa_p(__fsub_rn(sb[(long)g * cap + bs + pos], mb), pos, blen) : 0.f;
+#pragma unroll
+            for (int i = 0; i < PPT; ++i) {
+                const int pos = tid + 256 * i;
+                const float p = pos < blen ? sdpa_p(__fsub_rn(sv[g][i], mb), pos, blen) : 0.f;
                 pex[g][pos] = p;
                 pbf[g][pos] = rbf(p);
             }
@@ -212,34 +262,37 @@ __global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const fl
             m_old = mb;
             if (lane == 0) et_s[g] = et;
         }
-        // 8-key group chains of the slice: lane gl takes groups gl, gl + 16, ... (pairs, odd
-        // key first; keys past the block count 0 and add nothing: the chain stops there)
+        // the 8-key group chain of group gl over dims 8 d8 .. 8 d8 + 7: pairs, odd key
+        // first (keys past the block count 0 and add nothing: the chain stops there)
         const int ngrp = (blen + 7) / 8;
-#pragma unroll
-        for (int t = 0; t < GPL; ++t) {
-            const int gi = gl + GL * t;
-            if (gi >= ngrp) break;
-            const int k0 = gi * 8, cn = min(8, blen - k0);
-            float t0[G], t1[G];
+        if (gl < ngrp) {
+            const int k0 = gl * 8, cn = min(8, blen - k0);
 #pragma unroll
             for (int g = 0; g < G; ++g) {
-                t0[g] = 0.f;
-                t1[g] = 0.f;
+                float t[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) t[i] = 0.f;
 #pragma unroll
                 for (int j = 0; j < 8; j += 2) {
                     if (j < cn) {
                         if (j + 1 < cn) {
                             const float p1 = pbf[g][k0 + j + 1];
-                            t0[g] = fmaf(p1, bf_lo(vw[t][j + 1]), t0[g]);
-                            t1[g] = fmaf(p1, bf_hi(vw[t][j + 1]), t1[g]);
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                t[2 * q] = fmaf(p1, bf_lo(vb[j + 1][q]), t[2 * q]);
+                                t[2 * q + 1] = fmaf(p1, bf_hi(vb[j + 1][q]), t[2 * q + 1]);
+                            }
                         }
                         const float p0 = pbf[g][k0 + j];
-                        t0[g] = fmaf(p0, bf_lo(vw[t][j]), t0[g]);
-                        t1[g] = fmaf(p0, bf_hi(vw[t][j]), t1[g]);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            t[2 * q] = fmaf(p0, bf_lo(vb[j][q]), t[2 * q]);
+                            t[2 * q + 1] = fmaf(p0, bf_hi(vb[j][q]), t[2 * q + 1]);
+                        }
                     }
                 }
-                tmp[gi][g][2 * dp] = t0[g];
-                tmp[gi][g][2 * dp + 1] = t1[g];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) tmp[gl][g][8 * d8 + i] = t[i];
             }
         }
         __syncthreads();
