@@ -337,7 +337,7 @@ def main():
             _lib.check(rc_xl, "time_xlayer")   # a real launch failure, not a shape the launch does not serve
         if rc_xl == 0:
             xbytes = _lib.xlayer_bytes(B, cfg.backbone, wl_tx, cfg.backbone.num_decoder_layers)
-            pmc_x = os.path.join(REPO, "profiles", "r05_pmc_xlayer.json")
+            pmc_x = os.path.join(REPO, "profiles", "r06_pmc_xlayer.json")
             kname = ("xlayer_kernel: one decoder layer after its self attention as one persistent launch (o, "
                      "norm, cross-q, PM cross attention, cross-o, norm, gate/up + GeGLU, down in the reference's "
                      "K parts, norm, next q|k|v; f32 MFMA in the reference host's fp32 orders)")
@@ -395,10 +395,10 @@ def main():
                 alg_bytes = _lib.fused_block_bytes(B, wl_tx, d, f, self_keys=keys.value)
                 if keys.value > 0 and s_mode == 1:
                     kname = "fused_block_kernel<1> (the layer's self attention in front of its o-projection)"
-                    pmc, pmc_op = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s_front.json"), "fused_block_s"
+                    pmc, pmc_op = os.path.join(REPO, "profiles", "r06_pmc_fused_block_s_front.json"), "fused_block_s"
                 elif keys.value > 0:
                     kname = _lib.FUSED_BLOCK_S_KERNEL
-                    pmc, pmc_op = os.path.join(REPO, "profiles", "r05_pmc_fused_block_s.json"), "fused_block_s"
+                    pmc, pmc_op = os.path.join(REPO, "profiles", "r06_pmc_fused_block_s.json"), "fused_block_s"
                 else:
                     pmc, pmc_op = os.path.join(REPO, "profiles", "r04_pmc_fused_block.json"), "fused_block"
             else:
