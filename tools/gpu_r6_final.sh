@@ -8,6 +8,7 @@ rm -rf gpurun_out/pmc_fs gpurun_out/pmc_xl gpurun_out/prof_final6 gpurun_out/sum
 mkdir -p gpurun_out/pmc_fs gpurun_out/pmc_xl
 run fs_fetch 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fs/fetch -o pmc --output-format csv -- python3 tools/pmc_fused.py --self gpurun_out/pmc_fs/alg_f.json
 run fs_write 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_fs/write -o pmc --output-format csv -- python3 tools/pmc_fused.py --self gpurun_out/pmc_fs/alg_w.json
+cp gpurun_out/pmc_fs/alg_f.json gpurun_out/pmc_fs/alg.json
 run xl_fetch 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_xl/fetch -o pmc --output-format csv -- python3 tools/pmc_xlayer.py
 run xl_write 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_xl/write -o pmc --output-format csv -- python3 tools/pmc_xlayer.py
 for d in pmc_xl/fetch pmc_xl/write pmc_fs/fetch pmc_fs/write; do
