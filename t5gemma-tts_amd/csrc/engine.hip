@@ -2101,7 +2101,21 @@ extern "C" int t5g_time_xlayer(t5g_engine* e, int32_t B, int32_t iters, void* st
     int rc = 0;
     const char* rot_s = getenv("T5G_TIME_ROT");   // diagnostic, as t5g_time_decode_layer
     const int rot = rot_s ? std::min(std::max(atoi(rot_s), 1), L - 2) : 0;
-    for (int i = 0; i < n && !rc; ++i) rc = xlayer_launch(xlayer_args(e, B, rot > 0 ? 1 + i % rot : i % L), st);
+    // diagnostic T5G_TIME_SHARE: "chain" -- every launch reads layer 1's o / cross q / cross o /
+    // q|k|v weights and cross K / V (its G / D weights rotate); "gd" -- layer 1's gate/up and
+    // down (the rest rotates): which bytes' cache residency the launch is sensitive to
+    const char* share_s = getenv("T5G_TIME_SHARE");
+    const int share = !share_s ? 0 : !strcmp(share_s, "chain") ? 1 : !strcmp(share_s, "gd") ? 2 : 0;
+    const XLayerArgs a1 = xlayer_args(e, B, 1);
+    for (int i = 0; i < n && !rc; ++i) {
+        XLayerArgs a = xlayer_args(e, B, rot > 0 ? 1 + i % rot : i % L);
+        if (share == 1) {
+            a.Wo = a1.Wo, a.Wq = a1.Wq, a.Wco = a1.Wco, a.Wqkv = a1.Wqkv, a.ck = a1.ck, a.cv = a1.cv;
+        } else if (share == 2) {
+            a.Wgu = a1.Wgu, a.Wd = a1.Wd;
+        }
+        rc = xlayer_launch(a, st);
+    }
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;
