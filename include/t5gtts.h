@@ -320,12 +320,6 @@ int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable);
  * t5g_engine_attn_in_block_mode: where the last decode step ran S (2, 1, or 0 = its own
  * launch). */
 int t5g_engine_set_attn_in_block(t5g_engine* e, int32_t mode);
-/* Parity layer launch (xlayer.hip) Infinity Cache warm-up, default on (round 6): the
- * workgroups that idle until its cross-attention stage read the next launch's o-projection,
- * cross q / cross o weights and cross K / V, and this launch's q|k|v weights, so those
- * latency-bound stages find them in the 256 MiB Infinity Cache. Loads only: bits unchanged.
- * No reference counterpart (a scheduling choice of the MI355X memory system). */
-int t5g_engine_set_xl_warm(t5g_engine* e, int32_t on);
 int t5g_engine_attn_in_block_launches(t5g_engine* e, int64_t* n);
 int t5g_engine_attn_in_block_mode(t5g_engine* e, int32_t* mode);
 

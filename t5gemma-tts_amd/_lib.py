@@ -138,7 +138,6 @@ SIGNATURES = {
     "t5g_engine_set_attn_in_block": (C.c_int, [_P, _I]),
     "t5g_engine_attn_in_block_launches": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "t5g_engine_attn_in_block_mode": (C.c_int, [_P, C.POINTER(C.c_int32)]),
-    "t5g_engine_set_xl_warm": (C.c_int, [_P, C.c_int32]),
     "t5g_time_decode_layer": (C.c_int, [_P, _I, _I, _P, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "t5g_engine_set_text_max": (C.c_int, [_P, _I]),
     "t5g_engine_set_audio_max": (C.c_int, [_P, _I]),

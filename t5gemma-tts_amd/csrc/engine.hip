@@ -94,9 +94,6 @@ struct t5g_engine {
     int attn_in_block = 2;   // 0 own launch, 1 stage S in front of O1, 2 at the end of the previous launch
     int64_t s_launches = 0;   // persistent layer launches run with stage S (tests)
     int s_mode_used = 0;      // the last decode pass's stage-S placement: 2 tail, 1 front, 0 none
-    // parity layer launches warm the Infinity Cache for the next launch (t5g_engine_set_xl_warm)
-    bool xl_warm = true;
-    unsigned* xl_pf_sink = nullptr;
     float* afpart = nullptr;    // [B][Hkv][nsplit][G][D]
     float* afstat = nullptr;    // [B][Hkv][nsplit][G][2]
     unsigned* aftick = nullptr; // [B][Hkv]
@@ -663,27 +660,6 @@ static XLayerArgs xlayer_args(t5g_engine* e, int M, int l) {
     a.sync = xlayer_set(e, l);
     a.sync_next = xlayer_set(e, (l + 1) % c.n_dec_layers);
     a.timeout = e->fsync;
-    // Infinity Cache warm-up (xlayer.hip): the next launch's first stages' bytes, then this
-    // launch's q|k|v weights (the last launch: its q|k|v only, there is none)
-    a.pf_n = 0;
-    a.pf_sink = e->xl_pf_sink;
-    auto pf_add = [&](const void* p, int64_t bytes) {
-        if (e->xl_warm && p && bytes > 0 && bytes < (int64_t)0x40000000 && a.pf_n < XL_PF_MAX) {
-            a.pf[a.pf_n] = p;
-            a.pf_bytes[a.pf_n++] = (uint32_t)bytes;
-        }
-    };
-    if (!last) {
-        const t5g_engine::XLayer& Xn = e->dec_x[l + 1];
-        const int64_t kvb = (int64_t)M * c.n_kv_heads * c.max_text * c.head_dim * 2;
-        pf_add(Xn.o, (int64_t)ng_pad(c.hidden) * 16 * e->q_dim * 2);
-        pf_add(Xn.cross_q, (int64_t)ng_pad(e->q_dim) * 16 * c.hidden * 2);
-        pf_add(e->ck[l + 1], kvb);
-        pf_add(e->cv[l + 1], kvb);
-        pf_add(Xn.cross_o, (int64_t)ng_pad(c.hidden) * 16 * e->q_dim * 2);
-        pf_add(Xn.qkv, (int64_t)ng_pad(e->qkv_dim) * 16 * c.hidden * 2);
-    }
-    if (!a.pf_sink) a.pf_n = 0;
     return a;
 }
 
@@ -903,7 +879,6 @@ static int xmm_prepare(t5g_engine* e) {
     RC(alloc(e, &e->dhh16, B16 * d));
     RC(alloc(e, &e->dpart, 4 * B16 * d));
     HIPCHK(hipDeviceSynchronize());
-    RC(alloc(e, &e->xl_pf_sink, 64));
     e->xmm_ready = true;
     return T5G_OK;
 }
@@ -1792,15 +1767,6 @@ extern "C" int t5g_engine_set_attn_flash(t5g_engine* e, int32_t enable) {
     if (!e) return T5G_EINVAL;
     if (e->attn_flash != (enable != 0)) {
         e->attn_flash = enable != 0;
-        drop_graphs(e);   // captured launches follow the flag
-    }
-    return T5G_OK;
-}
-
-extern "C" int t5g_engine_set_xl_warm(t5g_engine* e, int32_t on) {
-    if (!e || on < 0 || on > 1) return T5G_EINVAL;
-    if (e->xl_warm != (on != 0)) {
-        e->xl_warm = on != 0;
         drop_graphs(e);   // captured launches follow the flag
     }
     return T5G_OK;

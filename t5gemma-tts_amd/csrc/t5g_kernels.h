@@ -145,7 +145,6 @@ constexpr int FM_LINE = 32, FM_SET_LINES = 67, FM_SET_WORDS = FM_SET_LINES * FM_
 // reference's two K parts, N3, the next layer's q|k|v -- the per-op launches' arithmetic,
 // bitwise. Decode rows M <= 8, the 2b-2b shapes (hidden 2304, q_dim 2048, head_dim 256, 8 q
 // heads over 4 kv heads, intermediate 9216), <= 64 text keys per row.
-constexpr int XL_PF_MAX = 8;
 struct XLayerArgs {
     int M;
     // E16 weights of the layer (Wqkv: the next layer's; null on the last layer)
@@ -174,13 +173,6 @@ struct XLayerArgs {
     unsigned* sync;             // this launch's XL_SET_LINES counter lines (zero when it starts)
     unsigned* sync_next;        // the next launch's set: zeroed by this launch
     unsigned* timeout;          // sticky timeout word (fused.hip's)
-    // Infinity Cache warm-up (loads only): bytes the next launch's chain stages read first
-    // (its o-projection, cross q and cross o weights, its cross K / V) and this launch's
-    // q|k|v weights, read by the workgroups that idle until stage A; pf_n = 0: none
-    const void* pf[XL_PF_MAX];
-    uint32_t pf_bytes[XL_PF_MAX];
-    int pf_n;
-    unsigned* pf_sink;          // written only if the folded bytes equal a constant
 };
 constexpr int XL_SET_LINES = 56, XL_SET_WORDS = XL_SET_LINES * FM_LINE;
 int xlayer_launch(const XLayerArgs& a, hipStream_t st);   // -1: not built for these args / this device

@@ -595,33 +595,6 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     auto none = [] {};
     XL_TS(0);
 
-    // ---- warm-up: workgroups [d / 16, nw) run no stage before A (~20 us in). Their waves
-    // 1..7 stream the bytes the next launch's first stages read (o-projection, cross q, cross
-    // o weights, cross K / V) and this launch's q|k|v weights through the Infinity Cache,
-    // which keeps them until used (< 256 MiB of other traffic in between): those stages are
-    // latency-bound chains, and cache-resident bytes shorten them. Loads
-    // only, folded into a value stored only if it equals a constant; done before A's wait.
-    if (a.pf_n > 0 && bu >= d / 16 && bu < nw && (tid >> 6) > 0) {
-        constexpr int DEPTH = 8;
-        const int lane = tid & 63, k = bu - d / 16, nk = nw - d / 16;
-        const int W = nk * (XL_NW - 1), w = k * (XL_NW - 1) + (tid >> 6) - 1;
-        uint32_t acc = 0;
-        for (int r = 0; r < a.pf_n; ++r) {
-            const __amdgpu_buffer_rsrc_t rs = xl_rsrc(a.pf[r], a.pf_bytes[r]);
-            const int nch = (int)((a.pf_bytes[r] + 1023u) >> 10);
-            for (int c0 = w; c0 < nch; c0 += W * DEPTH) {
-                u32x4 v[DEPTH];
-#pragma unroll
-                for (int u = 0; u < DEPTH; ++u)
-                    v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                         rs, ((c0 + u * W) << 10) + lane * 16, 0, 0));
-#pragma unroll
-                for (int u = 0; u < DEPTH; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
-            }
-        }
-        if (acc == 0x9e3779b9u && lane == 0) a.pf_sink[0] = acc;
-    }
-
     // ---- O1: o-projection of the self attention (K = q_dim: 64 chunks), groups 0..143
     if (bu < d / 16) {
         const XlGemv s{a.Wo, XL_QD / 32, xl_rsrc(a.att16_self, 16u * XL_QD * 2u), d, M,

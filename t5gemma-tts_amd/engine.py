@@ -243,11 +243,6 @@ class T5GemmaTTSEngine:
         m = 2 if mode is True else 0 if mode is False else int(mode)
         _lib.check(self.L.t5g_engine_set_attn_in_block(self.h, m), "set_attn_in_block")
 
-    def set_xl_warm(self, on: bool) -> None:
-        """Parity layer launches warm the Infinity Cache with the next launch's first stages'
-        bytes (csrc/xlayer.hip, default on). Loads only: tokens and logits unchanged."""
-        _lib.check(self.L.t5g_engine_set_xl_warm(self.h, 1 if on else 0), "set_xl_warm")
-
     def attn_in_block_mode(self) -> int:
         """Where the last fast-path decode step ran the self attention: 2 at the end of the
         previous layer's launch, 1 in front of the layer's o-projection, 0 its own launch."""
