@@ -2065,8 +2065,6 @@ extern "C" int t5g_time_xlayer(t5g_engine* e, int32_t B, int32_t iters, void* st
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, st));
     int rc = 0;
-    const char* rot_s = getenv("T5G_TIME_ROT");   // diagnostic, as t5g_time_decode_layer
-    const int rot = rot_s ? std::min(std::max(atoi(rot_s), 1), L - 2) : 0;
     // diagnostic T5G_TIME_SHARE: "chain" -- every launch reads layer 1's o / cross q / cross o /
     // q|k|v weights and cross K / V (its G / D weights rotate); "gd" -- layer 1's gate/up and
     // down (the rest rotates): which bytes' cache residency the launch is sensitive to
@@ -2074,8 +2072,8 @@ extern "C" int t5g_time_xlayer(t5g_engine* e, int32_t B, int32_t iters, void* st
     const int share = !share_s ? 0 : !strcmp(share_s, "chain") ? 1 : !strcmp(share_s, "gd") ? 2 : 0;
     const XLayerArgs a1 = xlayer_args(e, B, 1);
     for (int i = 0; i < n && !rc; ++i) {
-        XLayerArgs a = xlayer_args(e, B, rot > 0 ? 1 + i % rot : i % L);
-        if (share == 1) {
+        XLayerArgs a = xlayer_args(e, B, i % L);
+        if (share == 1 && a.Wqkv) {
             a.Wo = a1.Wo, a.Wq = a1.Wq, a.Wco = a1.Wco, a.Wqkv = a1.Wqkv, a.ck = a1.ck, a.cv = a1.cv;
         } else if (share == 2) {
             a.Wgu = a1.Wgu, a.Wd = a1.Wd;
@@ -2165,11 +2163,15 @@ extern "C" int t5g_time_decode_layer(t5g_engine* e, int32_t B, int32_t iters, vo
         }
     *keys = (float)(ksum / L);
     const int n = (iters + L - 1) / L * L;
-    // diagnostic (tools/probe_mall_layer.py): T5G_TIME_ROT=n rotates over layers 1..n only
-    // (n = 1: one layer's ~175 MB of weights stay in the 256 MiB Infinity Cache; n = 2: its
-    // activations and caches stay, its weights do not)
-    const char* rot_s = getenv("T5G_TIME_ROT");
-    const int rot = rot_s ? std::min(std::max(atoi(rot_s), 1), L - 2) : 0;
+    // diagnostic T5G_TIME_SHARE (tools/probe_cache_share.py): "chain" -- every launch reads
+    // layer 1's cross q / cross o / next q|k|v / next o weights and cross K / V (they then stay
+    // in the Infinity Cache; the G / D weights rotate); "gd" -- layer 1's gate/up and down.
+    // Each launch keeps its own layer's hand-off counter sets, so the synchronisation is the
+    // decode step's (a launch repeating a layer would find its counters un-zeroed)
+    const char* share_s = getenv("T5G_TIME_SHARE");
+    const int share = !share_s ? 0 : !strcmp(share_s, "chain") ? 1 : !strcmp(share_s, "gd") ? 2 : 0;
+    FusedMlpArgs f1;
+    if (share && !args(1, f1)) return T5G_EUNSUPPORTED;
     int rc = 0;
     for (int l = 0; l < L && !rc; ++l) rc = args(l, fa) ? fused_mlp(fa, st) : -1;
     hipEvent_t e0, e1;
@@ -2177,8 +2179,17 @@ extern "C" int t5g_time_decode_layer(t5g_engine* e, int32_t B, int32_t iters, vo
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, st));
     for (int i = 0; i < n && !rc; ++i) {
-        const int l = rot > 0 ? 1 + i % rot : i % L;
-        rc = args(l, fa) ? fused_mlp(fa, st) : -1;
+        if (!args(i % L, fa)) {
+            rc = -1;
+            break;
+        }
+        if (share == 1 && i % L != L - 1) {
+            fa.Wq = f1.Wq, fa.Wo = f1.Wo, fa.Wqkv = f1.Wqkv, fa.ck = f1.ck, fa.cv = f1.cv;
+            if (fa.Wo1n) fa.Wo1n = f1.Wo1n;
+        } else if (share == 2) {
+            fa.Wgu = f1.Wgu, fa.Wd = f1.Wd;
+        }
+        rc = fused_mlp(fa, st);
     }
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventSynchronize(e1));

@@ -1,8 +1,9 @@
-"""Which bytes' Infinity Cache residency the parity layer launch is sensitive to: xlayer_kernel
-timed over the 26 layers (t5g_time_xlayer) as in a decode step, with T5G_TIME_SHARE=chain
-(every launch reads layer 1's o / cross q / cross o / q|k|v weights and cross K / V, ~48 MB
-that then stay cached) or =gd (layer 1's gate/up and down, 127 MB), and T5G_TIME_ROT=1 (all
-of one layer). Warm-up on and off. GPU only."""
+"""Which bytes' Infinity Cache residency the persistent layer launches are sensitive to: the
+fast path's fused_block_kernel (t5g_time_decode_layer) and the parity path's xlayer_kernel
+(t5g_time_xlayer), timed over the 26 layers as in a decode step, and with
+T5G_TIME_SHARE=chain (every launch reads layer 1's chain-stage weights -- o / cross q /
+cross o / q|k|v -- and cross K / V, ~48 MB that then stay cached) or =gd (layer 1's gate/up
+and down, 127 MB). Every launch keeps its own layer's hand-off counters. GPU only."""
 import ctypes as C
 import json
 import os
@@ -31,19 +32,23 @@ def main():
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8, stop_repetition=3)
     L = _lib.lib()
     st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    eng.generate(utts, p, seeds=list(range(B)), chunk=64, parity=True)
     out = {}
-    for warm in (False, True):
-        eng.set_xl_warm(warm)
-        for env in ({}, {"T5G_TIME_SHARE": "chain"}, {"T5G_TIME_SHARE": "gd"}, {"T5G_TIME_ROT": "1"}):
-            for k in ("T5G_TIME_SHARE", "T5G_TIME_ROT"):
-                os.environ.pop(k, None)
-            os.environ.update(env)
-            us = C.c_float()
-            _lib.check(L.t5g_time_xlayer(eng.h, B, 208, st, C.byref(us)), "time_xlayer")
-            name = f"warm{int(warm)}_" + ("_".join(f"{k[9:].lower()}={v}" for k, v in env.items()) or "rot26")
+    for parity in (False, True):
+        eng.generate(utts, p, seeds=list(range(B)), chunk=64, parity=parity)
+        for share in (None, "chain", "gd"):
+            os.environ.pop("T5G_TIME_SHARE", None)
+            if share:
+                os.environ["T5G_TIME_SHARE"] = share
+            us, keys = C.c_float(), C.c_float()
+            if parity:
+                _lib.check(L.t5g_time_xlayer(eng.h, B, 208, st, C.byref(us)), "time_xlayer")
+            else:
+                _lib.check(L.t5g_time_decode_layer(eng.h, B, 208, st, C.byref(us), C.byref(keys)), "time_layer")
+            name = ("xlayer" if parity else "fused_block") + "_" + (share or "rotate")
             out[name] = round(us.value, 2)
             print(name, out[name], flush=True)
+        eng.set_exact(False)
+    os.environ.pop("T5G_TIME_SHARE", None)
     print(json.dumps(out))
 
 
