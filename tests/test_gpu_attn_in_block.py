@@ -82,6 +82,7 @@ def test_attention_in_block_bitwise_equal_to_flash_launch(B, tp_max, mode):
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
     seeds = list(range(900, 900 + B))
     on0, fon0, n_on0 = _run(eng, utts, p, seeds, mode)
+    assert eng.attn_in_block_mode() == mode   # short rows: each mode takes its own placement
     off, foff, n_off = _run(eng, utts, p, seeds, 0)
     on1, fon1, n_on1 = _run(eng, utts, p, seeds, mode)
     assert n_off == 0 and n_on0 > 0 and n_on1 > 0   # stage S ran, and only when enabled
@@ -145,7 +146,9 @@ def test_tail_mode_falls_back_to_front_past_two_slots_per_worker():
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
     seeds = list(range(16))
     on, fon, n_on = _run(eng, utts, p, seeds, 2)
+    assert eng.attn_in_block_mode() == 1   # the placement the decode launches took: in front
     off, foff, _ = _run(eng, utts, p, seeds, 0)
+    assert eng.attn_in_block_mode() == 0
     assert n_on > 0
     _assert_same(on, off, 16, "front fallback")
     _assert_same(fon, foff, 16, "front fallback graph")
@@ -169,6 +172,7 @@ def test_attention_in_block_long_rows(tp, max_audio):
     p = SamplingParams(top_k=30, top_p=0.9, temperature=0.8)
     seeds = list(range(8))
     on, fon, n_on = _run(eng, utts, p, seeds, 2)
+    assert eng.attn_in_block_mode() == 1   # past the tail's 2 slots per worker: front mode
     off, foff, n_off = _run(eng, utts, p, seeds, 0)
     assert n_off == 0 and n_on >= 2 * 12   # stage S ran in the decode launches
     _assert_same(on, off, 8, "long")

@@ -183,3 +183,28 @@ def test_c5_codec_44k_at_size():
     print(f"c5 codec 44k B{B}x{T} row {r} ({lens[r]} frames): RMS err {rms:.3e}, max {mx:.3e}")
     assert rms <= RMS_TOL and mx <= MAX_TOL
     codec.close()
+
+
+def test_time_gemms_counts_every_decode_gemm():
+    """xc2_time_gemms (the C5 line's codec roofline, bench.py --e2e): every GEMM launch of a
+    decode timed on its own -- 12 + 4 per transformer layer per decode (fc, the k7 embedding,
+    two per residual block x 4, q|k|v / o / fc1 / fc2 per layer, head, iSTFT basis), their
+    2 M N K flops at least the transformer layers' share, their time inside the decode's."""
+    import ctypes as C
+    from t5gemma_tts_amd.codec import XCodec2Decoder, codec_tiny, synthetic_codec_weights
+    cfg = codec_tiny()
+    B, T = 2, 40
+    codec = XCodec2Decoder(cfg, synthetic_codec_weights(cfg, 5), device="cuda:0", max_batch=B, max_frames=T)
+    codes = torch.randint(0, cfg.codebook_size, (B, T), dtype=torch.int32, device="cuda")
+    wav = torch.empty(B, T * cfg.hop_length, device="cuda")
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    g_us, g_fl, g_n, d_us = C.c_float(), C.c_double(), C.c_int32(), C.c_float()
+    assert codec.L.xc2_time_gemms(codec.h, C.c_void_p(codes.data_ptr()), B, T, C.c_void_p(wav.data_ptr()), 3, st,
+                                  C.byref(g_us), C.byref(g_fl), C.byref(g_n)) == 0
+    assert codec.L.xc2_time_decode(codec.h, C.c_void_p(codes.data_ptr()), B, T, C.c_void_p(wav.data_ptr()), 3, st,
+                                   C.byref(d_us)) == 0
+    h, i = cfg.hidden_size, cfg.intermediate_size
+    assert g_n.value == 12 + 4 * cfg.num_hidden_layers
+    assert g_fl.value >= 2.0 * B * T * cfg.num_hidden_layers * (4 * h * h + 2 * h * i)
+    assert 0 < g_us.value <= 1.05 * d_us.value
+    codec.close()
