@@ -190,6 +190,9 @@ struct XlGemv {
     __amdgpu_buffer_rsrc_t y, part;      // outputs (sc1 stores): Y [M][N] bf16 or Y16 / parts
     bool y16;                            // EPI_BF16: Y is row-major [M][N]; GEGLU: Y is the X16 act (K = N / 2)
     int xwin;                            // chunks of the X window staged in LDS (<= XL_XWIN)
+    bool verify = false;                 // X handed off by its data: reload words still XL_X16_SENT
+    unsigned* tmo = nullptr;             // (verify) the sticky timeout word, and the code to leave there
+    unsigned code = 0;
 };
 // the weights of one pass in registers: wave w holds chunks w, w + 8, ... (<= 9)
 struct XlW {
@@ -210,10 +213,7 @@ __device__ __forceinline__ void xl_issue_w(XlW& o, const XlGemv& s, const XlTask
 }
 // the X window [xb, xb + xwin) of rows 0..7 into LDS once per stage (per down part): per chunk
 // the 32 lanes (q, j < 8) of the X16 tile, 512 bytes (R8: lanes j >= 8 read lane j - 8's)
-// VCODE > 0: the window was handed off by its data (xl_wait_x16): words of rows < M still
-// XL_X16_SENT are reloaded; past the spin bound the sticky timeout word gets VCODE
-template <unsigned VCODE>
-__device__ __forceinline__ void xl_fill_x(const XlGemv& s, int xb, u32x4* xs, unsigned* tmo) {
+__device__ __forceinline__ void xl_fill_x(const XlGemv& s, int xb, u32x4* xs) {
     const int n = s.xwin * 32;
     u32x4 v[XL_XWIN * 32 / 512];
 #pragma unroll
@@ -223,7 +223,7 @@ __device__ __forceinline__ void xl_fill_x(const XlGemv& s, int xb, u32x4* xs, un
         asm volatile("" : "+v"(off));
         v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(s.x, off, 0, XL_AUX_SC1));
     }
-    if constexpr (VCODE > 0) {
+    if (s.verify) {
         // the window's words of rows < M that are still the sentinel: not yet visible -- reload
         // them (the stage's probe saw each row's last word, so this is the rare case)
 #pragma unroll
@@ -234,7 +234,7 @@ __device__ __forceinline__ void xl_fill_x(const XlGemv& s, int xb, u32x4* xs, un
                                      v[u][3] == XL_X16_SENT;
                  ++spins) {
                 if (spins > XL_SPIN_MAX) {
-                    __hip_atomic_store(tmo, VCODE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(s.tmo, s.code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -325,9 +325,9 @@ struct XlGemvLds {
 struct XlNoAfter {
     __device__ void operator()(int) const {}
 };
-template <int EPI, bool PART, unsigned VCODE = 0, typename TaskOf, typename Wait, typename After = XlNoAfter>
+template <int EPI, bool PART, typename TaskOf, typename Wait, typename After = XlNoAfter>
 __device__ __forceinline__ void xl_gemv(const XlGemv& s, int t0, int t1, TaskOf task_of, const XlGemvLds& L,
-                                        Wait wait, After after = After(), unsigned* tmo = nullptr) {
+                                        Wait wait, After after = After()) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (t0 >= t1) return;
     float acc = 0.f;   // folder threads: the chain across a task's passes
@@ -339,7 +339,7 @@ __device__ __forceinline__ void xl_gemv(const XlGemv& s, int t0, int t1, TaskOf 
         const XlTask t = task_of(i);
         if (t.xb != xb_cur) {   // uniform: a new X window (the stage's first pass, a down part change)
             xl_lds_barrier();   // every earlier reader of the LDS window is done
-            xl_fill_x<VCODE>(s, t.xb, L.xs, tmo);
+            xl_fill_x(s, t.xb, L.xs);
             xl_lds_barrier();
             xb_cur = t.xb;
         }
@@ -680,13 +680,12 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     if (bu < XL_QD / 16) {
         static_assert(XL_DOWN_KBC % 2 == 0 && XL_DOWN_KBC / 2 <= XL_SC, "down passes");
         const XlGemv s{a.Wq, d / 32, xl_rsrc(a.x16n1, 16u * d * 2u), XL_QD, M, xl_rsrc(a.q, (uint32_t)(M * XL_QD * 2)),
-                       xl_rsrc(nullptr, 0u), false, d / 32};
-        xl_gemv<EPI_BF16, false, 22u>(s, bu, bu + 1, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
-                                      [&] {
-                                          xl_wait_x16(a.x16n1, M, tmo, 22u);   // N1's rows, by their data
-                                          XL_TS(3);
-                                      },
-                                      XlNoAfter(), tmo);
+                       xl_rsrc(nullptr, 0u), false, d / 32, true, tmo, 22u};
+        xl_gemv<EPI_BF16, false>(s, bu, bu + 1, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
+                                 [&] {
+                                     xl_wait_x16(a.x16n1, M, tmo, 22u);   // N1's rows, by their data
+                                     XL_TS(3);
+                                 });
         xl_publish(set, XC_Q + bu / 32, 1u);
         XL_TS(4);
     }
@@ -739,11 +738,11 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     if (!normwg) {
         const int ngt = gd.n0 + gd.n1;
         const XlGemv s{a.Wgu, d / 32, xl_rsrc(a.x16n2, 16u * d * 2u), 2 * XL_F, M, xl_rsrc(a.act16, 16u * XL_F * 2u),
-                       xl_rsrc(nullptr, 0u), true, d / 32};
+                       xl_rsrc(nullptr, 0u), true, d / 32, true, tmo, 26u};
         // part 0's arrivals are published as soon as the worker's part-0 tasks are stored (the
         // down tasks of part 0 wait on those only), part 1's at the end
         const bool early0 = gd.n1 > 0;
-        xl_gemv<EPI_GEGLU, false, 26u>(
+        xl_gemv<EPI_GEGLU, false>(
             s, 0, ngt,
             [&](int i) { return XlTask{i < gd.n0 ? gd.g0_lo + i : gd.g1_lo + (i - gd.n0), 0, d / 32, 0, 0, true, true}; },
             gl,
@@ -759,8 +758,7 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
                                               __hip_atomic_fetch_add(xline(set, XC_G0 + (bu & 7)), (unsigned)gd.n0,
                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                       }
-                                  },
-                                  tmo);
+                                  });
         const int n0 = early0 ? 0 : gd.n0, n1 = gd.n1;
         xl_drain();
         __syncthreads();
@@ -812,13 +810,12 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
         int lo, hi;
         xl_run(a.qkv_dim / 16, nb, bu, lo, hi);
         const XlGemv s{a.Wqkv, d / 32, xl_rsrc(a.x16n3, 16u * d * 2u), a.qkv_dim, M,
-                       xl_rsrc(a.qkv, (uint32_t)(M * a.qkv_dim * 2)), xl_rsrc(nullptr, 0u), false, d / 32};
-        xl_gemv<EPI_BF16, false, 30u>(s, lo, hi, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
-                                      [&] {
-                                          xl_wait_x16(a.x16n3, M, tmo, 30u);   // N3's rows, by their data
-                                          XL_TS(17);
-                                      },
-                                      XlNoAfter(), tmo);
+                       xl_rsrc(a.qkv, (uint32_t)(M * a.qkv_dim * 2)), xl_rsrc(nullptr, 0u), false, d / 32, true, tmo, 30u};
+        xl_gemv<EPI_BF16, false>(s, lo, hi, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
+                                 [&] {
+                                     xl_wait_x16(a.x16n3, M, tmo, 30u);   // N3's rows, by their data
+                                     XL_TS(17);
+                                 });
         XL_TS(18);
     }
 }
