@@ -130,7 +130,6 @@ struct t5g_engine {
     bf16_t *head1_x = nullptr, *head2_x = nullptr;
     bf16_t *xn16 = nullptr, *att16 = nullptr, *act16 = nullptr, *mem16 = nullptr;   // packed tokens
     bf16_t *dxn16 = nullptr, *datt16 = nullptr, *dact16 = nullptr, *dhh16 = nullptr;   // decode rows
-    bf16_t* xl_x16 = nullptr;   // the parity layer's three norm outputs [3][16][hidden], XL_X16_SENT between uses
     float* dpart = nullptr;   // decode down projection: fp32 K-part values [4][B16][hidden]
     uint32_t* trig_exc = nullptr;   // parity mode: RoPE cos / sin exceptions (t5g_engine_set_rope_exc)
     int n_trig_exc = 0;
@@ -643,9 +642,6 @@ static XLayerArgs xlayer_args(t5g_engine* e, int M, int l) {
     a.h = e->dh;
     a.xn = e->dxn;
     a.xn16 = e->dxn16;
-    a.x16n1 = e->xl_x16;
-    a.x16n2 = e->xl_x16 + (size_t)16 * c.hidden;
-    a.x16n3 = e->xl_x16 + (size_t)32 * c.hidden;
     a.tmp = e->tmp;
     a.q = e->dq;
     a.att = e->datt;
@@ -878,8 +874,6 @@ static int xmm_prepare(t5g_engine* e) {
     RC(alloc(e, &e->act16, T16 * f));
     RC(alloc(e, &e->mem16, X16T * d));
     RC(alloc(e, &e->dxn16, B16 * d));
-    RC(alloc(e, &e->xl_x16, 3 * 16 * (int64_t)d));
-    HIPCHK(hipMemset(e->xl_x16, 0xff, (size_t)3 * 16 * d * sizeof(bf16_t)));   // XL_X16_SENT
     RC(alloc(e, &e->datt16, B16 * e->q_dim));
     RC(alloc(e, &e->dact16, B16 * f));
     RC(alloc(e, &e->dhh16, B16 * d));
@@ -1748,8 +1742,6 @@ static int check_handoff(t5g_engine* e, hipStream_t st) {
     // the flash / stage-S arrival tickets are zero between launches; a launch that gave up
     // (or left chunks uncovered) can leave them counting, so they are cleared with the counters
     hipMemsetAsync(e->aftick, 0, (size_t)e->c.max_batch * e->c.n_kv_heads * sizeof(unsigned), st);
-    // the parity layer's data hand-offs: every word back to the sentinel
-    if (e->xl_x16) hipMemsetAsync(e->xl_x16, 0xff, (size_t)3 * 16 * e->c.hidden * sizeof(bf16_t), st);
     hipStreamSynchronize(st);
     return T5G_EHANDOFF;
 }

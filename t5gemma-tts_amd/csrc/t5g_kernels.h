@@ -173,12 +173,7 @@ struct XLayerArgs {
     unsigned* sync;             // this launch's XL_SET_LINES counter lines (zero when it starts)
     unsigned* sync_next;        // the next launch's set: zeroed by this launch
     unsigned* timeout;          // sticky timeout word (fused.hip's)
-    // the three norms' X16 outputs read by Q, G and QKV, handed off by their data (round 6):
-    // every word of a row is XL_X16_SENT until its norm writes it, and is reset to it once
-    // this launch's readers are done (dedicated buffers [16][hidden], XL_X16_SENT at start)
-    bf16_t *x16n1, *x16n2, *x16n3;
 };
-constexpr uint32_t XL_X16_SENT = 0xffffffffu;   // two bf16 NaNs with every payload bit set: no norm writes it
 constexpr int XL_SET_LINES = 56, XL_SET_WORDS = XL_SET_LINES * FM_LINE;
 int xlayer_launch(const XLayerArgs& a, hipStream_t st);   // -1: not built for these args / this device
 

@@ -125,41 +125,6 @@ __device__ __forceinline__ void xl_publish(unsigned* set, int line, unsigned n) 
     if (threadIdx.x == 0 && n) __hip_atomic_fetch_add(xline(set, line), n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t xl_rsrc(const void* base, uint32_t bytes);
-// a norm -> GEMV hand-off by its data: wave 0 polls the last X16 word of each of the M rows
-// (lane m: row m; lane 63: the timeout word) until none is XL_X16_SENT any more, then the
-// workgroup meets; the X window load verifies every word (xl_fill_x)
-__device__ __forceinline__ void xl_wait_x16(const bf16_t* x16, int M, unsigned* tmo, unsigned code) {
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        const __amdgpu_buffer_rsrc_t xr = xl_rsrc(x16, 16u * XL_D * 2u);
-        const int off = (int)(x16_off(min(lane, M - 1), XL_D - 2, XL_D / 32) * 2);
-        for (unsigned spins = 0;; ++spins) {
-            const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, XL_AUX_SC1);
-            const unsigned t = lane == 63 ? xl_ld_rlx(tmo) : 0u;
-            if (__ballot(lane < M && w == XL_X16_SENT) == 0ull) break;
-            if (__shfl(t, 63, 64) != 0) break;
-            if (spins > XL_SPIN_MAX) {
-                if (lane == 0) __hip_atomic_store(tmo, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    xl_barrier();
-}
-// a norm workgroup's row m of an X16 norm output back to the sentinel (the thread -> word map
-// of xl_norm_row's stores, so a later store of the same thread lands after it)
-__device__ __forceinline__ void xl_x16_reset(bf16_t* x16, int m) {
-    const int c = threadIdx.x;
-    if (8 * c >= XL_D) return;
-    const __amdgpu_buffer_rsrc_t xr = xl_rsrc(x16, 16u * XL_D * 2u);
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-        __builtin_amdgcn_raw_buffer_store_b32(XL_X16_SENT, xr, (int)(x16_off(m, 8 * c + 2 * jj, XL_D / 32) * 2), 0,
-                                              XL_AUX_SC1);
-}
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t xl_rsrc(const void* base, uint32_t bytes) {
     const uint64_t p = (uint64_t)base;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
@@ -190,9 +155,6 @@ struct XlGemv {
     __amdgpu_buffer_rsrc_t y, part;      // outputs (sc1 stores): Y [M][N] bf16 or Y16 / parts
     bool y16;                            // EPI_BF16: Y is row-major [M][N]; GEGLU: Y is the X16 act (K = N / 2)
     int xwin;                            // chunks of the X window staged in LDS (<= XL_XWIN)
-    bool verify = false;                 // X handed off by its data: reload words still XL_X16_SENT
-    unsigned* tmo = nullptr;             // (verify) the sticky timeout word, and the code to leave there
-    unsigned code = 0;
 };
 // the weights of one pass in registers: wave w holds chunks w, w + 8, ... (<= 9)
 struct XlW {
@@ -222,26 +184,6 @@ __device__ __forceinline__ void xl_fill_x(const XlGemv& s, int xb, u32x4* xs) {
         int off = (kb * 64 + (r >> 3) * 16 + (r & 7)) * 16;
         asm volatile("" : "+v"(off));
         v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(s.x, off, 0, XL_AUX_SC1));
-    }
-    if (s.verify) {
-        // the window's words of rows < M that are still the sentinel: not yet visible -- reload
-        // them (the stage's probe saw each row's last word, so this is the rare case)
-#pragma unroll
-        for (int u = 0; u < XL_XWIN * 32 / 512; ++u) {
-            const int i = min((int)threadIdx.x + u * 512, n - 1), kb = xb + (i >> 5), r = i & 31;
-            if ((r & 7) >= s.M) continue;
-            for (unsigned spins = 0; v[u][0] == XL_X16_SENT || v[u][1] == XL_X16_SENT || v[u][2] == XL_X16_SENT ||
-                                     v[u][3] == XL_X16_SENT;
-                 ++spins) {
-                if (spins > XL_SPIN_MAX) {
-                    __hip_atomic_store(s.tmo, s.code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                const int off = (kb * 64 + (r >> 3) * 16 + (r & 7)) * 16;
-                v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(s.x, off, 0, XL_AUX_SC1));
-            }
-        }
     }
 #pragma unroll
     for (int u = 0; u < XL_XWIN * 32 / 512; ++u) {
@@ -370,8 +312,7 @@ struct XlNoTs {
 // norms (hrow) and goes back to HBM at N3; xn goes out row-major (plain) and in X16 (sc1).
 template <int NS, typename Wait, typename Ts = XlNoTs>
 __device__ __forceinline__ void xl_norm_row(const XLayerArgs& a, int m, const bf16_t* post_w, const bf16_t* pre_w,
-                                            u32x4* hrow, bool first, bool last, float* sq, bf16_t* x16, Wait wait,
-                                            Ts ts = Ts()) {
+                                            u32x4* hrow, bool first, bool last, float* sq, Wait wait, Ts ts = Ts()) {
     const int d = XL_D, c = threadIdx.x;
     const bool active = 8 * c < d;
     const int cc = active ? c : d / 8 - 1;
@@ -440,7 +381,7 @@ __device__ __forceinline__ void xl_norm_row(const XLayerArgs& a, int m, const bf
 #pragma unroll
         for (int j = 0; j < 4; ++j) pk[j] = pack2(v[2 * j], v[2 * j + 1]);
         *(u32x4*)(a.xn + (long)m * d + 8 * c) = pk;   // row-major copy (not read in this launch)
-        const __amdgpu_buffer_rsrc_t xr = xl_rsrc(x16, (uint32_t)(16 * d * 2));
+        const __amdgpu_buffer_rsrc_t xr = xl_rsrc(a.xn16, (uint32_t)(16 * d * 2));
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
             __builtin_amdgcn_raw_buffer_store_b32(pk[jj], xr, (int)(x16_off(m, 8 * c + 2 * jj, d / 32) * 2), 0,
@@ -662,12 +603,10 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
         xl_publish(set, XC_O1 + (bu & 7), 1u);
         XL_TS(1);
     }
-    // ---- N1 (norm workgroups); first, N3's X16 row back to the sentinel (its readers, the
-    // previous launch's QKV, are done)
+    // ---- N1 (norm workgroups)
     if (normwg) {
-        if constexpr (HAS_QKV) xl_x16_reset(a.x16n3, nrow);
         xl_norm_row<0>(
-            a, nrow, a.n1_post, a.n1_pre, hrow, true, false, sq, a.x16n1,
+            a, nrow, a.n1_post, a.n1_pre, hrow, true, false, sq,
             [&] {
                 xl_wait_wg<8>(set, XC_O1, (unsigned)(d / 16), tmo, 21u);
                 XL_TS(19);
@@ -679,11 +618,11 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     // ---- Q: cross-q (128 groups); published per kv head (32 groups: its two q heads)
     if (bu < XL_QD / 16) {
         static_assert(XL_DOWN_KBC % 2 == 0 && XL_DOWN_KBC / 2 <= XL_SC, "down passes");
-        const XlGemv s{a.Wq, d / 32, xl_rsrc(a.x16n1, 16u * d * 2u), XL_QD, M, xl_rsrc(a.q, (uint32_t)(M * XL_QD * 2)),
-                       xl_rsrc(nullptr, 0u), false, d / 32, true, tmo, 22u};
+        const XlGemv s{a.Wq, d / 32, xl_rsrc(a.xn16, 16u * d * 2u), XL_QD, M, xl_rsrc(a.q, (uint32_t)(M * XL_QD * 2)),
+                       xl_rsrc(nullptr, 0u), false, d / 32};
         xl_gemv<EPI_BF16, false>(s, bu, bu + 1, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
                                  [&] {
-                                     xl_wait_x16(a.x16n1, M, tmo, 22u);   // N1's rows, by their data
+                                     xl_wait_wg<1>(set, XC_N1, (unsigned)M, tmo, 22u);
                                      XL_TS(3);
                                  });
         xl_publish(set, XC_Q + bu / 32, 1u);
@@ -722,9 +661,8 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     }
     // ---- N2
     if (normwg) {
-        xl_norm_row<0>(a, nrow, a.n2_post, a.n2_pre, hrow, false, false, sq, a.x16n2, [&] {
+        xl_norm_row<0>(a, nrow, a.n2_post, a.n2_pre, hrow, false, false, sq, [&] {
             xl_wait_wg<8>(set, XC_O, (unsigned)(d / 16), tmo, 25u);
-            xl_x16_reset(a.x16n1, nrow);   // O is done, so A and Q -- N1's readers -- are
             XL_TS(9);
         });
         xl_publish(set, XC_N2, 1u);
@@ -737,8 +675,8 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     const XlGdRuns gd = xl_gd_runs(ngu, ntd, nw, bu);
     if (!normwg) {
         const int ngt = gd.n0 + gd.n1;
-        const XlGemv s{a.Wgu, d / 32, xl_rsrc(a.x16n2, 16u * d * 2u), 2 * XL_F, M, xl_rsrc(a.act16, 16u * XL_F * 2u),
-                       xl_rsrc(nullptr, 0u), true, d / 32, true, tmo, 26u};
+        const XlGemv s{a.Wgu, d / 32, xl_rsrc(a.xn16, 16u * d * 2u), 2 * XL_F, M, xl_rsrc(a.act16, 16u * XL_F * 2u),
+                       xl_rsrc(nullptr, 0u), true, d / 32};
         // part 0's arrivals are published as soon as the worker's part-0 tasks are stored (the
         // down tasks of part 0 wait on those only), part 1's at the end
         const bool early0 = gd.n1 > 0;
@@ -747,7 +685,7 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
             [&](int i) { return XlTask{i < gd.n0 ? gd.g0_lo + i : gd.g1_lo + (i - gd.n0), 0, d / 32, 0, 0, true, true}; },
             gl,
                                   [&] {
-                                      xl_wait_x16(a.x16n2, M, tmo, 26u);   // N2's rows, by their data
+                                      xl_wait_wg<1>(set, XC_N2, (unsigned)M, tmo, 26u);
                                       XL_TS(11);
                                   },
                                   [&](int i) {
@@ -796,10 +734,8 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     }
     // ---- N3: from the parts; h back to HBM
     if (normwg) {
-        // the last launch's N3 feeds the head, which reads the engine's own X16 rows
-        xl_norm_row<2>(a, nrow, a.n3_post, a.n3_pre, hrow, false, true, sq, HAS_QKV ? a.x16n3 : a.xn16, [&] {
+        xl_norm_row<2>(a, nrow, a.n3_post, a.n3_pre, hrow, false, true, sq, [&] {
             xl_wait_wg<8>(set, XC_D, (unsigned)ntd, tmo, 29u);
-            xl_x16_reset(a.x16n2, nrow);   // D is done, so G -- N2's reader -- is
             XL_TS(15);
         });
         xl_publish(set, XC_N3, 1u);
@@ -809,11 +745,11 @@ __global__ __launch_bounds__(XL_NW * 64) void xlayer_kernel(XLayerArgs a) {
     if constexpr (HAS_QKV) {
         int lo, hi;
         xl_run(a.qkv_dim / 16, nb, bu, lo, hi);
-        const XlGemv s{a.Wqkv, d / 32, xl_rsrc(a.x16n3, 16u * d * 2u), a.qkv_dim, M,
-                       xl_rsrc(a.qkv, (uint32_t)(M * a.qkv_dim * 2)), xl_rsrc(nullptr, 0u), false, d / 32, true, tmo, 30u};
+        const XlGemv s{a.Wqkv, d / 32, xl_rsrc(a.xn16, 16u * d * 2u), a.qkv_dim, M,
+                       xl_rsrc(a.qkv, (uint32_t)(M * a.qkv_dim * 2)), xl_rsrc(nullptr, 0u), false, d / 32};
         xl_gemv<EPI_BF16, false>(s, lo, hi, [&](int g) { return XlTask{g, 0, d / 32, 0, 0, true, true}; }, gl,
                                  [&] {
-                                     xl_wait_x16(a.x16n3, M, tmo, 30u);   // N3's rows, by their data
+                                     xl_wait_wg<1>(set, XC_N3, (unsigned)M, tmo, 30u);
                                      XL_TS(17);
                                  });
         XL_TS(18);
