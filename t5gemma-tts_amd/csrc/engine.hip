@@ -130,7 +130,6 @@ struct t5g_engine {
     bf16_t *head1_x = nullptr, *head2_x = nullptr;
     bf16_t *xn16 = nullptr, *att16 = nullptr, *act16 = nullptr, *mem16 = nullptr;   // packed tokens
     bf16_t *dxn16 = nullptr, *datt16 = nullptr, *dact16 = nullptr, *dhh16 = nullptr;   // decode rows
-    unsigned* xa_sync = nullptr;   // parity decode attention: one counter set per decoder layer (xattn.hip)
     float* dpart = nullptr;   // decode down projection: fp32 K-part values [4][B16][hidden]
     uint32_t* trig_exc = nullptr;   // parity mode: RoPE cos / sin exceptions (t5g_engine_set_rope_exc)
     int n_trig_exc = 0;
@@ -438,7 +437,6 @@ struct XattnFuse {
     int ld_new = 0, k_col0 = 0, v_col0 = 0;
     int ldq = 0;   // row stride of Q when it is not q_dim (the q | k | v buffer)
     int span_max = 0;   // host bound on every row's keys (0: cap)
-    int layer = -1;     // decode: the decoder layer (its counter set: scores + P.V as one launch)
 };
 static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const int* q_pos, const int* q_len,
                  const bf16_t* K, const bf16_t* Vc, int cap, const int* kv_len, int causal, int window, bf16_t* O,
@@ -473,13 +471,6 @@ static int xattn(t5g_engine* e, const bf16_t* Q, int Mq, const int* q_row, const
     a.k_col0 = fr.k_col0;
     a.v_col0 = fr.v_col0;
     a.span_max = fr.span_max;
-    if (fr.layer >= 0 && e->xa_sync && !q_pos && !q_len) {   // decode: scores + P.V as one launch
-        const long w = xd_sync_words(c.max_batch, c.n_kv_heads);
-        a.xsync = e->xa_sync + w * fr.layer;
-        a.xsync_next = e->xa_sync + w * ((fr.layer + 1) % c.n_dec_layers);
-        a.xtmo = e->fsync;
-        a.xsync_n = c.max_batch * c.n_kv_heads;
-    }
     if (c.softcap > 0.f) {
         // eager attention (eager.hip): decode rows on the engine's scores scratch, packed
         // (prefill / encoder) calls on a stream-ordered one (not inside a captured graph)
@@ -738,7 +729,6 @@ static int decoder_pass_exact(t5g_engine* e, int M, const int* ids, const int* t
             fr.rope_tab = e->rope_tab;
             fr.kv_new = e->qkv;
             fr.span_max = e->audio_max;   // the call's key bound (0: max_audio)
-            fr.layer = l;
             fr.ld_new = e->qkv_dim;
             fr.k_col0 = e->q_dim;
             fr.v_col0 = e->q_dim + e->kv_dim;
@@ -884,8 +874,6 @@ static int xmm_prepare(t5g_engine* e) {
     RC(alloc(e, &e->act16, T16 * f));
     RC(alloc(e, &e->mem16, X16T * d));
     RC(alloc(e, &e->dxn16, B16 * d));
-    RC(alloc(e, &e->xa_sync, (int64_t)c.n_dec_layers * xd_sync_words(c.max_batch, c.n_kv_heads)));
-    HIPCHK(hipMemset(e->xa_sync, 0, (size_t)c.n_dec_layers * xd_sync_words(c.max_batch, c.n_kv_heads) * 4));
     RC(alloc(e, &e->datt16, B16 * e->q_dim));
     RC(alloc(e, &e->dact16, B16 * f));
     RC(alloc(e, &e->dhh16, B16 * d));
@@ -1754,9 +1742,6 @@ static int check_handoff(t5g_engine* e, hipStream_t st) {
     // the flash / stage-S arrival tickets are zero between launches; a launch that gave up
     // (or left chunks uncovered) can leave them counting, so they are cleared with the counters
     hipMemsetAsync(e->aftick, 0, (size_t)e->c.max_batch * e->c.n_kv_heads * sizeof(unsigned), st);
-    // the parity decode attention's counter sets (a launch that gave up leaves them counting)
-    if (e->xa_sync)
-        hipMemsetAsync(e->xa_sync, 0, (size_t)e->c.n_dec_layers * xd_sync_words(e->c.max_batch, e->c.n_kv_heads) * 4, st);
     hipStreamSynchronize(st);
     return T5G_EHANDOFF;
 }
@@ -2538,19 +2523,11 @@ extern "C" int t5g_exact_attention(const void* q, int32_t Mq, const int32_t* q_r
         hipStream_t st = (hipStream_t)stream;
         const int G = n_heads / n_kv_heads, nsplit = (cap + 63) / 64;
         float *sb = nullptr, *mb = nullptr;
-        unsigned* xs = nullptr;   // the one-launch form's two counter sets (the engine's decode form)
-        const long xw = xd_sync_words(Mq, n_kv_heads);
         HIPCHK(hipMallocAsync((void**)&sb, (size_t)Mq * n_heads * cap * 4, st));
         HIPCHK(hipMallocAsync((void**)&mb, (size_t)Mq * n_kv_heads * nsplit * G * 4, st));
-        HIPCHK(hipMallocAsync((void**)&xs, (size_t)2 * xw * 4, st));
-        HIPCHK(hipMemsetAsync(xs, 0, (size_t)2 * xw * 4, st));
-        a.xsync = xs;
-        a.xsync_next = xs + xw;
-        a.xsync_n = Mq * n_kv_heads;
         const int rc = exact_attention_decode(a, sb, mb, cap, st);
         hipFreeAsync(sb, st);
         hipFreeAsync(mb, st);
-        hipFreeAsync(xs, st);
         RC(rc);
         return T5G_OK;
     }

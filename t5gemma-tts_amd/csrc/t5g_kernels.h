@@ -370,16 +370,7 @@ struct ExactAttnArgs {
                               // kv_new runs the one-launch form (xattn_single_kernel)
     float softcap;            // eager attention (eager.hip): > 0 the tanh logit softcap
     const uint16_t* tanh_lut; // eager: the reference host's bf16 tanh [65536]
-    // decode scores + P.V as ONE launch (xattn.hip xattn_fused_kernel) when set: this launch's
-    // counter set (a ticket word, then one XD_LINE line per (row, kv head)), zero at start,
-    // and the next launch's, zeroed by this one; xtmo: the sticky timeout word (optional)
-    unsigned* xsync;
-    unsigned* xsync_next;
-    unsigned* xtmo;
-    int xsync_n;              // (row, kv head) lines per set (>= Mq x Hkv; all zeroed for the next launch)
 };
-constexpr int XD_LINE = 32;   // words per counter line (128 B)
-inline long xd_sync_words(int Mq, int Hkv) { return (long)(1 + Mq * Hkv) * XD_LINE; }
 int exact_attention(const ExactAttnArgs& a, hipStream_t st);
 // decode (one query per row, at its last key): scores + P.V launches (xattn.hip) on the
 // scratch sbuf [Mq][Hq][cap] / mbuf [Mq][Hkv][ceil(cap / 64)][G]

@@ -26,7 +26,6 @@ namespace t5g {
 
 constexpr int XD_CH = 64;    // keys per scores workgroup
 constexpr int XD_DZ = 32;    // output dims per P.V workgroup
-constexpr int XD_AUX_SC1 = 16;   // buffer-op aux: write-through stores / coherent loads (in-launch hand-offs)
 
 // keys [lo, hi) of a decode query (the sdpa call's keys: a sliding-window layer whose
 // cache is at least `window` long sees its last `window` keys, DynamicSlidingWindowLayer)
@@ -43,29 +42,19 @@ __device__ __forceinline__ void xd_range(const ExactAttnArgs& a, int row, int& l
 // chains them over the chunks; the hadd tree (l2 + l2 ^ 8, adjacent pairs, pairs, last
 // pair) then takes two exchanges inside the quad -- the oneDNN gemv's adds in its order.
 template <int G, int XD_D, bool FUSE>
-struct XdScoresLds {
-    float qs[G][XD_D];
-    uint32_t knew[FUSE ? XD_D / 2 : 1];   // the rotated new key as bf16 pairs
-    float wmax[4][G];
-};
-// INL: scores and P.V in ONE launch (xattn_fused_kernel): this task's writes that the P.V
-// tasks of the same launch read -- the scores, the chunk maxima, the appended key / value --
-// go out write-through (sc1); the caller then drains and publishes. Returns false when the
-// chunk lies past the row (nothing written).
-template <int G, int XD_D, bool FUSE, bool INL>
-__device__ __forceinline__ bool xd_scores_task(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap, int nsplit,
-                                               int qi, int kvh, int ch, XdScoresLds<G, XD_D, FUSE>& L) {
+__global__ __launch_bounds__(256) void xattn_scores_kernel(ExactAttnArgs a, float* sbuf, float* mbuf, int cap,
+                                                           int nsplit) {
     constexpr int H2 = XD_D / 2, NCB = XD_D / 32;
-    auto& qs = L.qs;
-    auto& knew = L.knew;
-    auto& wmax = L.wmax;
-    const int tid = threadIdx.x;
+    __shared__ float qs[G][XD_D];
+    __shared__ uint32_t knew[FUSE ? XD_D / 2 : 1];   // the rotated new key as bf16 pairs
+    __shared__ float wmax[4][G];
+    const int qi = blockIdx.x, kvh = blockIdx.y, ch = blockIdx.z, tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6, kl = tid >> 2, qa = tid & 3;
     const int row = a.q_row ? a.q_row[qi] : qi;
     int lo, hi;
     xd_range(a, row, lo, hi);
     const int c0 = lo + ch * XD_CH;
-    if (c0 >= hi) return false;
+    if (c0 >= hi) return;
     const int key = c0 + kl;
     const bool valid = key < hi;
     const bf16_t* kr = a.K + row * a.kv_bstride + kvh * a.kv_hstride + (long)(valid ? key : c0) * XD_D + 8 * qa;
@@ -91,24 +80,15 @@ __device__ __forceinline__ bool xd_scores_task(const ExactAttnArgs& a, float* sb
             const bf16_t* vn = a.kv_new + (long)qi * a.ld_new + a.v_col0 + kvh * XD_D;
             bf16_t* kc = (bf16_t*)a.K + row * a.kv_bstride + kvh * a.kv_hstride + slot * XD_D;
             bf16_t* vc = (bf16_t*)a.V + row * a.kv_bstride + kvh * a.kv_hstride + slot * XD_D;
-            const __amdgpu_buffer_rsrc_t kcr = frag_rsrc(kc, XD_D * 2u), vcr = frag_rsrc(vc, XD_D * 2u);
             for (int d = tid; d < H2; d += 256) {
                 float o1, o2;
                 xd_rope(bf2f(kn[d]), bf2f(kn[d + H2]), tab[d], tab[H2 + d], o1, o2);
-                if constexpr (INL) {
-                    __builtin_amdgcn_raw_buffer_store_b16(f2bf(o1), kcr, d * 2, 0, XD_AUX_SC1);
-                    __builtin_amdgcn_raw_buffer_store_b16(f2bf(o2), kcr, (d + H2) * 2, 0, XD_AUX_SC1);
-                } else {
-                    kc[d] = f2bf(o1);
-                    kc[d + H2] = f2bf(o2);
-                }
+                kc[d] = f2bf(o1);
+                kc[d + H2] = f2bf(o2);
                 ((bf16_t*)knew)[d] = f2bf(o1);
                 ((bf16_t*)knew)[d + H2] = f2bf(o2);
             }
-            for (int d = tid; d < XD_D; d += 256) {
-                if constexpr (INL) __builtin_amdgcn_raw_buffer_store_b16(vn[d], vcr, d * 2, 0, XD_AUX_SC1);
-                else vc[d] = vn[d];
-            }
+            for (int d = tid; d < XD_D; d += 256) vc[d] = vn[d];
         }
         __syncthreads();
         if (has_new && key == hi - 1) {
@@ -151,29 +131,14 @@ __device__ __forceinline__ bool xd_scores_task(const ExactAttnArgs& a, float* sb
     for (int g = 0; g < G; ++g) {
         const bool own = valid && qa == 0;
         const float s = own ? sc[g] : -INFINITY;
-        if (own) {
-            float* sp = &sbuf[((long)qi * a.Hq + kvh * G + g) * cap + (key - lo)];
-            if constexpr (INL) st_sc1(sp, s);
-            else *sp = s;
-        }
+        if (own) sbuf[((long)qi * a.Hq + kvh * G + g) * cap + (key - lo)] = s;
         const float mx = wave_max(s);
         if (lane == 0) wmax[wave][g] = mx;
     }
     __syncthreads();
-    if (tid < G) {
-        float* mp = &mbuf[(((long)qi * a.Hkv + kvh) * nsplit + ch) * G + tid];
-        const float m = fmaxf(fmaxf(wmax[0][tid], wmax[1][tid]), fmaxf(wmax[2][tid], wmax[3][tid]));
-        if constexpr (INL) st_sc1(mp, m);
-        else *mp = m;
-    }
-    return true;
-}
-
-template <int G, int XD_D, bool FUSE>
-__global__ __launch_bounds__(256) void xattn_scores_kernel(ExactAttnArgs a, float* sbuf, float* mbuf, int cap,
-                                                           int nsplit) {
-    __shared__ XdScoresLds<G, XD_D, FUSE> L;
-    (void)xd_scores_task<G, XD_D, FUSE, false>(a, sbuf, mbuf, cap, nsplit, blockIdx.x, blockIdx.y, blockIdx.z, L);
+    if (tid < G)
+        mbuf[(((long)qi * a.Hkv + kvh) * nsplit + ch) * G + tid] =
+            fmaxf(fmaxf(wmax[0][tid], wmax[1][tid]), fmaxf(wmax[2][tid], wmax[3][tid]));
 }
 
 // Round 6 schedule (the same operations in the same order as round 5's, bitwise): every
@@ -184,38 +149,25 @@ __global__ __launch_bounds__(256) void xattn_scores_kernel(ExactAttnArgs a, floa
 // 16-byte words: lane (group gl = tid / 4 of the block, 8-dimension slice tid % 4) holds
 // the 8 keys of its group, 4x fewer load instructions than 4-byte words. Blocks past the
 // second load at the top of their own iteration.
-template <int G>
-struct XdPvLds {
-    float pex[G][SDPA_KV_BLOCK + 16];            // exact p (block sums)
-    float pbf[G][SDPA_KV_BLOCK];                 // bf16-rounded p (P.V)
-    float tmp[SDPA_KV_BLOCK / 8][G][XD_DZ];      // group chain sums of the block
-    float mrun[G][SDPA_MAX_BLOCKS];
-    float et_s[G], l_s[G];
-};
-// INL (xattn_fused_kernel): `wait` returns once this (row, kv head)'s scores tasks of the
-// same launch have all published; the chunk maxima and scores are read after it (sc1), the
-// V rows before it -- except the row's new key, appended by a scores task of this launch,
-// which is read again after the wait.
-template <int G, int XD_D, bool INL, typename Wait>
-__device__ __forceinline__ void xd_pv_task(const ExactAttnArgs& a, const float* sbuf, const float* mbuf, int cap,
-                                           int nsplit, int qi, int kvh, int z, XdPvLds<G>& Ls, Wait wait) {
+template <int G, int XD_D>
+__global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const float* sbuf, const float* mbuf,
+                                                       int cap, int nsplit) {
     constexpr int BLK = SDPA_KV_BLOCK;           // 512
     constexpr int NGRP = BLK / 8;                // 8-key groups per block (64: one per lane quad)
     constexpr int PPT = BLK / 256;               // block positions per thread (2)
     static_assert(NGRP * 4 == 256 && XD_DZ == 32, "lane map: 64 groups x 4 eight-dimension slices");
-    auto& pex = Ls.pex;
-    auto& pbf = Ls.pbf;
-    auto& tmp = Ls.tmp;
-    auto& mrun = Ls.mrun;
-    auto& et_s = Ls.et_s;
-    auto& l_s = Ls.l_s;
-    const int tid = threadIdx.x;
+    __shared__ float pex[G][BLK + 16];           // exact p (block sums)
+    __shared__ float pbf[G][BLK];                // bf16-rounded p (P.V)
+    __shared__ float tmp[NGRP][G][XD_DZ];        // group chain sums of the block
+    __shared__ float mrun[G][SDPA_MAX_BLOCKS];
+    __shared__ float et_s[G], l_s[G];
+    const int qi = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int row = a.q_row ? a.q_row[qi] : qi;
     int lo, hi;
     xd_range(a, row, lo, hi);
     const int span = max(hi - lo, 0);
-    if (span == 0) return;   // (uniform: no scores task of the row wrote anything either)
+    if (span == 0) return;
     const int nch = (span + XD_CH - 1) / XD_CH;
     const int nblk = (span + BLK - 1) / BLK;
     const float* sb = sbuf + ((long)qi * a.Hq + kvh * G) * cap;
@@ -226,13 +178,8 @@ __device__ __forceinline__ void xd_pv_task(const ExactAttnArgs& a, const float* 
     const int gm = wave < G ? wave : G - 1;
     float cmx[(SDPA_MAX_BLOCKS * (BLK / XD_CH) + 63) / 64];
     constexpr int NCM = (SDPA_MAX_BLOCKS * (BLK / XD_CH) + 63) / 64;
-    auto mload = [&]() {
 #pragma unroll
-        for (int i = 0; i < NCM; ++i) {
-            const float* p = &mb_row[min(lane + 64 * i, nch - 1) * G + gm];
-            cmx[i] = INL ? ld_sc1(p) : *p;
-        }
-    };
+    for (int i = 0; i < NCM; ++i) cmx[i] = mb_row[min(lane + 64 * i, nch - 1) * G + gm];
     auto vload = [&](u32x4 (&v)[8], int b) {
         const int bs = b * BLK, blen = min(BLK, span - bs);
 #pragma unroll
@@ -243,36 +190,15 @@ __device__ __forceinline__ void xd_pv_task(const ExactAttnArgs& a, const float* 
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int i = 0; i < PPT; ++i) {
-                const float* p = &sb[(long)g * cap + bs + min(tid + 256 * i, blen - 1)];
-                sv[g][i] = INL ? ld_sc1(p) : *p;
-            }
-    };
-    // INL: the row's new key (span - 1), appended by a scores task of this launch, read again
-    // after the wait, coherently, by the lanes holding it in block b's words
-    auto fix_new = [&](u32x4 (&v)[8], int b) {
-        if (!INL || !a.kv_new) return;
-        const int kn = span - 1, r = kn - b * BLK;
-        if (r < 0 || r >= BLK || r / 8 != gl) return;
-        const __amdgpu_buffer_rsrc_t vr = frag_rsrc(Vb + (long)kn * XD_D, XD_DZ * 2u);
-        v[r % 8] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vr, 16 * d8, 0, XD_AUX_SC1));
+            for (int i = 0; i < PPT; ++i) sv[g][i] = sb[(long)g * cap + bs + min(tid + 256 * i, blen - 1)];
     };
     u32x4 v0[8], v1[8];
     float s0[G][PPT], s1[G][PPT];
     const int b1 = min(1, nblk - 1);
-    if constexpr (!INL) mload();
     vload(v0, 0);
-    if constexpr (!INL) sload(s0, 0);
+    sload(s0, 0);
     vload(v1, b1);
-    if constexpr (!INL) sload(s1, b1);
-    if constexpr (INL) {
-        wait();
-        mload();
-        sload(s0, 0);
-        sload(s1, b1);
-        fix_new(v0, 0);
-        if (nblk > 1) fix_new(v1, 1);
-    }
+    sload(s1, b1);
     if (wave < G) {   // running max through each block, from the chunk maxima
         const int g = wave;
         float run = -INFINITY;
@@ -312,7 +238,6 @@ __device__ __forceinline__ void xd_pv_task(const ExactAttnArgs& a, const float* 
                 for (int i = 0; i < PPT; ++i) sv[g][i] = s1[g][i];
         } else {
             vload(vb, b);
-            fix_new(vb, b);
             sload(sv, b);
         }
         // exact p of the block's keys
@@ -394,72 +319,6 @@ __device__ __forceinline__ void xd_pv_task(const ExactAttnArgs& a, const float* 
         a.O[(long)qi * a.ldo + col] = o;
         if (a.O16) a.O16[x16_off(qi, col, a.ldo / 32)] = o;
     }
-}
-
-template <int G, int XD_D>
-__global__ __launch_bounds__(256) void xattn_pv_kernel(ExactAttnArgs a, const float* sbuf, const float* mbuf,
-                                                       int cap, int nsplit) {
-    __shared__ XdPvLds<G> L;
-    xd_pv_task<G, XD_D, false>(a, sbuf, mbuf, cap, nsplit, blockIdx.x, blockIdx.y, blockIdx.z, L, [] {});
-}
-
-// Round 6: scores and P.V as ONE launch. Every workgroup takes a ticket; the first
-// Mq x Hkv x nsplit tickets are the scores tasks (the scores launch's grid order), the rest
-// the P.V tasks. A scores task publishes one arrival on its (row, kv head)'s counter line
-// (also when its chunk lies past the row); a P.V task requests its V rows, waits for that
-// counter to reach nsplit, then reads the scores and chunk maxima. Every scores ticket is
-// taken before any P.V ticket, by a workgroup that waits on nothing, so the waits always
-// end. The counter set is this launch's (xsync); the launch zeroes the next one
-// (xsync_next), whose last user finished before this launch started. Same operations in the
-// same order as the two launches: bitwise.
-template <int G, int XD_D, bool FUSE>
-__global__ __launch_bounds__(256) void xattn_fused_kernel(ExactAttnArgs a, float* sbuf, float* mbuf, int cap,
-                                                          int nsplit) {
-    __shared__ union {
-        XdScoresLds<G, XD_D, FUSE> s;
-        XdPvLds<G> p;
-    } L;
-    __shared__ int ticket;
-    const int tid = threadIdx.x;
-    const int nS = a.Mq * a.Hkv * nsplit, nQK = a.Mq * a.Hkv;
-    if (tid == 0) {
-        const int t = (int)__hip_atomic_fetch_add(a.xsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ticket = t;
-        if (t == 0) {   // the next launch's set
-            __hip_atomic_store(a.xsync_next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int i = 0; i < max(a.xsync_n, nQK); ++i)
-                __hip_atomic_store(a.xsync_next + (1 + i) * XD_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    __syncthreads();
-    const int t = ticket;
-    if (t < nS) {
-        const int qi = t % a.Mq, kvh = (t / a.Mq) % a.Hkv, ch = t / nQK;
-        (void)xd_scores_task<G, XD_D, FUSE, true>(a, sbuf, mbuf, cap, nsplit, qi, kvh, ch, L.s);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores
-        __syncthreads();
-        if (tid == 0)
-            __hip_atomic_fetch_add(a.xsync + (1 + qi * a.Hkv + kvh) * XD_LINE, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    const int u = t - nS;
-    const int qi = u % a.Mq, kvh = (u / a.Mq) % a.Hkv, z = u / nQK;
-    unsigned* ctr = a.xsync + (1 + qi * a.Hkv + kvh) * XD_LINE;
-    xd_pv_task<G, XD_D, true>(a, sbuf, mbuf, cap, nsplit, qi, kvh, z, L.p, [&] {
-        if (tid < 64) {
-            for (unsigned spins = 0;; ++spins) {
-                if (ld_sc1(ctr) >= (unsigned)nsplit) break;
-                if (spins > (1u << 20)) {   // not reachable unless a scores task never ran
-                    if (tid == 0 && a.xtmo)
-                        __hip_atomic_store(a.xtmo, 40u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        __syncthreads();
-    });
 }
 
 // Rows of one 64-key chunk (cap <= 64: the PM cross attention over the text keys) in ONE
@@ -612,12 +471,6 @@ static void launch_xd(const ExactAttnArgs& a, float* sbuf, float* mbuf, int cap,
     if (span_max <= XD_CH && !a.kv_new) {   // one chunk per row, nothing appended: one launch
         if (a.rope_tab) hipLaunchKernelGGL((xattn_single_kernel<G, D, true>), gp, dim3(256), 0, st, a);
         else hipLaunchKernelGGL((xattn_single_kernel<G, D, false>), gp, dim3(256), 0, st, a);
-        return;
-    }
-    if (a.xsync) {   // one launch (xattn_fused_kernel): scores tickets, then P.V tickets
-        const unsigned nt = (unsigned)(a.Mq * a.Hkv * (nsplit + D / XD_DZ));
-        if (a.rope_tab) hipLaunchKernelGGL((xattn_fused_kernel<G, D, true>), dim3(nt), dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
-        else hipLaunchKernelGGL((xattn_fused_kernel<G, D, false>), dim3(nt), dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
         return;
     }
     if (a.rope_tab) hipLaunchKernelGGL((xattn_scores_kernel<G, D, true>), gs, dim3(256), 0, st, a, sbuf, mbuf, cap, nsplit);
