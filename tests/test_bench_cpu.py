@@ -18,7 +18,7 @@ def test_workloads_cover_baseline_configs():
         assert e2e == ("decoder" in desc and "RTF" in desc), (name, desc)
 
 
-@pytest.mark.parametrize("wl", ["c2", "c3", "c4", "c5"])
+@pytest.mark.parametrize("wl", ["c2", "c3", "c3p10", "c4", "c5"])
 def test_make_batch_shapes(wl):
     import bench
     from t5gemma_tts_amd.config import config_2b2b
@@ -68,3 +68,14 @@ def test_cpu_baseline_tiny():
     y = [1, 2, 3, cfg.y_sep_token]
     r = bench.cpu_baseline(cfg, sd, (x, y, len(y) + 20), 30)
     assert r["value"] > 0 and r["kind"] == "port" and "timed whole" in r["sample"]
+
+
+def test_c3p10_rows_pass_1024_keys():
+    """--workload c3p10 (round 6): C3's rows with a 10 s prompt (500 codes + y_sep), so every
+    row's keys pass 1 024 -- the stage-S range past one combine batch."""
+    import bench
+    b, tx, tp, e2e, idx = bench.WORKLOADS["c3p10"]
+    assert (b, tx, e2e, idx) == bench.WORKLOADS["c3"][:2] + (False, 2) and tp == 501
+    from t5gemma_tts_amd.config import config_2b2b
+    n_tok_row = bench.DUR_FRAMES + int(config_2b2b().extra_budget) + 1   # bench.py: tokens a row generates
+    assert 1 + tp + n_tok_row > 1024 >= 1 + bench.WORKLOADS["c3"][2] + n_tok_row
