@@ -65,6 +65,13 @@ def main():
                 continue
             d = (v - t0) * 0.01
             print(f"{k:2d} {NAMES[k]:20s} n={len(v):3d} min {d.min():7.2f} med {np.median(d):7.2f} max {d.max():7.2f} us")
+        if os.environ.get("FS_SLOW"):
+            # the workgroups that published att_self last: their own points 3-7 (and the ticket wait)
+            wg = np.nonzero(live)[0]
+            order = wg[np.argsort(ts[wg, 7])[::-1]][:int(os.environ["FS_SLOW"])]
+            for w in order:
+                pts = " ".join(f"{k}:{(ts[w, k] - t0) * 0.01:6.2f}" if ts[w, k] > 0 else f"{k}:   -  " for k in (19, 2, 3, 4, 5, 6, 7))
+                print(f"   wg {w:3d} (xcd {w % 8}) {pts}")
     assert L.t5g_dbg_set_fused_s(C.c_void_p(0)) == 0
     assert L.t5g_dbg_set_fused_s_var(0) == 0
 
