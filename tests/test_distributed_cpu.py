@@ -82,14 +82,14 @@ def _seed_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_bench_seeds_independent_of_sharding():
-    """A request samples with the same seed (and prompt) sharded over 2 ranks as in the
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_seeds_independent_of_sharding(world):
+    """A request samples with the same seed (and prompt) sharded over 2 or 8 ranks as in the
     unsharded batch: bench.py seeds by global request index (VERDICT r3 #7)."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     from t5gemma_tts_amd.config import config_2b2b
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -107,8 +107,10 @@ def test_bench_seeds_independent_of_sharding():
     assert len({o[0] for o in unsharded}) == len(unsharded)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_run_sharded_gloo(world):
+    """7 utterances over `world` gloo ranks (8: the driver's node size, one rank with an
+    empty shard): every rank ends with every utterance's output in request order."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
